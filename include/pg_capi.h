@@ -1,0 +1,239 @@
+/*
+ * pg_capi.h — the drop-in boundary of the MI355X guided path-tracing integrator.
+ *
+ * A thin C ABI (plain pointers, sizes and integer status codes; no C++ types, no exceptions)
+ * between a host integrator plugin and the HIP/gfx950 hot path.  It replaces the CPU side of
+ * the reference's progressive Monte-Carlo integrator for ONE job:
+ *
+ *   reference surface                                    replaced by
+ *   ------------------------------------------------------------------------------------------
+ *   Integrator::preprocess            include/mitsuba/render/integrator.h:61   pg_create + pg_upload_scene
+ *   ProgressiveMonteCarloIntegrator::render / renderSamples
+ *                                     src/librender/progressiveintegrator.cpp:65-114,170-220
+ *                                                                              pg_render_pass (one progression)
+ *   ProgressiveMonteCarloIntegrator::renderBlock (per-pixel sample loop, clamp, ImageBlock::put)
+ *                                     src/librender/progressiveintegrator.cpp:222-282   (inside pg_render_pass)
+ *   ProgressiveMIPathTracer::Li       src/integrators/path/progressive_path.cpp:133-314 (inside pg_render_pass)
+ *   ProgressiveMonteCarloIntegrator::postprogression (guiding refit slot)
+ *                                     src/librender/progressiveintegrator.cpp:314-317  pg_splat_* + pg_refit
+ *   Integrator::cancel                integrator.h:84; progressiveintegrator.cpp:319-326  pg_cancel
+ *   Film::develop / ImageBlock readback  src/librender/renderproc.cpp:142-149        pg_read_film
+ *   Integrator::postprocess           integrator.h:96                             pg_get_stats + pg_destroy
+ *
+ * Every function returns a pg_status; on failure pg_last_error() holds a message (the Mitsuba
+ * adapter turns it into Log(EError, ...), which throws: include/mitsuba/core/formatter.h:33).
+ * All host arrays passed in are caller-owned and copied; all device memory is owned by the
+ * context and released by pg_destroy.  One context per render job; calls come from one thread
+ * except pg_cancel, which may be called from any thread.
+ */
+#ifndef PG_CAPI_H
+#define PG_CAPI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PG_ABI_VERSION 1
+
+typedef int32_t pg_status;
+enum {
+    PG_OK = 0,
+    PG_ERR_INVALID = 1,    /* bad argument / inconsistent scene */
+    PG_ERR_HIP = 2,        /* HIP runtime error */
+    PG_ERR_OOM = 3,        /* device allocation failed */
+    PG_ERR_STATE = 4,      /* call out of order (e.g. render before upload) */
+    PG_ERR_CANCELLED = 5,  /* pg_cancel() was called */
+    PG_ERR_NO_DEVICE = 6   /* no gfx950 device visible */
+};
+
+/* BSDF models (reference: EBSDFModel, include/mitsuba/render/bsdf.h:287-297; plugins in src/bsdfs/). */
+enum {
+    PG_BSDF_DIFFUSE = 0,          /* src/bsdfs/diffuse.cpp          */
+    PG_BSDF_CONDUCTOR = 1,        /* src/bsdfs/conductor.cpp        */
+    PG_BSDF_ROUGHCONDUCTOR = 2,   /* src/bsdfs/roughconductor.cpp   */
+    PG_BSDF_DIELECTRIC = 3,       /* src/bsdfs/dielectric.cpp       */
+    PG_BSDF_ROUGHDIELECTRIC = 4,  /* src/bsdfs/roughdielectric.cpp  */
+    PG_BSDF_PLASTIC = 5,          /* src/bsdfs/plastic.cpp          */
+    PG_BSDF_COUNT = 6
+};
+/* Microfacet distributions (src/bsdfs/microfacet.h:48-58). */
+enum { PG_DIST_BECKMANN = 0, PG_DIST_GGX = 1 };
+/* Material flags. */
+#define PG_MAT_TWOSIDED 1u    /* wrap in the 'twosided' adapter (src/bsdfs/twosided.cpp) */
+#define PG_MAT_NONLINEAR 2u   /* plastic: 'nonlinear' (src/bsdfs/plastic.cpp) */
+#define PG_MAT_SAMPLE_ALL 4u  /* microfacet: sampleVisible=false (microfacet.h:112) */
+
+/* One material; 112 bytes.  Conductor eta/k are RGB and already divided by extEta
+ * (roughconductor.cpp:173-188).  Dielectric/plastic use int_ior/ext_ior. */
+typedef struct pg_material {
+    uint32_t type;
+    uint32_t distribution;
+    uint32_t flags;
+    uint32_t pad0;
+    float alpha_u, alpha_v;
+    float int_ior, ext_ior;
+    float diffuse_reflectance[4];    /* diffuse.reflectance, plastic.diffuseReflectance */
+    float specular_reflectance[4];
+    float specular_transmittance[4];
+    float eta[4];
+    float k[4];
+} pg_material;
+
+/* A shape = a contiguous triangle range with one BSDF and optionally one area emitter
+ * (reference: Shape/TriMesh + AreaLight, src/librender/trimesh.cpp, src/emitters/area.cpp). */
+typedef struct pg_shape {
+    uint32_t tri_begin;
+    uint32_t tri_count;
+    uint32_t material;
+    int32_t emitter; /* index into emitters, or -1 */
+} pg_shape;
+
+/* Area emitter attached to a shape (src/emitters/area.cpp:158-183).  Sampling weight 1, so the
+ * scene picks emitters uniformly (Scene::sampleEmitterDirect, src/librender/scene.cpp:871-895). */
+typedef struct pg_emitter {
+    uint32_t shape;
+    uint32_t pad[3];
+    float radiance[4];
+} pg_emitter;
+
+/* Pinhole camera with Mitsuba 'perspective' semantics (src/sensors/perspective.cpp:271-298,
+ * Transform::lookAt src/libcore/transform.cpp:191-214): fov along x, near/far clip. */
+typedef struct pg_camera {
+    float origin[3];
+    float target[3];
+    float up[3];
+    float fov_x_deg;
+    float near_clip;
+    float far_clip;
+    uint32_t width;
+    uint32_t height;
+} pg_camera;
+
+/* Flattened scene (what a Mitsuba adapter extracts from Scene::getShapes()/getBSDFs()/emitters). */
+typedef struct pg_scene_desc {
+    uint32_t num_vertices;
+    uint32_t num_triangles;
+    uint32_t num_shapes;
+    uint32_t num_materials;
+    uint32_t num_emitters;
+    uint32_t pad0;
+    const float *positions;     /* 3 * num_vertices */
+    const float *normals;       /* 3 * num_vertices, or NULL (face normals) */
+    const uint32_t *indices;    /* 3 * num_triangles */
+    const pg_shape *shapes;     /* shapes partition [0, num_triangles) */
+    const pg_material *materials;
+    const pg_emitter *emitters;
+    pg_camera camera;
+} pg_scene_desc;
+
+/* Integrator parameters (MonteCarloIntegrator props: src/librender/integrator.cpp:195-230;
+ * progressive: progressiveintegrator.cpp:296-300; useNee: progressive_path.cpp:117) plus the
+ * SD-tree guiding parameters (Mueller et al. 2017) and the device/shard placement. */
+typedef struct pg_config {
+    int32_t device;               /* HIP device ordinal used by this context */
+    int32_t max_depth;            /* -1 = unbounded (Mitsuba default) */
+    int32_t rr_depth;             /* 5 */
+    int32_t use_nee;              /* 1 */
+    int32_t hide_emitters;        /* 0 */
+    int32_t strict_normals;       /* 0 */
+    float max_component_value;    /* +inf */
+    uint32_t seed;                /* 1337 (deterministic.cpp salt) */
+    int32_t guiding;              /* 0 = plain progressive path tracer, 1 = SD-tree guided */
+    float bsdf_sampling_fraction; /* 0.5 */
+    float s_tree_threshold;       /* 12000 */
+    float d_tree_threshold;       /* 0.01 */
+    int32_t d_tree_max_depth;     /* 20 */
+    int32_t record_max_vertices;  /* 32: training-record vertices kept per path */
+    int32_t rank;                 /* image-tile shard of this context */
+    int32_t world_size;
+    uint32_t tile_size;           /* 32 (Scene::setBlockSize default) */
+    uint32_t max_paths_in_flight; /* 0 = auto */
+    int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024) */
+    int32_t pad0;
+} pg_config;
+
+/* Training record written per non-delta path vertex (SoA-free 32-byte AoS). */
+typedef struct pg_record {
+    float pos[3];
+    uint32_t dir;      /* canonical (cos theta, phi) square coords as 2 x u16 */
+    float radiance;    /* average incident radiance estimate along dir */
+    float wo_pdf;      /* pdf the direction was sampled with (one-sample MIS) */
+    float product;     /* radiance * bsdf average (reserved for product-driven loss) */
+    float weight;      /* statistical weight (1) */
+} pg_record;
+
+typedef struct pg_stats {
+    uint64_t paths;           /* camera paths traced since create */
+    uint64_t segments;        /* path segments (extension rays) */
+    uint64_t shadow_rays;
+    uint64_t records;         /* training records written */
+    double trace_ms;          /* device time of the closest-hit kernel */
+    double shade_ms;
+    double shadow_ms;
+    double other_ms;
+    uint64_t trace_launches;
+    uint64_t stree_nodes;
+    uint64_t dtree_nodes;
+} pg_stats;
+
+/* ---- lifecycle ---------------------------------------------------------------------- */
+pg_status pg_config_default(pg_config *cfg);
+pg_status pg_create(const pg_config *cfg, void **ctx_out);
+pg_status pg_destroy(void *ctx);
+const char *pg_last_error(void *ctx);
+int32_t pg_abi_version(void);
+pg_status pg_cancel(void *ctx); /* thread-safe */
+
+/* ---- scene ---------------------------------------------------------------------------- */
+pg_status pg_upload_scene(void *ctx, const pg_scene_desc *scene);
+
+/* ---- one progression (pass): spp samples per pixel of this rank's tiles,
+ *      sample indices [sample_offset, sample_offset + spp).  record != 0 writes training
+ *      records (only meaningful with guiding).  Accumulates into the film. ------------ */
+pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_t record);
+
+/* ---- training records / SD-tree refit (the postprogression slot) ------------------------ */
+pg_status pg_get_record_count(void *ctx, uint64_t *count);
+/* Copy local records out: dst is host memory unless dst_is_device != 0. */
+pg_status pg_get_records(void *ctx, void *dst, uint64_t max_records, int32_t dst_is_device, uint64_t *written);
+/* Splat records (e.g. the all-gathered set of every rank) into the building SD-tree. */
+pg_status pg_splat_records(void *ctx, const void *src, uint64_t count, int32_t src_is_device);
+/* Splat this context's own records (single-GPU case). */
+pg_status pg_splat_local_records(void *ctx);
+/* Build sampling trees from the building trees, refine the S-tree for training iteration
+ * `iteration`, reset the building trees; clears the local record buffer. */
+pg_status pg_refit(void *ctx, uint32_t iteration);
+/* Serialize / inject the SD-tree (golden-vector tests).  Query size with buf == NULL. */
+pg_status pg_get_sdtree(void *ctx, void *buf, uint64_t capacity, uint64_t *size);
+pg_status pg_put_sdtree(void *ctx, const void *buf, uint64_t size);
+/* Evaluate / sample the sampling SD-tree on the device for host arrays (parity tests). */
+pg_status pg_sdtree_pdf(void *ctx, const float *pos, const float *dir, uint64_t n, float *pdf_out);
+pg_status pg_sdtree_sample(void *ctx, const float *pos, const float *u, uint64_t n, float *dir_out, float *pdf_out);
+
+/* ---- film ------------------------------------------------------------------------------ */
+/* rgbw: width*height*4 floats (sum r,g,b, sample count); sumsq: width*height*4 (sum r^2,g^2,b^2,0).
+ * Pixels outside this rank's tiles are zero.  Either pointer may be NULL. */
+pg_status pg_read_film(void *ctx, float *rgbw, float *sumsq);
+pg_status pg_reset_film(void *ctx);
+pg_status pg_get_stats(void *ctx, pg_stats *stats);
+/* Number of pixels owned by this rank (tile shard). */
+pg_status pg_local_pixel_count(void *ctx, uint64_t *count);
+
+/* ---- unit-level device entry points used by the parity tests ---------------------------- */
+/* rays: n x 8 floats (o.xyz, tmin, d.xyz, tmax).  hits: n x 4 (t, prim as float bits, u, v);
+ * prim = 0xFFFFFFFF for a miss.  any_hit: hits[i*4] = 1 if occluded else 0. */
+pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hit, float *hits);
+/* BSDF queries on the device for material `material` of the uploaded scene.
+ * wi: n x 3 local; u: n x 3 (2D sample + component sample); out per query 12 floats:
+ * wo.xyz, pdf, weight.rgb, sampled_type, eval(wi,wo_given).rgb, pdf(wi,wo_given).
+ * wo_given: n x 3 local directions for the eval/pdf part (may be NULL). */
+pg_status pg_bsdf_query(void *ctx, uint32_t material, const float *wi, const float *u,
+                        const float *wo_given, uint64_t n, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PG_CAPI_H */

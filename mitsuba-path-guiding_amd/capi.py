@@ -1,0 +1,147 @@
+"""ctypes mirror of include/pg_capi.h (the C-ABI boundary).
+
+Struct layouts here must match the header byte for byte; tests/test_capi_abi.py checks the sizes
+against the compiled library.  This module only describes types and loads a library; it does no
+compute.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "libpgamd.so")
+
+PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, PG_ERR_NO_DEVICE = range(7)
+PG_BSDF_DIFFUSE, PG_BSDF_CONDUCTOR, PG_BSDF_ROUGHCONDUCTOR, PG_BSDF_DIELECTRIC, PG_BSDF_ROUGHDIELECTRIC, PG_BSDF_PLASTIC = range(6)
+PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
+PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
+
+# EBSDFType bits (include/mitsuba/render/bsdf.h:224-262)
+ENull, EDiffuseReflection, EDiffuseTransmission, EGlossyReflection = 0x1, 0x2, 0x4, 0x8
+EGlossyTransmission, EDeltaReflection, EDeltaTransmission = 0x10, 0x20, 0x40
+EFrontSide, EBackSide = 0x8000, 0x10000
+EDelta = EDeltaReflection | EDeltaTransmission
+ESmooth = EDiffuseReflection | EDiffuseTransmission | EGlossyReflection | EGlossyTransmission
+
+F4 = C.c_float * 4
+
+
+class pg_material(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("distribution", C.c_uint32), ("flags", C.c_uint32), ("pad0", C.c_uint32),
+                ("alpha_u", C.c_float), ("alpha_v", C.c_float), ("int_ior", C.c_float), ("ext_ior", C.c_float),
+                ("diffuse_reflectance", F4), ("specular_reflectance", F4), ("specular_transmittance", F4),
+                ("eta", F4), ("k", F4)]
+
+
+class pg_shape(C.Structure):
+    _fields_ = [("tri_begin", C.c_uint32), ("tri_count", C.c_uint32), ("material", C.c_uint32), ("emitter", C.c_int32)]
+
+
+class pg_emitter(C.Structure):
+    _fields_ = [("shape", C.c_uint32), ("pad", C.c_uint32 * 3), ("radiance", F4)]
+
+
+class pg_camera(C.Structure):
+    _fields_ = [("origin", C.c_float * 3), ("target", C.c_float * 3), ("up", C.c_float * 3),
+                ("fov_x_deg", C.c_float), ("near_clip", C.c_float), ("far_clip", C.c_float),
+                ("width", C.c_uint32), ("height", C.c_uint32)]
+
+
+class pg_scene_desc(C.Structure):
+    _fields_ = [("num_vertices", C.c_uint32), ("num_triangles", C.c_uint32), ("num_shapes", C.c_uint32),
+                ("num_materials", C.c_uint32), ("num_emitters", C.c_uint32), ("pad0", C.c_uint32),
+                ("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
+                ("indices", C.POINTER(C.c_uint32)), ("shapes", C.POINTER(pg_shape)),
+                ("materials", C.POINTER(pg_material)), ("emitters", C.POINTER(pg_emitter)),
+                ("camera", pg_camera)]
+
+
+class pg_config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("max_depth", C.c_int32), ("rr_depth", C.c_int32), ("use_nee", C.c_int32),
+                ("hide_emitters", C.c_int32), ("strict_normals", C.c_int32), ("max_component_value", C.c_float),
+                ("seed", C.c_uint32), ("guiding", C.c_int32), ("bsdf_sampling_fraction", C.c_float),
+                ("s_tree_threshold", C.c_float), ("d_tree_threshold", C.c_float), ("d_tree_max_depth", C.c_int32),
+                ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
+                ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
+                ("pad0", C.c_int32)]
+
+
+class pg_record(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("dir", C.c_uint32), ("radiance", C.c_float), ("wo_pdf", C.c_float),
+                ("product", C.c_float), ("weight", C.c_float)]
+
+
+class pg_stats(C.Structure):
+    _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("records", C.c_uint64),
+                ("trace_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double), ("other_ms", C.c_double),
+                ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64)]
+
+
+def default_config(**overrides):
+    """Mirror of pg_config_default() (kept in sync; tests compare both)."""
+    c = pg_config()
+    c.device = 0
+    c.max_depth = -1
+    c.rr_depth = 5
+    c.use_nee = 1
+    c.hide_emitters = 0
+    c.strict_normals = 0
+    c.max_component_value = float("inf")
+    c.seed = 1337
+    c.guiding = 0
+    c.bsdf_sampling_fraction = 0.5
+    c.s_tree_threshold = 12000.0
+    c.d_tree_threshold = 0.01
+    c.d_tree_max_depth = 20
+    c.record_max_vertices = 32
+    c.rank = 0
+    c.world_size = 1
+    c.tile_size = 32
+    c.max_paths_in_flight = 0
+    c.gpu_depth_cap = 1024
+    for k, v in overrides.items():
+        if not hasattr(c, k):
+            raise AttributeError(f"pg_config has no field {k!r}")
+        setattr(c, k, v)
+    return c
+
+
+# (name, restype, argtypes) for every entry point declared in include/pg_capi.h
+VP = C.c_void_p
+SIGNATURES = [
+    ("pg_config_default", C.c_int32, [C.POINTER(pg_config)]),
+    ("pg_create", C.c_int32, [C.POINTER(pg_config), C.POINTER(VP)]),
+    ("pg_destroy", C.c_int32, [VP]),
+    ("pg_last_error", C.c_char_p, [VP]),
+    ("pg_abi_version", C.c_int32, []),
+    ("pg_cancel", C.c_int32, [VP]),
+    ("pg_upload_scene", C.c_int32, [VP, C.POINTER(pg_scene_desc)]),
+    ("pg_render_pass", C.c_int32, [VP, C.c_uint32, C.c_uint32, C.c_int32]),
+    ("pg_get_record_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
+    ("pg_get_records", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, C.POINTER(C.c_uint64)]),
+    ("pg_splat_records", C.c_int32, [VP, VP, C.c_uint64, C.c_int32]),
+    ("pg_splat_local_records", C.c_int32, [VP]),
+    ("pg_refit", C.c_int32, [VP, C.c_uint32]),
+    ("pg_get_sdtree", C.c_int32, [VP, VP, C.c_uint64, C.POINTER(C.c_uint64)]),
+    ("pg_put_sdtree", C.c_int32, [VP, VP, C.c_uint64]),
+    ("pg_sdtree_pdf", C.c_int32, [VP, VP, VP, C.c_uint64, VP]),
+    ("pg_sdtree_sample", C.c_int32, [VP, VP, VP, C.c_uint64, VP, VP]),
+    ("pg_read_film", C.c_int32, [VP, VP, VP]),
+    ("pg_reset_film", C.c_int32, [VP]),
+    ("pg_get_stats", C.c_int32, [VP, C.POINTER(pg_stats)]),
+    ("pg_local_pixel_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
+    ("pg_trace_rays", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
+    ("pg_bsdf_query", C.c_int32, [VP, C.c_uint32, VP, VP, VP, C.c_uint64, VP]),
+]
+
+
+def load_library(path=None):
+    """Load libpgamd.so and attach prototypes.  Raises if it is missing (no fallback path)."""
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        raise RuntimeError(f"HIP extension {path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
+    lib = C.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib

@@ -1,0 +1,843 @@
+// Host driver behind the C-ABI (include/pg_capi.h): device context, scene flattening/upload,
+// the progressive pass driver (ProgressiveMonteCarloIntegrator::renderSamples/renderBlock,
+// src/librender/progressiveintegrator.cpp:65-114,222-282, re-expressed as a GPU wavefront loop),
+// training-record management and the SD-tree refit hook (postprogression, :314-317).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/pg_capi.h"
+#include "pg_bvh.h"
+#include "pg_kernels.h"
+#include "pg_layout.h"
+#include "pg_sdtree.h"
+
+namespace {
+
+constexpr uint32_t kStackDepth = 48;  // must match STACK_DEPTH in pg_kernels.hip
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t alloc(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        release();
+        if (n == 0) return hipSuccess;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        else p = nullptr;
+        return e;
+    }
+    template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+struct Ctx {
+    pg_config cfg{};
+    std::string err;
+    std::atomic<bool> cancel{false};
+    hipStream_t stream = nullptr;
+    // scene
+    bool has_scene = false;
+    GParams g{};
+    DevBuf nodes, woop, tshade, mats, ems, emtri, emcdf;
+    uint32_t num_tris = 0, num_mats = 0;
+    std::vector<GMat> host_mats;
+    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
+    // shard
+    std::vector<uint32_t> local_pixels;
+    DevBuf d_local_pixels;
+    // path state
+    uint32_t P = 0;
+    int vtx_slots = 0;
+    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, counters;
+    uint32_t *h_counter = nullptr;  // pinned
+    // film
+    DevBuf film, film_sq;
+    // records
+    DevBuf records, rec_count;
+    uint64_t rec_capacity = 0;
+    uint64_t rec_host_count = 0;
+    DevBuf ext_records;
+    // sd-tree
+    pgh::SdTree sd;
+    DevBuf sd_snodes, sd_meta, sd_qsum, sd_qchild, sd_bchild, sd_bsum, sd_count;
+    bool sd_dirty = true;
+    // stats
+    pg_stats stats{};
+    std::vector<EventPair> evpool;
+    size_t evused = 0;
+};
+
+thread_local std::string g_tls_err;
+
+pg_status fail(Ctx *c, pg_status code, const std::string &msg) {
+    if (c) c->err = msg;
+    else g_tls_err = msg;
+    return code;
+}
+
+#define HIPC(c, expr)                                                                                              \
+    do {                                                                                                           \
+        hipError_t e_ = (expr);                                                                                    \
+        if (e_ != hipSuccess)                                                                                      \
+            return fail((c), e_ == hipErrorOutOfMemory ? PG_ERR_OOM : PG_ERR_HIP,                                  \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                                        \
+    } while (0)
+
+inline float luminance(const float *c) { return c[0] * 0.212671f + c[1] * 0.715160f + c[2] * 0.072169f; }
+
+// fresnelDielectricExt (util.cpp:653-683), host copy for BSDF::configure()-time constants
+float fresnelDielectricExtH(float cosThetaI_, float eta) {
+    if (eta == 1) return 0.0f;
+    float scale = (cosThetaI_ > 0) ? 1 / eta : eta;
+    float cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0f) return 1.0f;
+    float cosThetaI = std::fabs(cosThetaI_);
+    float cosThetaT = std::sqrt(cosThetaTSqr);
+    float Rs = (cosThetaI - eta * cosThetaT) / (cosThetaI + eta * cosThetaT);
+    float Rp = (eta * cosThetaI - cosThetaT) / (eta * cosThetaI + cosThetaT);
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+// fresnelDiffuseReflectance(eta, fast=false) (util.cpp:816-870): 2 * int_0^1 F(sqrt(xi)) dxi ... as
+// the integral of F over the cosine-weighted hemisphere, by composite Simpson in double.
+float fresnelDiffuseReflectanceH(float eta) {
+    const int N = 2000;
+    double h = 1.0 / N, acc = 0;
+    for (int i = 0; i <= N; ++i) {
+        double w = (i == 0 || i == N) ? 1 : ((i & 1) ? 4 : 2);
+        acc += w * fresnelDielectricExtH((float)std::sqrt(i * h), eta);
+    }
+    return (float)(acc * h / 3.0);
+}
+
+// BSDF::configure(): type bits and derived constants of each plugin
+GMat makeGMat(const pg_material &m) {
+    GMat g{};
+    g.model = m.type;
+    g.dist = m.distribution;
+    g.flags = m.flags;
+    g.alpha_u = std::max(m.alpha_u, 1e-4f);  // MicrofacetDistribution clamps alpha (microfacet.h:70-72)
+    g.alpha_v = std::max(m.alpha_v, 1e-4f);
+    g.eta = m.int_ior / m.ext_ior;
+    g.invEta = 1.0f / g.eta;
+    g.invEta2 = 1.0f / (g.eta * g.eta);
+    for (int i = 0; i < 4; ++i) {
+        g.diff[i] = m.diffuse_reflectance[i];
+        g.spec[i] = m.specular_reflectance[i];
+        g.trans[i] = m.specular_transmittance[i];
+        g.ceta[i] = m.eta[i];
+        g.ck[i] = m.k[i];
+    }
+    uint32_t sides = 0x8000u;  // EFrontSide
+    switch (m.type) {
+        case PG_BSDF_DIFFUSE: g.type = 0x2; break;                       // EDiffuseReflection
+        case PG_BSDF_CONDUCTOR: g.type = 0x20; break;                    // EDeltaReflection
+        case PG_BSDF_ROUGHCONDUCTOR: g.type = 0x8; break;                // EGlossyReflection
+        case PG_BSDF_DIELECTRIC: g.type = 0x20 | 0x40; sides |= 0x10000u; break;
+        case PG_BSDF_ROUGHDIELECTRIC: g.type = 0x8 | 0x10; sides |= 0x10000u; break;
+        case PG_BSDF_PLASTIC: {
+            g.type = 0x20 | 0x2;
+            g.fdrInt = fresnelDiffuseReflectanceH(1 / g.eta);
+            float dAvg = luminance(m.diffuse_reflectance), sAvg = luminance(m.specular_reflectance);
+            g.specWeight = sAvg / (dAvg + sAvg);
+            break;
+        }
+        default: g.type = 0;
+    }
+    if (m.flags & PG_MAT_TWOSIDED) sides |= 0x10000u;
+    g.type |= sides;
+    return g;
+}
+
+// Shading record of triangle t (pg_layout.h PG_TRI_SHADE_F4)
+void packShade(float *o, const float *P, const float *N, const uint32_t *I, uint32_t t, uint32_t bits, uint32_t orig) {
+    const uint32_t i0 = I[3 * (size_t)t], i1 = I[3 * (size_t)t + 1], i2 = I[3 * (size_t)t + 2];
+    const float *p0 = P + 3 * (size_t)i0, *p1 = P + 3 * (size_t)i1, *p2 = P + 3 * (size_t)i2;
+    float n0[3], n1[3], n2[3];
+    if (N) {
+        for (int a = 0; a < 3; ++a) {
+            n0[a] = N[3 * (size_t)i0 + a];
+            n1[a] = N[3 * (size_t)i1 + a];
+            n2[a] = N[3 * (size_t)i2 + a];
+        }
+    } else {  // face normal (TriMesh without vertex normals)
+        float e1[3] = {p1[0] - p0[0], p1[1] - p0[1], p1[2] - p0[2]};
+        float e2[3] = {p2[0] - p0[0], p2[1] - p0[1], p2[2] - p0[2]};
+        float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        float l = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+        for (int a = 0; a < 3; ++a) n0[a] = n1[a] = n2[a] = l > 0 ? c[a] / l : 0.0f;
+    }
+    float b, o2;
+    std::memcpy(&b, &bits, 4);
+    std::memcpy(&o2, &orig, 4);
+    float rec[20] = {p0[0], p0[1], p0[2], b,     p1[0], p1[1], p1[2], n2[2], p2[0], p2[1],
+                     p2[2], o2,    n0[0], n0[1], n0[2], n1[0], n1[1], n1[2], n2[0], n2[1]};
+    std::memcpy(o, rec, sizeof rec);
+}
+
+template <class T>
+pg_status upload(Ctx *c, DevBuf &b, const std::vector<T> &v) {
+    size_t n = std::max<size_t>(v.size() * sizeof(T), 16);
+    HIPC(c, b.alloc(n));
+    if (!v.empty()) HIPC(c, hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    return PG_OK;
+}
+
+SceneDev sceneView(const Ctx *c) {
+    return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->tshade.as<float4>(), c->mats.as<GMat>(),
+                    c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>()};
+}
+SDDev sdView(const Ctx *c) {
+    SDDev s{};
+    s.snodes = c->sd_snodes.as<uint2>();
+    s.meta = c->sd_meta.as<uint4>();
+    s.qsum = c->sd_qsum.as<float4>();
+    s.qchild = c->sd_qchild.as<uint4>();
+    s.bchild = c->sd_bchild.as<uint4>();
+    s.bsum = c->sd_bsum.as<unsigned long long>();
+    s.count = c->sd_count.as<uint32_t>();
+    for (int a = 0; a < 3; ++a) s.lo[a] = c->sd.lo[a];
+    s.extent = c->sd.extent;
+    s.built = c->sd.built ? 1 : 0;
+    return s;
+}
+PathDev pathView(const Ctx *c) {
+    return PathDev{c->ray_o.as<float4>(), c->ray_d.as<float4>(), c->hit.as<float4>(), c->thr.as<float4>(),
+                   c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(), c->sh_o.as<float4>(),
+                   c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->P};
+}
+
+pg_status uploadSd(Ctx *c) {
+    pgh::SdTree::Flat f;
+    c->sd.flatten(f);
+    pg_status s;
+    if ((s = upload(c, c->sd_snodes, f.snodes)) || (s = upload(c, c->sd_meta, f.meta)) ||
+        (s = upload(c, c->sd_qsum, f.qsum)) || (s = upload(c, c->sd_qchild, f.qchild)) ||
+        (s = upload(c, c->sd_bchild, f.bchild)) || (s = upload(c, c->sd_bsum, f.bsum)) ||
+        (s = upload(c, c->sd_count, f.count)))
+        return s;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->stats.stree_nodes = c->sd.snode.size() / 2;
+    c->stats.dtree_nodes = c->sd.samplingNodes();
+    c->sd_dirty = false;
+    return PG_OK;
+}
+
+// pull device-side building sums + counts into the host tree
+pg_status downloadSd(Ctx *c) {
+    size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
+    std::vector<uint64_t> bsum(4 * nb);
+    std::vector<uint32_t> cnt(nl);
+    HIPC(c, hipMemcpyAsync(bsum.data(), c->sd_bsum.p, bsum.size() * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(cnt.data(), c->sd_count.p, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->sd.absorb(bsum, cnt);
+    return PG_OK;
+}
+
+EventPair nextEvents(Ctx *c) {
+    if (c->evused == c->evpool.size()) {
+        EventPair e;
+        (void)hipEventCreate(&e.a);
+        (void)hipEventCreate(&e.b);
+        c->evpool.push_back(e);
+    }
+    return c->evpool[c->evused++];
+}
+
+// path-state capacity for a pass over `total` paths
+pg_status ensurePaths(Ctx *c, uint32_t want) {
+    uint32_t P = want;
+    int vslots = (c->cfg.guiding ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0);
+    if (P <= c->P && vslots <= c->vtx_slots) return PG_OK;
+    P = std::max(P, c->P);
+    vslots = std::max(vslots, c->vtx_slots);
+    size_t f4 = (size_t)P * 16;
+    HIPC(c, c->ray_o.alloc(f4));
+    HIPC(c, c->ray_d.alloc(f4));
+    HIPC(c, c->hit.alloc(f4));
+    HIPC(c, c->thr.alloc(f4));
+    HIPC(c, c->rad.alloc(f4));
+    HIPC(c, c->prev.alloc(f4));
+    HIPC(c, c->pinfo.alloc(f4));
+    HIPC(c, c->sh_o.alloc(f4));
+    HIPC(c, c->sh_d.alloc(f4));
+    HIPC(c, c->sh_c.alloc(f4));
+    HIPC(c, c->q0.alloc((size_t)P * 4));
+    HIPC(c, c->q1.alloc((size_t)P * 4));
+    HIPC(c, c->qs.alloc((size_t)P * 4));
+    if (vslots > 0) HIPC(c, c->vtx.alloc((size_t)vslots * P * 48));
+    c->P = P;
+    c->vtx_slots = vslots;
+    return PG_OK;
+}
+
+pg_status ensureRecords(Ctx *c, uint64_t want) {
+    if (want <= c->rec_capacity) return PG_OK;
+    uint64_t cap = std::max<uint64_t>(want + want / 2, 1u << 20);
+    DevBuf nb;
+    HIPC(c, nb.alloc(cap * sizeof(pg_record)));
+    if (c->rec_host_count)
+        HIPC(c, hipMemcpyAsync(nb.p, c->records.p, c->rec_host_count * sizeof(pg_record), hipMemcpyDeviceToDevice,
+                               c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    std::swap(c->records.p, nb.p);
+    std::swap(c->records.bytes, nb.bytes);
+    c->rec_capacity = cap;
+    return PG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t pg_abi_version(void) { return PG_ABI_VERSION; }
+
+pg_status pg_config_default(pg_config *c) {
+    if (!c) return PG_ERR_INVALID;
+    std::memset(c, 0, sizeof *c);
+    c->device = 0;
+    c->max_depth = -1;
+    c->rr_depth = 5;
+    c->use_nee = 1;
+    c->hide_emitters = 0;
+    c->strict_normals = 0;
+    c->max_component_value = std::numeric_limits<float>::infinity();
+    c->seed = 1337;
+    c->guiding = 0;
+    c->bsdf_sampling_fraction = 0.5f;
+    c->s_tree_threshold = 12000.0f;
+    c->d_tree_threshold = 0.01f;
+    c->d_tree_max_depth = 20;
+    c->record_max_vertices = 32;
+    c->rank = 0;
+    c->world_size = 1;
+    c->tile_size = 32;
+    c->max_paths_in_flight = 0;
+    c->gpu_depth_cap = 1024;
+    return PG_OK;
+}
+
+const char *pg_last_error(void *ctx) {
+    if (!ctx) return g_tls_err.c_str();
+    return ((Ctx *)ctx)->err.c_str();
+}
+
+pg_status pg_create(const pg_config *cfg, void **out) {
+    if (!cfg || !out) return fail(nullptr, PG_ERR_INVALID, "pg_create: null argument");
+    *out = nullptr;
+    if (cfg->world_size < 1 || cfg->rank < 0 || cfg->rank >= cfg->world_size)
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: bad rank/world_size");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(nullptr, PG_ERR_NO_DEVICE, "pg_create: no HIP device visible");
+    if (cfg->device < 0 || cfg->device >= n) return fail(nullptr, PG_ERR_INVALID, "pg_create: bad device ordinal");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) != hipSuccess)
+        return fail(nullptr, PG_ERR_HIP, "pg_create: hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, PG_ERR_NO_DEVICE, std::string("pg_create: device is ") + prop.gcnArchName + ", need gfx950");
+    Ctx *c = new Ctx();
+    c->cfg = *cfg;
+    if (c->cfg.tile_size == 0) c->cfg.tile_size = 32;
+    if (c->cfg.gpu_depth_cap <= 0) c->cfg.gpu_depth_cap = 1024;
+    if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_counter, 16, hipHostMallocDefault) != hipSuccess) {
+        delete c;
+        return fail(nullptr, PG_ERR_HIP, "pg_create: stream/pinned allocation failed");
+    }
+    *out = c;
+    return PG_OK;
+}
+
+pg_status pg_destroy(void *ctx) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return PG_OK;
+    (void)hipSetDevice(c->cfg.device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &e : c->evpool) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    if (c->h_counter) (void)hipHostFree(c->h_counter);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return PG_OK;
+}
+
+pg_status pg_cancel(void *ctx) {
+    if (!ctx) return PG_ERR_INVALID;
+    ((Ctx *)ctx)->cancel.store(true);
+    return PG_OK;
+}
+
+pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !d) return fail(c, PG_ERR_INVALID, "pg_upload_scene: null argument");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!d->positions || !d->indices || !d->shapes || !d->materials || d->num_triangles == 0)
+        return fail(c, PG_ERR_INVALID, "pg_upload_scene: empty scene");
+    if (d->camera.width == 0 || d->camera.height == 0) return fail(c, PG_ERR_INVALID, "pg_upload_scene: empty film");
+    const uint32_t nt = d->num_triangles;
+    for (uint64_t i = 0; i < 3ull * nt; ++i)
+        if (d->indices[i] >= d->num_vertices) return fail(c, PG_ERR_INVALID, "pg_upload_scene: index out of range");
+    if (d->num_materials > 65535 || d->num_emitters > 65534)
+        return fail(c, PG_ERR_INVALID, "pg_upload_scene: too many materials/emitters");
+    // per-triangle (material | emitter+1 << 16) from the shape partition
+    std::vector<uint32_t> triBits(nt, 0xFFFFFFFFu);
+    for (uint32_t s = 0; s < d->num_shapes; ++s) {
+        const pg_shape &sh = d->shapes[s];
+        if ((uint64_t)sh.tri_begin + sh.tri_count > nt || sh.material >= d->num_materials ||
+            (sh.emitter >= 0 && (uint32_t)sh.emitter >= d->num_emitters))
+            return fail(c, PG_ERR_INVALID, "pg_upload_scene: bad shape");
+        uint32_t bits = sh.material | ((uint32_t)(sh.emitter + 1) << 16);
+        for (uint32_t t = 0; t < sh.tri_count; ++t) triBits[sh.tri_begin + t] = bits;
+    }
+    for (uint32_t t = 0; t < nt; ++t)
+        if (triBits[t] == 0xFFFFFFFFu) return fail(c, PG_ERR_INVALID, "pg_upload_scene: triangle without a shape");
+
+    pgh::BvhOut bvh;
+    if (!pgh::buildBvh(d->positions, d->indices, nt, kStackDepth, bvh))
+        return fail(c, PG_ERR_INVALID, "pg_upload_scene: BVH deeper than the traversal stack");
+    std::vector<float> shade((size_t)20 * nt);
+    for (uint32_t k = 0; k < nt; ++k) {
+        uint32_t t = bvh.order[k];
+        packShade(&shade[20 * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
+    }
+    // emitters: compact triangle array + area CDF (double accumulation of fp32 areas)
+    std::vector<GEmitter> ems;
+    std::vector<float> emtri, emcdf;
+    for (uint32_t e = 0; e < d->num_emitters; ++e) {
+        const pg_emitter &pe = d->emitters[e];
+        if (pe.shape >= d->num_shapes) return fail(c, PG_ERR_INVALID, "pg_upload_scene: emitter without shape");
+        const pg_shape &sh = d->shapes[pe.shape];
+        GEmitter g{};
+        g.tri_begin = (uint32_t)(emtri.size() / 20);
+        g.tri_count = sh.tri_count;
+        g.cdf_begin = (uint32_t)emcdf.size();
+        std::vector<double> cum(sh.tri_count + 1, 0.0);
+        double acc = 0;
+        for (uint32_t i = 0; i < sh.tri_count; ++i) {
+            uint32_t t = sh.tri_begin + i;
+            const float *a = d->positions + 3 * (size_t)d->indices[3 * (size_t)t];
+            const float *b = d->positions + 3 * (size_t)d->indices[3 * (size_t)t + 1];
+            const float *cc = d->positions + 3 * (size_t)d->indices[3 * (size_t)t + 2];
+            float u[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, v[3] = {cc[0] - a[0], cc[1] - a[1], cc[2] - a[2]};
+            float x[3] = {u[1] * v[2] - u[2] * v[1], u[2] * v[0] - u[0] * v[2], u[0] * v[1] - u[1] * v[0]};
+            float area = 0.5f * std::sqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+            acc += (double)area;
+            cum[i + 1] = acc;
+            size_t o = emtri.size();
+            emtri.resize(o + 20);
+            packShade(&emtri[o], d->positions, d->normals, d->indices, t, 0, t);
+        }
+        if (!(acc > 0)) return fail(c, PG_ERR_INVALID, "pg_upload_scene: emitter with zero area");
+        for (uint32_t i = 0; i < sh.tri_count; ++i) emcdf.push_back((float)(cum[i] / acc));
+        emcdf.push_back(1.0f);
+        g.inv_area = 1.0f / (float)acc;
+        for (int k = 0; k < 4; ++k) g.radiance[k] = pe.radiance[k];
+        ems.push_back(g);
+    }
+    c->host_mats.clear();
+    for (uint32_t m = 0; m < d->num_materials; ++m) c->host_mats.push_back(makeGMat(d->materials[m]));
+
+    pg_status s;
+    if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) || (s = upload(c, c->tshade, shade)) ||
+        (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||
+        (s = upload(c, c->emcdf, emcdf)))
+        return s;
+
+    // camera (Transform::lookAt, transform.cpp:191-214) and integrator constants
+    GParams &g = c->g;
+    std::memset(&g, 0, sizeof g);
+    const pg_camera &cam = d->camera;
+    float dir[3] = {cam.target[0] - cam.origin[0], cam.target[1] - cam.origin[1], cam.target[2] - cam.origin[2]};
+    float l = std::sqrt(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+    for (int a = 0; a < 3; ++a) dir[a] /= l;
+    const float *up = cam.up;
+    float left[3] = {up[1] * dir[2] - up[2] * dir[1], up[2] * dir[0] - up[0] * dir[2], up[0] * dir[1] - up[1] * dir[0]};
+    l = std::sqrt(left[0] * left[0] + left[1] * left[1] + left[2] * left[2]);
+    for (int a = 0; a < 3; ++a) left[a] /= l;
+    float nup[3] = {dir[1] * left[2] - dir[2] * left[1], dir[2] * left[0] - dir[0] * left[2],
+                    dir[0] * left[1] - dir[1] * left[0]};
+    for (int a = 0; a < 3; ++a) {
+        g.cam_o[a] = cam.origin[a];
+        g.cam_left[a] = left[a];
+        g.cam_up[a] = nup[a];
+        g.cam_dir[a] = dir[a];
+    }
+    g.tan_half = std::tan(cam.fov_x_deg * 3.14159265358979323846f / 360.0f);
+    g.aspect = (float)cam.width / (float)cam.height;
+    g.near_clip = cam.near_clip;
+    g.far_clip = cam.far_clip;
+    g.width = cam.width;
+    g.height = cam.height;
+    g.num_emitters = d->num_emitters;
+    g.num_materials = d->num_materials;
+
+    // tile shard of this rank: 32x32 tiles dealt round-robin
+    const uint32_t T = c->cfg.tile_size, tx = (cam.width + T - 1) / T, ty = (cam.height + T - 1) / T;
+    c->local_pixels.clear();
+    for (uint32_t t = 0; t < tx * ty; ++t) {
+        if ((int32_t)(t % (uint32_t)c->cfg.world_size) != c->cfg.rank) continue;
+        uint32_t x0 = (t % tx) * T, y0 = (t / tx) * T;
+        for (uint32_t y = y0; y < std::min(y0 + T, cam.height); ++y)
+            for (uint32_t x = x0; x < std::min(x0 + T, cam.width); ++x) c->local_pixels.push_back(y * cam.width + x);
+    }
+    if ((s = upload(c, c->d_local_pixels, c->local_pixels))) return s;
+    size_t fb = (size_t)cam.width * cam.height * 16;
+    HIPC(c, c->film.alloc(fb));
+    HIPC(c, c->film_sq.alloc(fb));
+    HIPC(c, hipMemsetAsync(c->film.p, 0, fb, c->stream));
+    HIPC(c, hipMemsetAsync(c->film_sq.p, 0, fb, c->stream));
+    HIPC(c, c->counters.alloc(64));
+    HIPC(c, c->rec_count.alloc(16));
+    HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 16, c->stream));
+    c->rec_host_count = 0;
+    c->num_tris = nt;
+    c->num_mats = d->num_materials;
+    for (int a = 0; a < 3; ++a) {
+        c->scene_lo[a] = bvh.lo[a];
+        c->scene_hi[a] = bvh.hi[a];
+    }
+    c->sd.reset(c->scene_lo, c->scene_hi);
+    if ((s = uploadSd(c))) return s;
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->has_scene = true;
+    return PG_OK;
+}
+
+pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_t record) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_render_pass: null context");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_render_pass: no scene uploaded");
+    if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const uint32_t npix = (uint32_t)c->local_pixels.size();
+    if (npix == 0 || spp == 0) return PG_OK;
+    const bool rec = record && c->cfg.guiding;
+    uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
+    uint64_t total = (uint64_t)npix * spp;
+    uint32_t want = (uint32_t)std::min<uint64_t>(total, cap);
+    pg_status s;
+    if ((s = ensurePaths(c, want))) return s;
+    GParams g = c->g;
+    g.max_depth = c->cfg.max_depth;
+    g.rr_depth = c->cfg.rr_depth;
+    g.use_nee = c->cfg.use_nee;
+    g.hide_emitters = c->cfg.hide_emitters;
+    g.strict_normals = c->cfg.strict_normals;
+    g.guiding = c->cfg.guiding;
+    g.record = rec ? 1 : 0;
+    g.max_vertices = rec ? std::min(c->cfg.record_max_vertices, c->vtx_slots) : 0;
+    g.max_component_value = c->cfg.max_component_value;
+    g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
+    g.seed = c->cfg.seed;
+    g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
+    const SceneDev sc = sceneView(c);
+    const SDDev sd = sdView(c);
+    const PathDev pv = pathView(c);
+    uint32_t *cnt = c->counters.as<uint32_t>();  // [0],[1] ping-pong live counts, [2] shadow count
+    // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
+    uint32_t layersPer = std::max<uint32_t>(1, c->P / npix);
+    uint32_t pixPer = std::min(npix, c->P);
+    for (uint32_t l0 = 0; l0 < spp; l0 += layersPer) {
+        uint32_t nl = std::min(layersPer, spp - l0);
+        if (npix > c->P) nl = 1;
+        for (uint32_t pb = 0; pb < npix; pb += pixPer) {
+            uint32_t np = std::min(pixPer, npix - pb);
+            uint32_t n = np * nl;
+            if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+            uint32_t *qin = c->q0.as<uint32_t>(), *qout = c->q1.as<uint32_t>();
+            int cin = 0;
+            pg_launch_camera(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + l0, qin);
+            c->h_counter[0] = n;
+            HIPC(c, hipMemcpyAsync(cnt, c->h_counter, 4, hipMemcpyHostToDevice, c->stream));
+            uint32_t live = n;
+            for (uint32_t bounce = 0; live > 0; ++bounce) {
+                HIPC(c, hipMemsetAsync(cnt + (1 - cin), 0, 4, c->stream));
+                HIPC(c, hipMemsetAsync(cnt + 2, 0, 4, c->stream));
+                EventPair et = nextEvents(c);
+                HIPC(c, hipEventRecord(et.a, c->stream));
+                pg_launch_trace(c->stream, sc, pv, qin, cnt + cin, live);
+                HIPC(c, hipEventRecord(et.b, c->stream));
+                EventPair es = nextEvents(c);
+                HIPC(c, hipEventRecord(es.a, c->stream));
+                pg_launch_shade(c->stream, g, sc, sd, pv, qin, cnt + cin, live, qout, cnt + (1 - cin), c->qs.as<uint32_t>(),
+                                cnt + 2);
+                HIPC(c, hipEventRecord(es.b, c->stream));
+                EventPair ew = nextEvents(c);
+                HIPC(c, hipEventRecord(ew.a, c->stream));
+                pg_launch_shadow(c->stream, sc, pv, c->qs.as<uint32_t>(), cnt + 2, live);
+                HIPC(c, hipEventRecord(ew.b, c->stream));
+                HIPC(c, hipGetLastError());
+                HIPC(c, hipMemcpyAsync(c->h_counter, cnt, 12, hipMemcpyDeviceToHost, c->stream));
+                HIPC(c, hipStreamSynchronize(c->stream));
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, et.a, et.b);
+                c->stats.trace_ms += ms;
+                c->stats.trace_launches++;
+                (void)hipEventElapsedTime(&ms, es.a, es.b);
+                c->stats.shade_ms += ms;
+                (void)hipEventElapsedTime(&ms, ew.a, ew.b);
+                c->stats.shadow_ms += ms;
+                c->evused = 0;
+                c->stats.segments += live;
+                c->stats.shadow_rays += c->h_counter[2];
+                live = c->h_counter[1 - cin];
+                std::swap(qin, qout);
+                cin = 1 - cin;
+                if (bounce > (uint32_t)c->cfg.gpu_depth_cap + 2) break;
+            }
+            pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
+                           c->film_sq.as<float4>());
+            if (rec) {
+                // bound: every slot can emit at most max_vertices records
+                if ((s = ensureRecords(c, c->rec_host_count + (uint64_t)n * g.max_vertices))) return s;
+                pg_launch_commit(c->stream, pv, n, g.max_vertices, c->records.as<pg_record>(),
+                                 c->rec_count.as<unsigned long long>(), c->rec_capacity);
+                unsigned long long rc = 0;
+                HIPC(c, hipMemcpyAsync(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost, c->stream));
+                HIPC(c, hipStreamSynchronize(c->stream));
+                c->stats.records += rc - c->rec_host_count;
+                c->rec_host_count = rc;
+            }
+            HIPC(c, hipGetLastError());
+            c->stats.paths += n;
+        }
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_get_record_count(void *ctx, uint64_t *count) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !count) return fail(c, PG_ERR_INVALID, "pg_get_record_count: null argument");
+    *count = c->rec_host_count;
+    return PG_OK;
+}
+
+pg_status pg_get_records(void *ctx, void *dst, uint64_t max_records, int32_t dst_is_device, uint64_t *written) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!dst && max_records)) return fail(c, PG_ERR_INVALID, "pg_get_records: null argument");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    uint64_t n = std::min(max_records, c->rec_host_count);
+    if (n)
+        HIPC(c, hipMemcpyAsync(dst, c->records.p, n * sizeof(pg_record),
+                               dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (written) *written = n;
+    return PG_OK;
+}
+
+pg_status pg_splat_records(void *ctx, const void *src, uint64_t count, int32_t src_is_device) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!src && count)) return fail(c, PG_ERR_INVALID, "pg_splat_records: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_splat_records: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!count) return PG_OK;
+    const pg_record *dsrc = (const pg_record *)src;
+    if (!src_is_device) {
+        HIPC(c, c->ext_records.alloc(count * sizeof(pg_record)));
+        HIPC(c, hipMemcpyAsync(c->ext_records.p, src, count * sizeof(pg_record), hipMemcpyHostToDevice, c->stream));
+        dsrc = c->ext_records.as<pg_record>();
+    }
+    EventPair e = nextEvents(c);
+    HIPC(c, hipEventRecord(e.a, c->stream));
+    pg_launch_splat(c->stream, sdView(c), dsrc, count);
+    HIPC(c, hipEventRecord(e.b, c->stream));
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipStreamSynchronize(c->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e.a, e.b);
+    c->stats.other_ms += ms;
+    c->evused = 0;
+    return PG_OK;
+}
+
+pg_status pg_splat_local_records(void *ctx) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_splat_local_records: null context");
+    if (c->rec_host_count == 0) return PG_OK;
+    return pg_splat_records(ctx, c->records.p, c->rec_host_count, 1);
+}
+
+pg_status pg_refit(void *ctx, uint32_t iteration) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_refit: null context");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_refit: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    pg_status s;
+    if ((s = downloadSd(c))) return s;
+    c->sd.refit(iteration, c->cfg.s_tree_threshold, c->cfg.d_tree_threshold, c->cfg.d_tree_max_depth);
+    if ((s = uploadSd(c))) return s;
+    HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 8, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    c->rec_host_count = 0;
+    return PG_OK;
+}
+
+pg_status pg_get_sdtree(void *ctx, void *buf, uint64_t capacity, uint64_t *size) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !size) return fail(c, PG_ERR_INVALID, "pg_get_sdtree: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_get_sdtree: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    pg_status s;
+    if ((s = downloadSd(c))) return s;
+    std::vector<uint8_t> blob = c->sd.serialize();
+    *size = blob.size();
+    if (buf) {
+        if (capacity < blob.size()) return fail(c, PG_ERR_INVALID, "pg_get_sdtree: buffer too small");
+        std::memcpy(buf, blob.data(), blob.size());
+    }
+    return PG_OK;
+}
+
+pg_status pg_put_sdtree(void *ctx, const void *buf, uint64_t size) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !buf) return fail(c, PG_ERR_INVALID, "pg_put_sdtree: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_put_sdtree: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    pgh::SdTree t;
+    if (!t.deserialize((const uint8_t *)buf, size)) return fail(c, PG_ERR_INVALID, "pg_put_sdtree: malformed blob");
+    c->sd = std::move(t);
+    return uploadSd(c);
+}
+
+pg_status pg_sdtree_pdf(void *ctx, const float *pos, const float *dir, uint64_t n, float *out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !pos || !dir || !out) return fail(c, PG_ERR_INVALID, "pg_sdtree_pdf: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_sdtree_pdf: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    DevBuf a, b, o;
+    HIPC(c, a.alloc(n * 12 + 16));
+    HIPC(c, b.alloc(n * 12 + 16));
+    HIPC(c, o.alloc(n * 4 + 16));
+    HIPC(c, hipMemcpyAsync(a.p, pos, n * 12, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(b.p, dir, n * 12, hipMemcpyHostToDevice, c->stream));
+    pg_launch_sd_pdf(c->stream, sdView(c), a.as<float>(), b.as<float>(), (uint32_t)n, o.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(out, o.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_sdtree_sample(void *ctx, const float *pos, const float *u, uint64_t n, float *dir_out, float *pdf_out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !pos || !u || !dir_out || !pdf_out) return fail(c, PG_ERR_INVALID, "pg_sdtree_sample: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_sdtree_sample: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    DevBuf a, b, d, p;
+    HIPC(c, a.alloc(n * 12 + 16));
+    HIPC(c, b.alloc(n * 8 + 16));
+    HIPC(c, d.alloc(n * 12 + 16));
+    HIPC(c, p.alloc(n * 4 + 16));
+    HIPC(c, hipMemcpyAsync(a.p, pos, n * 12, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(b.p, u, n * 8, hipMemcpyHostToDevice, c->stream));
+    pg_launch_sd_sample(c->stream, sdView(c), a.as<float>(), b.as<float>(), (uint32_t)n, d.as<float>(), p.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(dir_out, d.p, n * 12, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(pdf_out, p.p, n * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_read_film(void *ctx, float *rgbw, float *sumsq) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_read_film: null context");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_read_film: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    size_t fb = (size_t)c->g.width * c->g.height * 16;
+    if (rgbw) HIPC(c, hipMemcpyAsync(rgbw, c->film.p, fb, hipMemcpyDeviceToHost, c->stream));
+    if (sumsq) HIPC(c, hipMemcpyAsync(sumsq, c->film_sq.p, fb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_reset_film(void *ctx) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_reset_film: null context");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_reset_film: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    size_t fb = (size_t)c->g.width * c->g.height * 16;
+    HIPC(c, hipMemsetAsync(c->film.p, 0, fb, c->stream));
+    HIPC(c, hipMemsetAsync(c->film_sq.p, 0, fb, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_get_stats(void *ctx, pg_stats *st) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !st) return fail(c, PG_ERR_INVALID, "pg_get_stats: null argument");
+    *st = c->stats;
+    return PG_OK;
+}
+
+pg_status pg_local_pixel_count(void *ctx, uint64_t *count) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !count) return fail(c, PG_ERR_INVALID, "pg_local_pixel_count: null argument");
+    *count = c->local_pixels.size();
+    return PG_OK;
+}
+
+pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hit, float *hits) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!rays && n) || (!hits && n)) return fail(c, PG_ERR_INVALID, "pg_trace_rays: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_trace_rays: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!n) return PG_OK;
+    DevBuf r, h;
+    HIPC(c, r.alloc(n * 32));
+    HIPC(c, h.alloc(n * 16));
+    HIPC(c, hipMemcpyAsync(r.p, rays, n * 32, hipMemcpyHostToDevice, c->stream));
+    pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, any_hit, h.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(hits, h.p, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_bsdf_query(void *ctx, uint32_t material, const float *wi, const float *u, const float *wo_given, uint64_t n,
+                        float *out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!wi && n) || (!u && n) || (!out && n)) return fail(c, PG_ERR_INVALID, "pg_bsdf_query: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_bsdf_query: no scene");
+    if (material >= c->num_mats) return fail(c, PG_ERR_INVALID, "pg_bsdf_query: bad material");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!n) return PG_OK;
+    DevBuf a, b, g, o;
+    HIPC(c, a.alloc(n * 12));
+    HIPC(c, b.alloc(n * 12));
+    HIPC(c, o.alloc(n * 48));
+    HIPC(c, hipMemcpyAsync(a.p, wi, n * 12, hipMemcpyHostToDevice, c->stream));
+    HIPC(c, hipMemcpyAsync(b.p, u, n * 12, hipMemcpyHostToDevice, c->stream));
+    if (wo_given) {
+        HIPC(c, g.alloc(n * 12));
+        HIPC(c, hipMemcpyAsync(g.p, wo_given, n * 12, hipMemcpyHostToDevice, c->stream));
+    }
+    pg_launch_bsdf_query(c->stream, c->mats.as<GMat>() + material, a.as<float>(), b.as<float>(),
+                         wo_given ? g.as<float>() : nullptr, (uint32_t)n, o.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(out, o.p, n * 48, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,704 @@
+// gfx950 kernels of the guided path-tracing wavefront (DESIGN.md §"Kernels").
+//
+// One bounce of the reference's ProgressiveMIPathTracer::Li (progressive_path.cpp:133-314) is
+// split into:  trace (closest hit over the live-path queue) -> shade (emission/MIS of the previous
+// segment, Russian roulette, NEE sampling, BSDF / SD-tree one-sample-MIS direction sampling,
+// training-vertex write, queue compaction by wave ballot) -> shadow (any hit; adds the NEE
+// contribution).  Camera rays, film accumulation, record commit and SD-tree splat are separate
+// kernels.  Path state is SoA float4/uint4 arrays indexed by path slot.
+#include "pg_device.h"
+#include "pg_kernels.h"
+
+using namespace pgd;
+
+#define TRACE_BLOCK 128
+#define STACK_DEPTH 48
+#define SHADE_BLOCK 256
+
+namespace {
+
+// ---------------------------------------------------------------------------------------------
+// BVH traversal (binned-SAH BVH2, 64-B nodes; Woop unit-triangle test, 48-B triangles).
+// Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142, sahkdtree3.h:178-308)
+// with the same contract: closest t in [tmin, tmax] (any hit for shadow rays).
+template <bool ANY>
+__device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+                                         float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
+                                         uint32_t *__restrict__ stk) {
+    const float eps = 1e-30f;
+    f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
+                 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
+                 1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+    f3 ood = o * idir;
+    int sp = 0;
+    int node = 0;
+    bool found = false;
+    for (;;) {
+        if (node >= 0) {
+            const float4 n0 = nodes[4 * node + 0];
+            const float4 n1 = nodes[4 * node + 1];
+            const float4 n2 = nodes[4 * node + 2];
+            const float4 n3 = nodes[4 * node + 3];
+            float a0 = fmaf(n0.x, idir.x, -ood.x), a1 = fmaf(n0.y, idir.x, -ood.x);
+            float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
+            float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
+            float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), tmin));
+            float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), tmax));
+            float b0 = fmaf(n1.x, idir.x, -ood.x), b1 = fmaf(n1.y, idir.x, -ood.x);
+            float b2 = fmaf(n1.z, idir.y, -ood.y), b3 = fmaf(n1.w, idir.y, -ood.y);
+            float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
+            float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), tmin));
+            float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tmax));
+            bool h0 = c0min <= c0max, h1 = c1min <= c1max;
+            int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+            if (h0 && h1) {
+                int nearC = ch0, farC = ch1;
+                if (c1min < c0min) {
+                    nearC = ch1;
+                    farC = ch0;
+                }
+                if (sp < STACK_DEPTH) stk[(sp++) * TRACE_BLOCK] = (uint32_t)farC;
+                node = nearC;
+                continue;
+            } else if (h0) {
+                node = ch0;
+                continue;
+            } else if (h1) {
+                node = ch1;
+                continue;
+            }
+        } else {
+            uint32_t leaf = ~(uint32_t)node;
+            uint32_t first = leaf >> 4, cnt = leaf & 15u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                uint32_t t = first + k;
+                const float4 w0 = woop[3 * t + 0];
+                float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
+                float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
+                float tt = oz / dz;
+                if (tt >= tmin && tt <= tmax) {
+                    const float4 w1 = woop[3 * t + 1];
+                    float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
+                    if (a >= 0.0f && a <= 1.0f) {
+                        const float4 w2 = woop[3 * t + 2];
+                        float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) +
+                                  tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
+                        if (b >= 0.0f && a + b <= 1.0f) {
+                            found = true;
+                            if (ANY) return true;
+                            tmax = tt;
+                            hitTri = t;
+                            hu = b;             // weight of p1
+                            hv = 1.0f - a - b;  // weight of p2
+                        }
+                    }
+                }
+            }
+        }
+        if (sp == 0) break;
+        node = (int)stk[(--sp) * TRACE_BLOCK];
+    }
+    return found;
+}
+
+__device__ __forceinline__ float miWeight(float a, float b) {
+    a *= a;
+    b *= b;
+    return a / (a + b);
+}
+
+// wave-aggregated append of `pred` lanes' values into q (one atomic per wave)
+__device__ __forceinline__ void waveAppend(bool pred, uint32_t value, uint32_t *q, uint32_t *count) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0) return;
+    int lane = threadIdx.x & 63;
+    int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (pred) {
+        unsigned long long below = m & ((1ull << lane) - 1ull);
+        q[base + __popcll(below)] = value;
+    }
+}
+
+struct Hit {
+    f3 p, geoN, shN;
+    Frame sh;
+    f3 wi;
+    uint32_t mat;
+    int emitter;
+};
+
+__device__ __forceinline__ void fetchHit(const SceneDev &sc, uint32_t tri, float u, float v, f3 rd, Hit &h) {
+    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
+    float4 s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3], s4 = r[4];
+    uint32_t bits = __float_as_uint(s0.w);
+    h.mat = bits & 0xFFFFu;
+    h.emitter = (int)(bits >> 16) - 1;
+    float b0 = 1 - u - v;
+    f3 p0 = xyz(s0), p1 = xyz(s1), p2 = xyz(s2);
+    f3 n0 = xyz(s3), n1 = mk(s3.w, s4.x, s4.y), n2 = mk(s4.z, s4.w, s1.w);
+    // fillIntersectionRecord<true> (skdtree.h:343-430)
+    h.p = p0 * b0 + p1 * u + p2 * v;
+    f3 side1 = p1 - p0, side2 = p2 - p0;
+    f3 fn = cross(side1, side2);
+    float l = len(fn);
+    if (!isZero(fn)) fn = fn / l;
+    f3 shn = normalize(n0 * b0 + n1 * u + n2 * v);
+    if (dot(fn, shn) < 0) fn = -fn;
+    h.geoN = fn;
+    h.shN = shn;
+    h.sh = shadingFrame(shn, side1);
+    h.wi = h.sh.toLocal(-rd);
+}
+
+// Scene::sampleEmitterDirect without the visibility test (scene.cpp:871-895 + area.cpp:158-171 +
+// shape.cpp:102-115 + trimesh.cpp:412-423 + triangle.cpp:24-45); returns radiance/pdf.
+__device__ __forceinline__ f3 sampleEmitter(const GParams &g, const SceneDev &sc, f3 ref, f3 refN, float sx, float sy,
+                                            f3 &dOut, float &dist, float &pdfOut) {
+    uint32_t ne = g.num_emitters;
+    pdfOut = 0;
+    if (ne == 0) return mk1(0.f);
+    uint32_t ei = min((uint32_t)(sx * (float)ne), ne - 1);
+    sx = sx * (float)ne - (float)ei;
+    const GEmitter em = sc.ems[ei];
+    // DiscreteDistribution::sampleReuse over the area CDF (lower_bound)
+    const float *cdf = sc.emcdf + em.cdf_begin;
+    uint32_t lo = 0, hi = em.tri_count + 1;  // first index with cdf[i] >= sy
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (cdf[mid] < sy) lo = mid + 1; else hi = mid;
+    }
+    int e = (int)lo - 1;
+    uint32_t idx = (uint32_t)min((int)em.tri_count - 1, max(0, e));
+    while (cdf[idx + 1] - cdf[idx] == 0 && idx < em.tri_count - 1) ++idx;
+    sy = (sy - cdf[idx]) / (cdf[idx + 1] - cdf[idx]);
+    const float4 *r = sc.emtri + (size_t)PG_TRI_SHADE_F4 * (em.tri_begin + idx);
+    float4 s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3], s4 = r[4];
+    f3 p0 = xyz(s0), p1 = xyz(s1), p2 = xyz(s2);
+    float a = safe_sqrt(1.0f - sx);
+    float bx = 1 - a, by = a * sy;
+    f3 sideA = p1 - p0, sideB = p2 - p0;
+    f3 p = p0 + (sideA * bx) + (sideB * by);
+    f3 n0 = xyz(s3), n1 = mk(s3.w, s4.x, s4.y), n2 = mk(s4.z, s4.w, s1.w);
+    f3 n = normalize(n0 * (1.0f - bx - by) + n1 * bx + n2 * by);
+    float pdf = em.inv_area;
+    f3 d = p - ref;
+    float distSq = dot(d, d);
+    dist = sqrtf(distSq);
+    d = d / dist;
+    float dp = absDot(d, n);
+    pdf *= dp != 0 ? (distSq / dp) : 0.0f;
+    dOut = d;
+    if (dot(d, refN) >= 0 && dot(d, n) < 0 && pdf != 0) {
+        float emPdf = 1.0f / (float)ne;
+        pdfOut = pdf * emPdf;
+        return mk(em.radiance[0], em.radiance[1], em.radiance[2]) / pdf / emPdf;
+    }
+    return mk1(0.f);
+}
+
+}  // namespace
+
+// =============================================================================================
+// camera rays: PerspectiveCamera::sampleRay (perspective.cpp:271-298) for (pixel, sample) slots
+__global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint32_t *__restrict__ local_pixels,
+                                                uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
+                                                uint32_t sample_base, uint32_t *__restrict__ queue) {
+    uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if (slot >= npix * nlayers) return;
+    uint32_t layer = slot / npix, lp = slot - layer * npix;
+    uint32_t pix = local_pixels[pix_begin + lp];
+    uint32_t sample = sample_base + layer;
+    uint32_t key = rngKey(pix, g.seed);
+    float jx, jy;
+    rng2(key, sample, 0, jx, jy);
+    float px = (float)(pix % g.width) + jx, py = (float)(pix / g.width) + jy;
+    float sx = px / (float)g.width, sy = py / (float)g.height;
+    f3 nearP = mk((1.0f - 2.0f * sx) * g.tan_half, (1.0f - 2.0f * sy) / g.aspect * g.tan_half, 1.0f);
+    f3 d = normalize(nearP);
+    float invZ = 1.0f / d.z;
+    f3 left = mk(g.cam_left[0], g.cam_left[1], g.cam_left[2]);
+    f3 up = mk(g.cam_up[0], g.cam_up[1], g.cam_up[2]);
+    f3 dir = mk(g.cam_dir[0], g.cam_dir[1], g.cam_dir[2]);
+    f3 wd = left * d.x + up * d.y + dir * d.z;
+    p.ray_o[slot] = make_float4(g.cam_o[0], g.cam_o[1], g.cam_o[2], g.near_clip * invZ);
+    p.ray_d[slot] = f4(wd, g.far_clip * invZ);
+    p.thr[slot] = make_float4(1.f, 1.f, 1.f, 1.f);
+    p.rad[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+    p.prev[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+    p.pinfo[slot] = make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u);
+    queue[slot] = slot;
+}
+
+// closest hit for every queued path: hit[slot] = (t, BVH-order triangle | ~0, u, v)
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
+                                                       const uint32_t *__restrict__ count) {
+    __shared__ uint32_t stack[STACK_DEPTH * TRACE_BLOCK];
+    uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x;
+    if (i >= *count) return;
+    uint32_t slot = queue[i];
+    float4 o = p.ray_o[slot], d = p.ray_d[slot];
+    float tmax = d.w;
+    uint32_t tri = 0xFFFFFFFFu;
+    float u = 0, v = 0;
+    bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stack + threadIdx.x);
+    p.hit[slot] = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+}
+
+// any hit for queued shadow rays; unoccluded -> add the NEE contribution to L (and to the
+// training vertex's radiance snapshot, so its record excludes light arriving from elsewhere)
+__global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
+                                                        const uint32_t *__restrict__ count) {
+    __shared__ uint32_t stack[STACK_DEPTH * TRACE_BLOCK];
+    uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x;
+    if (i >= *count) return;
+    uint32_t slot = queue[i];
+    float4 o = p.sh_o[slot], d = p.sh_d[slot];
+    float tmax = d.w;
+    uint32_t tri;
+    float u, v;
+    bool occ = traverse<true>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stack + threadIdx.x);
+    if (!occ) {
+        float4 c = p.sh_c[slot];
+        float4 L = p.rad[slot];
+        p.rad[slot] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
+        uint32_t vi = __float_as_uint(c.w);
+        if (vi != 0xFFFFFFFFu) {
+            float4 *vl = p.vtx + ((size_t)vi * p.P + slot) * 3 + 2;
+            float4 a = *vl;
+            *vl = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w);
+        }
+    }
+}
+
+// one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
+__global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, SDDev sd, PathDev p,
+                                                       const uint32_t *__restrict__ queue_in,
+                                                       const uint32_t *__restrict__ count_in,
+                                                       uint32_t *__restrict__ queue_out, uint32_t *__restrict__ count_out,
+                                                       uint32_t *__restrict__ shadow_queue,
+                                                       uint32_t *__restrict__ shadow_count) {
+    uint32_t i = blockIdx.x * SHADE_BLOCK + threadIdx.x;
+    bool alive = false, shadow = false, dirtyL = false;
+    uint32_t slot = 0;
+    f3 L = mk1(0.f);
+    if (i < *count_in) {
+        slot = queue_in[i];
+        do {
+            uint4 pi = p.pinfo[slot];
+            const uint32_t pix = pi.x, sample = pi.y;
+            uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16, nv = pi.w;
+            float4 hv = p.hit[slot];
+            float4 T4 = p.thr[slot];
+            float4 L4 = p.rad[slot];
+            f3 T = xyz(T4);
+            L = xyz(L4);
+            float eta = T4.w;
+            uint32_t tri = __float_as_uint(hv.y);
+            if (tri == 0xFFFFFFFFu) break;  // escaped: no environment emitter
+            const uint32_t key = rngKey(pix, g.seed);
+            f3 rd = xyz(p.ray_d[slot]);
+            Hit h;
+            fetchHit(sc, tri, hv.z, hv.w, rd, h);
+            f3 Le = mk1(0.f);
+            if (h.emitter >= 0 && dot(h.shN, -rd) > 0) {  // AreaLight::eval (area.cpp)
+                const GEmitter &em = sc.ems[h.emitter];
+                Le = mk(em.radiance[0], em.radiance[1], em.radiance[2]);
+            }
+            // ---- finish the previous bounce: emitter hit by the sampled direction (MIS), then RR
+            if (depth > 1) {
+                if (h.emitter >= 0) {
+                    float4 pv = p.prev[slot];
+                    float lumPdf = 0.0f;
+                    if (g.use_nee && !(flags & PF_PREV_DELTA)) {
+                        f3 prevRefN = xyz(pv);
+                        if (dot(rd, prevRefN) >= 0 && dot(rd, h.shN) < 0) {
+                            const GEmitter &em = sc.ems[h.emitter];
+                            lumPdf = em.inv_area * (hv.x * hv.x) / absDot(rd, h.shN) * (1.0f / (float)g.num_emitters);
+                        }
+                    }
+                    float w = g.use_nee ? miWeight(pv.w, lumPdf) : 1.0f;
+                    L = L + T * Le * w;
+                    dirtyL = true;
+                }
+                if (depth - 1 >= (uint32_t)g.rr_depth) {
+                    float q = fminf(maxc(T) * eta * eta, 0.95f);
+                    if (rng1(key, sample, dimOf(depth - 1, SLOT_RR)) >= q) break;
+                    T = T / q;
+                }
+            }
+            if (depth > g.depth_cap) break;
+            const GMat M = sc.mats[h.mat];
+            if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
+                L = L + T * Le;
+                dirtyL = true;
+            }
+            if ((g.max_depth > 0 && (int)depth >= g.max_depth) ||
+                (g.strict_normals && dot(rd, h.geoN) * h.wi.z >= 0))
+                break;
+            const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
+            const bool guide = g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
+            SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent,
+                      sd.built};
+            uint4 meta = make_uint4(0, 0, 0, 0);
+            if (guide) meta = sd.meta[sdLookup(sv, h.p)];
+            const float alpha = g.bsdf_fraction;
+
+            // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow
+            f3 neeC = mk1(0.f), neeD = mk1(0.f);
+            float neeDist = 0;
+            if (g.use_nee && (M.type & ESmooth)) {
+                float s0, s1;
+                rng2(key, sample, dimOf(depth, SLOT_NEE), s0, s1);
+                float emPdf;
+                f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, neeD, neeDist, emPdf);
+                if (!isZero(value)) {
+                    f3 woL = h.sh.toLocal(neeD);
+                    f3 bsdfVal = bsdfEval(M, h.wi, woL);
+                    if (!isZero(bsdfVal) && (!g.strict_normals || dot(h.geoN, neeD) * woL.z > 0)) {
+                        float bp = bsdfPdf(M, h.wi, woL);
+                        if (guide) bp = alpha * bp + (1 - alpha) * sdPdf(sv, meta, neeD);
+                        float w = miWeight(emPdf, bp);
+                        neeC = T * value * bsdfVal * w;
+                        shadow = true;
+                    }
+                }
+            }
+
+            // ---- direction sampling: BSDF, or one-sample MIS between BSDF and the D-tree
+            BS bs;
+            f3 weight;
+            float woPdf;
+            bool ok = true;
+            {
+                float b0, b1;
+                rng2(key, sample, dimOf(depth, SLOT_BSDF), b0, b1);
+                float b2 = rng1(key, sample, dimOf(depth, SLOT_COMP));
+                if (!guide) {
+                    weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+                    woPdf = bs.pdf;
+                } else if (rng1(key, sample, dimOf(depth, SLOT_GUIDE_CHOICE)) < alpha) {
+                    weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+                    if (isZero(weight)) {
+                        ok = false;
+                    } else {
+                        float dPdf = sdPdf(sv, meta, h.sh.toWorld(bs.wo));
+                        woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
+                        weight = weight * (bs.pdf / woPdf);
+                    }
+                } else {
+                    float g0, g1, dPdf, cu, cv;
+                    rng2(key, sample, dimOf(depth, SLOT_GUIDE), g0, g1);
+                    sdSampleCanon(sv, meta, g0, g1, cu, cv, dPdf);
+                    f3 dW = canonicalToDir(cu, cv);
+                    f3 woL = h.sh.toLocal(dW);
+                    f3 f = bsdfEval(M, h.wi, woL);
+                    float bp = bsdfPdf(M, h.wi, woL);
+                    woPdf = alpha * bp + (1 - alpha) * dPdf;
+                    if (!(woPdf > 0) || isZero(f)) {
+                        ok = false;
+                    } else {
+                        weight = f / woPdf;
+                        bs.wo = woL;
+                        bs.pdf = bp;
+                        bool refl = h.wi.z * woL.z > 0;
+                        bs.type = refl ? ((M.type & EDiffuseReflection) ? EDiffuseReflection : EGlossyReflection)
+                                       : EGlossyTransmission;
+                        bs.eta = refl ? 1.0f : (h.wi.z > 0 ? M.eta : M.invEta);
+                    }
+                }
+            }
+            uint32_t vtxIndex = 0xFFFFFFFFu;
+            if (ok && !isZero(weight)) {
+                if (bs.type != ENull) flags |= PF_SCATTERED;
+                f3 wo = h.sh.toWorld(bs.wo);
+                if (!(g.strict_normals && dot(h.geoN, wo) * bs.wo.z <= 0)) {
+                    f3 Tn = T * weight;
+                    // training vertex: (x, wo, woPdf, T after this bounce, L snapshot)
+                    if (g.record && !(bs.type & EDelta) && nv < (uint32_t)g.max_vertices) {
+                        float cu, cv;
+                        dirToCanonical(wo, cu, cv);
+                        float4 *vb = p.vtx + ((size_t)nv * p.P + slot) * 3;
+                        vb[0] = f4(h.p, woPdf);
+                        vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
+                        vb[2] = f4(L, 0.0f);
+                        vtxIndex = nv;
+                        nv++;
+                    }
+                    float tmin = kEpsilon * fmaxf(fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z)), kEpsilon);
+                    p.ray_o[slot] = f4(h.p, tmin);
+                    p.ray_d[slot] = f4(wo, __int_as_float(0x7f800000));
+                    p.thr[slot] = f4(Tn, eta * bs.eta);
+                    p.prev[slot] = f4(refN, woPdf);
+                    flags = (flags & ~(PF_EMITTED_QUERY | PF_PREV_DELTA)) | ((bs.type & EDelta) ? PF_PREV_DELTA : 0u);
+                    p.pinfo[slot] = make_uint4(pix, sample, (depth + 1) | (flags << 16), nv);
+                    alive = true;
+                }
+            }
+            if (shadow) {
+                float tmin = kEpsilon * fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z));
+                p.sh_o[slot] = f4(h.p, tmin);
+                p.sh_d[slot] = f4(neeD, neeDist * (1 - kShadowEpsilon));
+                p.sh_c[slot] = f4(neeC, __uint_as_float(vtxIndex));
+            }
+            if (!alive && nv != pi.w) p.pinfo[slot] = make_uint4(pix, sample, pi.z, nv);
+        } while (false);
+        if (dirtyL) p.rad[slot] = f4(L, 0.0f);
+    }
+    waveAppend(alive, slot, queue_out, count_out);
+    waveAppend(shadow, slot, shadow_queue, shadow_count);
+}
+
+// film: box-filtered accumulation of every layer's sample into its pixel, in sample order
+// (ProgressiveMonteCarloIntegrator::renderBlock clamp + ImageBlock::put validity check)
+__global__ __launch_bounds__(256) void k_film(GParams g, PathDev p, const uint32_t *__restrict__ local_pixels,
+                                              uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
+                                              float4 *__restrict__ film, float4 *__restrict__ sumsq) {
+    uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
+    if (lp >= npix) return;
+    uint32_t pix = local_pixels[pix_begin + lp];
+    float4 a = film[pix], q = sumsq[pix];
+    for (uint32_t l = 0; l < nlayers; ++l) {
+        float4 L = p.rad[(size_t)l * npix + lp];
+        float m = fmaxf(L.x, fmaxf(L.y, L.z));
+        if (m > g.max_component_value) {
+            float s = g.max_component_value / m;
+            L.x *= s;
+            L.y *= s;
+            L.z *= s;
+        }
+        bool okv = isfinite(L.x) && isfinite(L.y) && isfinite(L.z) && L.x >= 0 && L.y >= 0 && L.z >= 0;
+        if (!okv) continue;
+        a.x += L.x;
+        a.y += L.y;
+        a.z += L.z;
+        a.w += 1.0f;
+        q.x += L.x * L.x;
+        q.y += L.y * L.y;
+        q.z += L.z * L.z;
+    }
+    film[pix] = a;
+    sumsq[pix] = q;
+}
+
+// training records of finished paths: radiance along wo_i = (L_final - L_i) / T_i (channel-wise)
+__global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int maxV, pg_record *__restrict__ recs,
+                                                unsigned long long *__restrict__ rec_count,
+                                                unsigned long long capacity) {
+    uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nv = 0;
+    if (slot < nslots) nv = min(p.pinfo[slot].w, (uint32_t)maxV);
+    // wave inclusive scan of nv
+    int lane = threadIdx.x & 63;
+    uint32_t incl = nv;
+    for (int off = 1; off < 64; off <<= 1) {
+        uint32_t y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+    }
+    uint32_t total = __shfl(incl, 63);
+    unsigned long long base = 0;
+    if (lane == 63 && total) base = atomicAdd(rec_count, (unsigned long long)total);
+    base = __shfl(base, 63);
+    if (nv == 0) return;
+    unsigned long long o = base + (incl - nv);
+    float4 L = p.rad[slot];
+    for (uint32_t k = 0; k < nv; ++k, ++o) {
+        if (o >= capacity) return;
+        const float4 *vb = p.vtx + ((size_t)k * p.P + slot) * 3;
+        float4 a = vb[0], b = vb[1], c = vb[2];
+        float woPdf = a.w;
+        float lr = (b.x * woPdf > 1e-4f) ? (L.x - c.x) / b.x : 0.0f;
+        float lg = (b.y * woPdf > 1e-4f) ? (L.y - c.y) / b.y : 0.0f;
+        float lb = (b.z * woPdf > 1e-4f) ? (L.z - c.z) / b.z : 0.0f;
+        pg_record r;
+        r.pos[0] = a.x;
+        r.pos[1] = a.y;
+        r.pos[2] = a.z;
+        r.dir = __float_as_uint(b.w);
+        r.radiance = (lr + lg + lb) * (1.0f / 3.0f);
+        r.wo_pdf = woPdf;
+        r.product = 0.0f;
+        r.weight = 1.0f;
+        float4 *dst = reinterpret_cast<float4 *>(recs + o);
+        dst[0] = make_float4(r.pos[0], r.pos[1], r.pos[2], __uint_as_float(r.dir));
+        dst[1] = make_float4(r.radiance, r.wo_pdf, r.product, r.weight);
+    }
+}
+
+// SD-tree splat: records -> building-tree leaf quadrants (2^-24 fixed point, u64 atomics)
+__global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__restrict__ recs, unsigned long long n) {
+    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float4 *src = reinterpret_cast<const float4 *>(recs + i);
+    float4 a = src[0], b = src[1];
+    float woPdf = b.y;
+    if (!(woPdf > 0)) return;
+    float val;
+    {
+#pragma clang fp contract(off)
+        val = b.x / woPdf;
+    }
+    if (!(val >= 0) || !(val < 1e30f)) return;
+    float s = val * 16777216.0f;
+    if (s >= 4.0e18f) s = 4.0e18f;
+    unsigned long long fx = (unsigned long long)s;
+    SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent, sd.built};
+    uint32_t dt = sdLookup(sv, mk(a.x, a.y, a.z));
+    atomicAdd(sd.count + dt, 1u);
+    uint32_t dirw = __float_as_uint(a.w);
+    float u = ((float)(dirw & 0xFFFFu) + 0.5f) * (1.0f / 65536.0f);
+    float v = ((float)(dirw >> 16) + 0.5f) * (1.0f / 65536.0f);
+    uint32_t node = sd.meta[dt].y;
+    for (int guard = 0; guard < 64; ++guard) {
+        int q = childIndex(u, v);
+        uint32_t c = c4(sd.bchild[node], q);
+        if (c == 0) {
+            atomicAdd(sd.bsum + 4 * (size_t)node + q, fx);
+            break;
+        }
+        node = c;
+    }
+}
+
+// ---- unit-level kernels used by the parity tests ---------------------------------------------
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const float *__restrict__ rays, uint32_t n,
+                                                            int any, float *__restrict__ hits) {
+    __shared__ uint32_t stack[STACK_DEPTH * TRACE_BLOCK];
+    uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const float *r = rays + 8 * (size_t)i;
+    f3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
+    float tmax = r[7];
+    uint32_t tri = 0xFFFFFFFFu;
+    float u = 0, v = 0;
+    float *h = hits + 4 * (size_t)i;
+    if (any) {
+        bool occ = traverse<true>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stack + threadIdx.x);
+        h[0] = occ ? 1.0f : 0.0f;
+        h[1] = h[2] = h[3] = 0.0f;
+        return;
+    }
+    bool hit = traverse<false>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stack + threadIdx.x);
+    uint32_t orig = hit ? __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w) : 0xFFFFFFFFu;
+    h[0] = hit ? tmax : 0.0f;
+    h[1] = __uint_as_float(orig);
+    h[2] = u;
+    h[3] = v;
+}
+
+__global__ __launch_bounds__(256) void k_bsdf_query(const GMat *mat, const float *wi, const float *u, const float *wog,
+                                                    uint32_t n, float *out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GMat M = *mat;
+    f3 w = mk(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]);
+    BS bs;
+    f3 wt = bsdfSample(M, w, u[3 * i], u[3 * i + 1], u[3 * i + 2], bs);
+    float *o = out + 12 * (size_t)i;
+    bool z = isZero(wt);
+    o[0] = bs.wo.x;
+    o[1] = bs.wo.y;
+    o[2] = bs.wo.z;
+    o[3] = z ? 0.0f : bs.pdf;
+    o[4] = wt.x;
+    o[5] = wt.y;
+    o[6] = wt.z;
+    o[7] = z ? 0.0f : (float)bs.type;
+    if (wog) {
+        f3 g = mk(wog[3 * i], wog[3 * i + 1], wog[3 * i + 2]);
+        f3 e = bsdfEval(M, w, g);
+        o[8] = e.x;
+        o[9] = e.y;
+        o[10] = e.z;
+        o[11] = bsdfPdf(M, w, g);
+    } else {
+        o[8] = o[9] = o[10] = o[11] = 0.0f;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sd_pdf(SDDev sd, const float *pos, const float *dir, uint32_t n, float *out) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent, sd.built};
+    uint4 meta = sd.meta[sdLookup(sv, mk(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]))];
+    out[i] = sdPdf(sv, meta, mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]));
+}
+
+__global__ __launch_bounds__(256) void k_sd_sample(SDDev sd, const float *pos, const float *u, uint32_t n, float *dir,
+                                                   float *pdf) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent, sd.built};
+    uint4 meta = sd.meta[sdLookup(sv, mk(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]))];
+    float cu, cv, pd;
+    sdSampleCanon(sv, meta, u[2 * i], u[2 * i + 1], cu, cv, pd);
+    f3 d = canonicalToDir(cu, cv);
+    dir[3 * i] = d.x;
+    dir[3 * i + 1] = d.y;
+    dir[3 * i + 2] = d.z;
+    pdf[i] = pd;
+}
+
+// =============================================================================================
+static inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
+
+void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
+                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, uint32_t *queue) {
+    uint64_t n = (uint64_t)npix * nlayers;
+    if (!n) return;
+    hipLaunchKernelGGL(k_camera, dim3(blocks(n, 256)), dim3(256), 0, s, g, p, local_pixels, pix_begin, npix, nlayers,
+                       sample_base, queue);
+}
+void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
+                     uint32_t max_count) {
+    if (!max_count) return;
+    hipLaunchKernelGGL(k_trace, dim3(blocks(max_count, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
+}
+void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
+                     const uint32_t *queue_in, const uint32_t *count_in, uint32_t max_count, uint32_t *queue_out,
+                     uint32_t *count_out, uint32_t *shadow_queue, uint32_t *shadow_count) {
+    if (!max_count) return;
+    hipLaunchKernelGGL(k_shade, dim3(blocks(max_count, SHADE_BLOCK)), dim3(SHADE_BLOCK), 0, s, g, sc, sd, p, queue_in,
+                       count_in, queue_out, count_out, shadow_queue, shadow_count);
+}
+void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
+                      uint32_t max_count) {
+    if (!max_count) return;
+    hipLaunchKernelGGL(k_shadow, dim3(blocks(max_count, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
+}
+void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
+                    uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq) {
+    if (!npix) return;
+    hipLaunchKernelGGL(k_film, dim3(blocks(npix, 256)), dim3(256), 0, s, g, p, local_pixels, pix_begin, npix, nlayers,
+                       film_rgbw, film_sumsq);
+}
+void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
+                      unsigned long long *rec_count, unsigned long long rec_capacity) {
+    if (!nslots) return;
+    hipLaunchKernelGGL(k_commit, dim3(blocks(nslots, 256)), dim3(256), 0, s, p, nslots, max_vertices, records, rec_count,
+                       rec_capacity);
+}
+void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_splat, dim3(blocks(n, 256)), dim3(256), 0, s, sd, recs, n);
+}
+void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_trace_rays, dim3(blocks(n, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, rays, n, any, hits);
+}
+void pg_launch_bsdf_query(hipStream_t s, const GMat *mat, const float *wi, const float *u, const float *wog, uint32_t n,
+                          float *out) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_bsdf_query, dim3(blocks(n, 256)), dim3(256), 0, s, mat, wi, u, wog, n, out);
+}
+void pg_launch_sd_pdf(hipStream_t s, const SDDev &sd, const float *pos, const float *dir, uint32_t n, float *out) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_sd_pdf, dim3(blocks(n, 256)), dim3(256), 0, s, sd, pos, dir, n, out);
+}
+void pg_launch_sd_sample(hipStream_t s, const SDDev &sd, const float *pos, const float *u, uint32_t n, float *dir,
+                         float *pdf) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_sd_sample, dim3(blocks(n, 256)), dim3(256), 0, s, sd, pos, u, n, dir, pdf);
+}

@@ -1,0 +1,64 @@
+// GPU record layouts shared by the host driver (pg_host.cpp) and the kernels (pg_kernels.hip).
+// Sizes are static_asserted; DESIGN.md §"Data layout in HBM" documents them.
+#pragma once
+#include <stdint.h>
+
+#include "../../include/pg_capi.h"
+
+// Material record: 128 B (8 x 16 B), derived constants precomputed on the host (BSDF::configure()).
+struct GMat {
+    uint32_t model, dist, flags, type;  // pg BSDF model, microfacet distribution, PG_MAT_* flags, EBSDFType bits
+    float alpha_u, alpha_v, eta, invEta;
+    float invEta2, fdrInt, specWeight, pad0;
+    float diff[4];
+    float spec[4];
+    float trans[4];
+    float ceta[4];
+    float ck[4];
+};
+static_assert(sizeof(GMat) == 128, "GMat layout");
+
+// Area emitter record: 32 B.  Triangles of emitter e are em_tri[tri_begin, tri_begin + tri_count),
+// each with its normalized area-CDF entry em_cdf[tri_begin + 1 + i] (em_cdf[tri_begin] = 0 slot
+// lives at index tri_begin + e, see pg_host.cpp: cdf arrays are stored with one leading zero each).
+struct GEmitter {
+    uint32_t tri_begin;   // into em_tri
+    uint32_t tri_count;
+    uint32_t cdf_begin;   // into em_cdf (tri_count + 1 entries)
+    float inv_area;
+    float radiance[4];
+};
+static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
+
+// Per-triangle shading record (5 x float4 = 80 B), indexed by BVH-order triangle id:
+//   [0] p0.xyz, bits(material | (emitter + 1) << 16)
+//   [1] p1.xyz, n2.z
+//   [2] p2.xyz, bits(original triangle id)
+//   [3] n0.xyz, n1.x
+//   [4] n1.y, n1.z, n2.x, n2.y
+// The same layout is used for the compact emitter-triangle array.
+#define PG_TRI_SHADE_F4 5
+
+// BVH2 node (4 x float4 = 64 B):
+//   [0] c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y   [1] c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y
+//   [2] c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z   [3] bits(child0), bits(child1), 0, 0
+// child >= 0: inner node index; child < 0: leaf, ~child = (first_tri << 4) | count (count <= 15).
+#define PG_BVH_NODE_F4 4
+#define PG_LEAF_MAX 8
+
+// Path-state flags (pinfo.z high bits)
+#define PF_SCATTERED 0x1u
+#define PF_EMITTED_QUERY 0x2u
+#define PF_PREV_DELTA 0x4u
+
+// Kernel-side constants of one render context.
+struct GParams {
+    // camera
+    float cam_o[3], cam_left[3], cam_up[3], cam_dir[3];
+    float tan_half, aspect, near_clip, far_clip;
+    uint32_t width, height;
+    // integrator
+    int32_t max_depth, rr_depth, use_nee, hide_emitters, strict_normals, guiding, record, max_vertices;
+    float max_component_value, bsdf_fraction;
+    uint32_t seed, num_emitters, num_materials, depth_cap;
+};

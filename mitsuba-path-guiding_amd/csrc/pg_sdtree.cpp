@@ -1,0 +1,262 @@
+// SD-tree host refit + wire format (see pg_sdtree.h and DESIGN.md §"SD-tree").
+#include "pg_sdtree.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+namespace pgh {
+namespace {
+
+constexpr uint32_t kMagic = 0x44534750u;  // 'PGSD'
+constexpr uint32_t kLeafMark = 0xFFFFFFFFu;
+
+inline float fixedToFloat(uint64_t x) { return (float)std::ldexp((double)x, -24); }
+inline float total4(const float *s) { return ((s[0] + s[1]) + s[2]) + s[3]; }
+
+// bottom-up quadrant sums of a building tree (integer, exact)
+uint64_t propagate(std::vector<SdNodeB> &b, uint32_t n) {
+    uint64_t tot = 0;
+    for (int q = 0; q < 4; ++q) {
+        if (b[n].child[q]) b[n].sum[q] = propagate(b, b[n].child[q]);
+        tot += b[n].sum[q];
+    }
+    return tot;
+}
+
+// New building topology: refine every quadrant of the (just built) tree whose energy fraction
+// exceeds rho, below max_depth; quadrants of leaves keep refining with sum/4 estimates.
+void rebuildTopology(SdLeaf &L, int maxDepth, float rho) {
+    struct Tmp { float s[4]; uint32_t c[4]; };
+    std::vector<Tmp> nodes(1, Tmp{{0, 0, 0, 0}, {0, 0, 0, 0}});
+    struct Item { uint32_t dst; uint32_t src; bool prev; int depth; };
+    std::vector<Item> stack{{0, 0, true, 1}};
+    const float total = L.total;
+    while (!stack.empty()) {
+        Item it = stack.back();
+        stack.pop_back();
+        float ss[4];
+        uint32_t sc[4];
+        if (it.prev) {
+            for (int q = 0; q < 4; ++q) {
+                ss[q] = L.sampling[it.src].sum[q];
+                sc[q] = L.sampling[it.src].child[q];
+            }
+        } else {
+            for (int q = 0; q < 4; ++q) {
+                ss[q] = nodes[it.src].s[q];
+                sc[q] = 0;
+            }
+        }
+        for (int q = 0; q < 4; ++q) {
+            float frac = total > 0 ? (ss[q] / total) : std::pow(0.25f, (float)it.depth);
+            if (!(it.depth < maxDepth && frac > rho)) continue;
+            uint32_t c = (uint32_t)nodes.size();
+            nodes[it.dst].c[q] = c;
+            Tmp t;
+            for (int k = 0; k < 4; ++k) {
+                t.s[k] = ss[q] / 4;
+                t.c[k] = 0;
+            }
+            nodes.push_back(t);
+            if (it.prev && sc[q]) stack.push_back({c, sc[q], true, it.depth + 1});
+            else stack.push_back({c, c, false, it.depth + 1});
+        }
+    }
+    L.building.assign(nodes.size(), SdNodeB{});
+    for (size_t i = 0; i < nodes.size(); ++i)
+        for (int q = 0; q < 4; ++q) L.building[i].child[q] = nodes[i].c[q];
+    L.count = 0;
+}
+
+}  // namespace
+
+void SdTree::reset(const float bmin[3], const float bmax[3]) {
+    float m = std::max(bmax[0] - bmin[0], std::max(bmax[1] - bmin[1], bmax[2] - bmin[2]));
+    for (int a = 0; a < 3; ++a) lo[a] = bmin[a];
+    extent = m;
+    snode = {kLeafMark, 0u};
+    leaves.assign(1, SdLeaf{});
+    built = false;
+}
+
+void SdTree::refit(uint32_t iteration, float sThreshold, float rho, int maxDepth) {
+    // 1. build: building -> sampling (fp32 from the exact integer sums)
+    for (SdLeaf &L : leaves) {
+        propagate(L.building, 0);
+        L.sampling.assign(L.building.size(), SdNodeS{});
+        for (size_t i = 0; i < L.building.size(); ++i)
+            for (int q = 0; q < 4; ++q) {
+                L.sampling[i].sum[q] = fixedToFloat(L.building[i].sum[q]);
+                L.sampling[i].child[q] = L.building[i].child[q];
+            }
+        L.total = total4(L.sampling[0].sum);
+    }
+    // 2. refine the S-tree: split leaves whose record count exceeds c * sqrt(2^k); children copy
+    //    the D-trees and halve the count; recursion continues into the children (DFS, child0 first)
+    const double thr = (double)sThreshold * std::sqrt(std::pow(2.0, (double)iteration));
+    std::vector<uint32_t> stack{0};
+    while (!stack.empty()) {
+        uint32_t n = stack.back();
+        stack.pop_back();
+        if (snode[2 * n] == kLeafMark && (double)leaves[snode[2 * n + 1]].count > thr) {
+            uint32_t l0 = snode[2 * n + 1];
+            leaves[l0].count /= 2;
+            uint32_t l1 = (uint32_t)leaves.size();
+            leaves.push_back(leaves[l0]);
+            uint32_t c0 = (uint32_t)(snode.size() / 2);
+            snode.push_back(kLeafMark);
+            snode.push_back(l0);
+            snode.push_back(kLeafMark);
+            snode.push_back(l1);
+            snode[2 * n] = c0;
+            snode[2 * n + 1] = c0 + 1;
+        }
+        if (snode[2 * n] != kLeafMark) {
+            stack.push_back(snode[2 * n + 1]);
+            stack.push_back(snode[2 * n]);
+        }
+    }
+    // 3. reset the building trees
+    for (SdLeaf &L : leaves) rebuildTopology(L, maxDepth, rho);
+    built = true;
+}
+
+size_t SdTree::samplingNodes() const {
+    size_t n = 0;
+    for (auto &L : leaves) n += L.sampling.size();
+    return n;
+}
+size_t SdTree::buildingNodes() const {
+    size_t n = 0;
+    for (auto &L : leaves) n += L.building.size();
+    return n;
+}
+
+void SdTree::flatten(Flat &f) const {
+    f.snodes = snode;
+    f.meta.assign(4 * leaves.size(), 0);
+    size_t ns = samplingNodes(), nb = buildingNodes();
+    f.qsum.assign(4 * ns, 0.0f);
+    f.qchild.assign(4 * ns, 0);
+    f.bchild.assign(4 * nb, 0);
+    f.bsum.assign(4 * nb, 0);
+    f.count.assign(leaves.size(), 0);
+    uint32_t sb = 0, bb = 0;
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        const SdLeaf &L = leaves[i];
+        f.meta[4 * i + 0] = sb;
+        f.meta[4 * i + 1] = bb;
+        f.meta[4 * i + 2] = L.count;
+        std::memcpy(&f.meta[4 * i + 3], &L.total, 4);
+        for (size_t k = 0; k < L.sampling.size(); ++k)
+            for (int q = 0; q < 4; ++q) {
+                f.qsum[4 * (sb + k) + q] = L.sampling[k].sum[q];
+                f.qchild[4 * (sb + k) + q] = L.sampling[k].child[q] ? L.sampling[k].child[q] + sb : 0;
+            }
+        for (size_t k = 0; k < L.building.size(); ++k)
+            for (int q = 0; q < 4; ++q) {
+                f.bchild[4 * (bb + k) + q] = L.building[k].child[q] ? L.building[k].child[q] + bb : 0;
+                f.bsum[4 * (bb + k) + q] = L.building[k].sum[q];
+            }
+        f.count[i] = L.count;
+        sb += (uint32_t)L.sampling.size();
+        bb += (uint32_t)L.building.size();
+    }
+}
+
+void SdTree::absorb(const std::vector<uint64_t> &bsum, const std::vector<uint32_t> &count) {
+    size_t bb = 0;
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        SdLeaf &L = leaves[i];
+        for (size_t k = 0; k < L.building.size(); ++k)
+            for (int q = 0; q < 4; ++q) L.building[k].sum[q] = bsum[4 * (bb + k) + q];
+        L.count = count[i];
+        bb += L.building.size();
+    }
+}
+
+// Wire format (little endian), shared with the oracle's golden vectors:
+//   u32 magic 'PGSD', u32 version 1, u32 built, u32 0
+//   f32 lo.xyz, 0, hi.xyz, 0            (cube)
+//   u32 num_snodes, num_dtrees, num_sampling_nodes, num_building_nodes
+//   num_snodes x {u32 child0, u32 child1}
+//   num_dtrees x {u32 sampling_base, building_base, sampling_count, building_count, f32 total, u32 count, 0, 0}
+//   sampling nodes x {f32 sum[4], u32 child[4] (absolute, 0 = leaf)}
+//   building nodes x {u64 sum[4], u32 child[4] (absolute, 0 = leaf)}
+std::vector<uint8_t> SdTree::serialize() const {
+    std::vector<uint8_t> out;
+    auto put = [&](const void *p, size_t n) {
+        const uint8_t *b = (const uint8_t *)p;
+        out.insert(out.end(), b, b + n);
+    };
+    uint32_t hdr[4] = {kMagic, 1u, built ? 1u : 0u, 0u};
+    put(hdr, 16);
+    float box[8] = {lo[0], lo[1], lo[2], extent, lo[0] + extent, lo[1] + extent, lo[2] + extent, 0};
+    put(box, 32);
+    Flat f;
+    flatten(f);
+    uint32_t cnt[4] = {(uint32_t)(snode.size() / 2), (uint32_t)leaves.size(), (uint32_t)(f.qsum.size() / 4),
+                       (uint32_t)(f.bchild.size() / 4)};
+    put(cnt, 16);
+    put(snode.data(), 4 * snode.size());
+    for (size_t i = 0; i < leaves.size(); ++i) {
+        uint32_t m[8] = {f.meta[4 * i], f.meta[4 * i + 1], (uint32_t)leaves[i].sampling.size(),
+                         (uint32_t)leaves[i].building.size(), f.meta[4 * i + 3], leaves[i].count, 0, 0};
+        put(m, 32);
+    }
+    for (size_t k = 0; k < f.qsum.size() / 4; ++k) {
+        put(&f.qsum[4 * k], 16);
+        put(&f.qchild[4 * k], 16);
+    }
+    for (size_t k = 0; k < f.bchild.size() / 4; ++k) {
+        put(&f.bsum[4 * k], 32);
+        put(&f.bchild[4 * k], 16);
+    }
+    return out;
+}
+
+bool SdTree::deserialize(const uint8_t *p, size_t n) {
+    size_t off = 0;
+    auto get = [&](void *d, size_t k) {
+        if (off + k > n) return false;
+        std::memcpy(d, p + off, k);
+        off += k;
+        return true;
+    };
+    uint32_t hdr[4], cnt[4];
+    float box[8];
+    if (!get(hdr, 16) || hdr[0] != kMagic || hdr[1] != 1 || !get(box, 32) || !get(cnt, 16)) return false;
+    built = hdr[2] != 0;
+    for (int a = 0; a < 3; ++a) lo[a] = box[a];
+    extent = box[3];
+    snode.assign(2 * (size_t)cnt[0], 0);
+    if (!get(snode.data(), 8 * (size_t)cnt[0])) return false;
+    leaves.assign(cnt[1], SdLeaf{});
+    std::vector<uint32_t> sb(cnt[1]), bb(cnt[1]);
+    for (uint32_t i = 0; i < cnt[1]; ++i) {
+        uint32_t m[8];
+        if (!get(m, 32)) return false;
+        sb[i] = m[0];
+        bb[i] = m[1];
+        leaves[i].sampling.assign(m[2], SdNodeS{});
+        leaves[i].building.assign(m[3], SdNodeB{});
+        std::memcpy(&leaves[i].total, &m[4], 4);
+        leaves[i].count = m[5];
+    }
+    for (uint32_t i = 0; i < cnt[1]; ++i)
+        for (auto &nd : leaves[i].sampling) {
+            if (!get(nd.sum, 16) || !get(nd.child, 16)) return false;
+            for (int q = 0; q < 4; ++q)
+                if (nd.child[q]) nd.child[q] -= sb[i];
+        }
+    for (uint32_t i = 0; i < cnt[1]; ++i)
+        for (auto &nd : leaves[i].building) {
+            if (!get(nd.sum, 32) || !get(nd.child, 16)) return false;
+            for (int q = 0; q < 4; ++q)
+                if (nd.child[q]) nd.child[q] -= bb[i];
+        }
+    return off == n;
+}
+
+}  // namespace pgh

@@ -1,0 +1,58 @@
+// Host side of the SD-tree (Mueller et al. 2017): the topology refit that runs in the
+// postprogression slot (src/librender/progressiveintegrator.cpp:314-317) and the flat device
+// layout it uploads.  The per-sample work (lookup, sample, pdf, splat) runs on the GPU
+// (pg_device.h / pg_kernels.hip); this refit is a few ms per training iteration on the host.
+// Spec: DESIGN.md §"SD-tree" (restated from the paper; parity unpinned against the reference,
+// which does not contain the guiding code).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+namespace pgh {
+
+struct SdNodeS {  // sampling quadtree node
+    float sum[4] = {0, 0, 0, 0};
+    uint32_t child[4] = {0, 0, 0, 0};  // tree-local, 0 = leaf
+};
+struct SdNodeB {  // building quadtree node
+    uint64_t sum[4] = {0, 0, 0, 0};    // 2^-24 fixed point
+    uint32_t child[4] = {0, 0, 0, 0};
+};
+struct SdLeaf {  // D-tree pair attached to one S-tree leaf
+    std::vector<SdNodeS> sampling{SdNodeS{}};
+    float total = 0;
+    std::vector<SdNodeB> building{SdNodeB{}};
+    uint32_t count = 0;
+};
+
+struct SdTree {
+    float lo[3] = {0, 0, 0}, extent = 1;
+    std::vector<uint32_t> snode;  // 2 words per node: child0 (0xFFFFFFFF = leaf), child1 / leaf index
+    std::vector<SdLeaf> leaves;
+    bool built = false;
+
+    void reset(const float bmin[3], const float bmax[3]);
+    void refit(uint32_t iteration, float s_threshold, float rho, int max_depth);
+    std::vector<uint8_t> serialize() const;
+    bool deserialize(const uint8_t *p, size_t n);
+
+    // flat views for upload
+    struct Flat {
+        std::vector<uint32_t> snodes;   // 2 per node
+        std::vector<uint32_t> meta;     // 4 per leaf
+        std::vector<float> qsum;        // 4 per sampling node
+        std::vector<uint32_t> qchild;   // 4 per sampling node (absolute)
+        std::vector<uint32_t> bchild;   // 4 per building node (absolute)
+        std::vector<uint64_t> bsum;     // 4 per building node
+        std::vector<uint32_t> count;    // per leaf
+    };
+    void flatten(Flat &f) const;
+    // absorb device-side building sums/counts (same absolute layout as flatten())
+    void absorb(const std::vector<uint64_t> &bsum, const std::vector<uint32_t> &count);
+    size_t samplingNodes() const;
+    size_t buildingNodes() const;
+};
+
+}  // namespace pgh

@@ -1,0 +1,282 @@
+"""Host-side mirror of the reference's progressive integrator plugin surface, over the C-ABI.
+
+    reference                                              here
+    -----------------------------------------------------  ---------------------------------------
+    ProgressiveMIPathTracer (progressive_path.cpp:89-124)   ProgressivePathTracer
+    <guided progressive path tracer> (absent)     GuidedPathTracer
+    Integrator::preprocess (integrator.h:61)                .preprocess(scene)
+    ProgressiveMonteCarloIntegrator::render (progressive-   .render()
+      integrator.cpp:170-220) / renderSamples (:65-114)
+    preprogression / postprogression (:308-317)             .preprogression() / .postprogression()
+    Integrator::cancel (integrator.h:84)                    .cancel()  (thread-safe)
+    Integrator::postprocess (integrator.h:96)               .postprocess()
+
+Properties use the reference's XML names (maxDepth, rrDepth, strictNormals, hideEmitters, useNee,
+samplesPerProgression, maxComponentValue; guiding: trainingIterations, sTreeThreshold,
+dTreeThreshold, bsdfSamplingFraction).  Errors raise RuntimeError with pg_last_error(), like
+Log(EError, ...) throws in Mitsuba.  There is no CPU fallback: without libpgamd.so or a gfx950
+device every entry point raises.
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import capi
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def library():
+    global _lib
+    with _lib_lock:
+        if _lib is None:
+            _lib = capi.load_library()
+    return _lib
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class PGError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__(f"pg status {status}: {msg}")
+        self.status = status
+
+
+class Device:
+    """One pg_ctx: a render context bound to one HIP device and one image-tile shard."""
+
+    def __init__(self, config=None, **overrides):
+        self.lib = library()
+        self.cfg = config if config is not None else capi.default_config(**overrides)
+        h = C.c_void_p()
+        st = self.lib.pg_create(C.byref(self.cfg), C.byref(h))
+        if st != capi.PG_OK:
+            raise PGError(st, self.lib.pg_last_error(None).decode())
+        self.h = h
+        self.scene = None
+
+    def _chk(self, st):
+        if st != capi.PG_OK:
+            raise PGError(st, self.lib.pg_last_error(self.h).decode())
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- scene / passes
+    def upload(self, scene):
+        self.scene = scene
+        self._chk(self.lib.pg_upload_scene(self.h, C.byref(scene.desc())))
+
+    def render_pass(self, spp, sample_offset=0, record=False):
+        self._chk(self.lib.pg_render_pass(self.h, spp, sample_offset, int(bool(record))))
+
+    def cancel(self):
+        self._chk(self.lib.pg_cancel(self.h))
+
+    # -- records / SD-tree
+    def record_count(self):
+        n = C.c_uint64()
+        self._chk(self.lib.pg_get_record_count(self.h, C.byref(n)))
+        return n.value
+
+    def get_records(self, dst_ptr=None, max_records=None):
+        """Host copy (np.uint8 view, 32 B per record), or copy into a device pointer."""
+        n = self.record_count() if max_records is None else max_records
+        w = C.c_uint64()
+        if dst_ptr is not None:
+            self._chk(self.lib.pg_get_records(self.h, C.c_void_p(dst_ptr), n, 1, C.byref(w)))
+            return w.value
+        buf = np.zeros(n * 32, np.uint8)
+        self._chk(self.lib.pg_get_records(self.h, _p(buf), n, 0, C.byref(w)))
+        return buf[: w.value * 32]
+
+    def splat_records(self, recs=None, device_ptr=None, count=None):
+        if device_ptr is not None:
+            self._chk(self.lib.pg_splat_records(self.h, C.c_void_p(device_ptr), count, 1))
+        else:
+            recs = np.ascontiguousarray(recs, np.uint8)
+            self._chk(self.lib.pg_splat_records(self.h, _p(recs), len(recs) // 32, 0))
+
+    def splat_local(self):
+        self._chk(self.lib.pg_splat_local_records(self.h))
+
+    def refit(self, iteration):
+        self._chk(self.lib.pg_refit(self.h, iteration))
+
+    def get_sdtree(self):
+        n = C.c_uint64()
+        self._chk(self.lib.pg_get_sdtree(self.h, None, 0, C.byref(n)))
+        buf = np.zeros(n.value, np.uint8)
+        self._chk(self.lib.pg_get_sdtree(self.h, _p(buf), n.value, C.byref(n)))
+        return buf
+
+    def put_sdtree(self, blob):
+        blob = np.ascontiguousarray(blob, np.uint8)
+        self._chk(self.lib.pg_put_sdtree(self.h, _p(blob), len(blob)))
+
+    def sdtree_pdf(self, pos, d):
+        pos = np.ascontiguousarray(pos, np.float32)
+        d = np.ascontiguousarray(d, np.float32)
+        out = np.zeros(len(pos), np.float32)
+        self._chk(self.lib.pg_sdtree_pdf(self.h, _p(pos), _p(d), len(pos), _p(out)))
+        return out
+
+    def sdtree_sample(self, pos, u):
+        pos = np.ascontiguousarray(pos, np.float32)
+        u = np.ascontiguousarray(u, np.float32)
+        d = np.zeros((len(pos), 3), np.float32)
+        pdf = np.zeros(len(pos), np.float32)
+        self._chk(self.lib.pg_sdtree_sample(self.h, _p(pos), _p(u), len(pos), _p(d), _p(pdf)))
+        return d, pdf
+
+    # -- film / stats
+    def read_film(self):
+        W, H = self.scene.width, self.scene.height
+        rgbw = np.zeros((H, W, 4), np.float32)
+        sq = np.zeros((H, W, 4), np.float32)
+        self._chk(self.lib.pg_read_film(self.h, _p(rgbw), _p(sq)))
+        return rgbw, sq
+
+    def reset_film(self):
+        self._chk(self.lib.pg_reset_film(self.h))
+
+    def stats(self):
+        s = capi.pg_stats()
+        self._chk(self.lib.pg_get_stats(self.h, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in capi.pg_stats._fields_}
+
+    def local_pixel_count(self):
+        n = C.c_uint64()
+        self._chk(self.lib.pg_local_pixel_count(self.h, C.byref(n)))
+        return n.value
+
+    # -- unit-level queries
+    def trace_rays(self, rays, any_hit=False):
+        rays = np.ascontiguousarray(rays, np.float32)
+        hits = np.zeros((len(rays), 4), np.float32)
+        self._chk(self.lib.pg_trace_rays(self.h, _p(rays), len(rays), int(any_hit), _p(hits)))
+        return hits
+
+    def bsdf_query(self, material, wi, u, wo_given=None):
+        wi = np.ascontiguousarray(wi, np.float32)
+        u = np.ascontiguousarray(u, np.float32)
+        wg = None if wo_given is None else np.ascontiguousarray(wo_given, np.float32)
+        out = np.zeros((len(wi), 12), np.float32)
+        self._chk(self.lib.pg_bsdf_query(self.h, material, _p(wi), _p(u), _p(wg), len(wi), _p(out)))
+        return out
+
+
+class ProgressivePathTracer:
+    """Mirror of ProgressiveMIPathTracer: plain (unguided) progressive path tracing on the GPU."""
+
+    guided = False
+
+    def __init__(self, props=None, device=0, rank=0, world_size=1):
+        props = dict(props or {})
+        self.props = props
+        self.cfg = capi.default_config(
+            device=device, rank=rank, world_size=world_size,
+            max_depth=int(props.get("maxDepth", -1)), rr_depth=int(props.get("rrDepth", 5)),
+            strict_normals=int(bool(props.get("strictNormals", False))),
+            hide_emitters=int(bool(props.get("hideEmitters", False))),
+            use_nee=int(bool(props.get("useNee", True))),
+            max_component_value=float(props.get("maxComponentValue", float("inf"))),
+            seed=int(props.get("seed", 1337)), guiding=int(self.guided),
+            bsdf_sampling_fraction=float(props.get("bsdfSamplingFraction", 0.5)),
+            s_tree_threshold=float(props.get("sTreeThreshold", 12000.0)),
+            d_tree_threshold=float(props.get("dTreeThreshold", 0.01)),
+            max_paths_in_flight=int(props.get("maxPathsInFlight", 0)))
+        self.spp_per_progression = int(props.get("samplesPerProgression", 1))
+        self.dev = None
+        self.progression = 0
+        self.sample_offset = 0
+        self._cancel = threading.Event()
+
+    def preprocess(self, scene):
+        self.dev = Device(self.cfg)
+        self.dev.upload(scene)
+        self.progression = 0
+        self.sample_offset = 0
+        return True
+
+    def preprogression(self):
+        self.progression += 1
+
+    def postprogression(self):
+        pass
+
+    def render_progression(self, spp, record=False):
+        self.preprogression()
+        self.dev.render_pass(spp, self.sample_offset, record)
+        self.sample_offset += spp
+        self.postprogression()
+
+    def render(self, spp):
+        """renderSamples: spp / samplesPerProgression progressions; returns (rgbw, sumsq)."""
+        passes = max(1, spp // self.spp_per_progression)
+        for _ in range(passes):
+            if self._cancel.is_set():
+                return None
+            self.render_progression(self.spp_per_progression)
+        return self.dev.read_film()
+
+    def cancel(self):
+        self._cancel.set()
+        if self.dev is not None:
+            self.dev.cancel()
+
+    def postprocess(self):
+        st = self.dev.stats() if self.dev else {}
+        if self.dev:
+            self.dev.close()
+        return st
+
+
+class GuidedPathTracer(ProgressivePathTracer):
+    """SD-tree guided progressive path tracer (Mueller et al. 2017 on the fork's scaffolding).
+
+    Training: iteration k renders 2^k progressions' worth of spp with training records, then the
+    postprogression hook exchanges records (identity on one GPU; RCCL all-gather across ranks via
+    `exchange`), splats them into the building SD-tree and refits.  The film is reset before the
+    final render, which samples with the last trained tree.
+    """
+
+    guided = True
+
+    def __init__(self, props=None, device=0, rank=0, world_size=1, exchange=None):
+        super().__init__(props, device, rank, world_size)
+        self.training_iterations = int(self.props.get("trainingIterations", 5))
+        self.exchange = exchange  # callable(dev) -> None: all-gather + splat into dev (N > 1)
+
+    def train(self):
+        for it in range(self.training_iterations):
+            if self._cancel.is_set():
+                return
+            self.preprogression()
+            self.dev.render_pass(2 ** it, self.sample_offset, record=True)
+            self.sample_offset += 2 ** it
+            self.postprogression_train(it)
+
+    def postprogression_train(self, it):
+        if self.exchange is None:
+            self.dev.splat_local()
+        else:
+            self.exchange(self.dev)
+        self.dev.refit(it)
+
+    def render(self, spp):
+        self.train()
+        self.dev.reset_film()
+        return super().render(spp)

@@ -1,0 +1,494 @@
+// ORACLE — test infrastructure only.  CPU restatement of the reference's ray casting, hit-record
+// fill, area-light sampling and pinhole camera:
+//   ShapeKDTree::rayIntersect (adaptive epsilon, AABB clip)  src/librender/skdtree.cpp:112-142,207-227
+//   TriAccel::load / rayIntersect                             include/mitsuba/render/triaccel.h:37-157
+//   fillIntersectionRecord<true> + computeShadingFrame         include/mitsuba/render/skdtree.h:343-430
+//   Scene::sampleEmitterDirect / pdfEmitterDirect              src/librender/scene.cpp:871-895,992-995
+//   AreaLight::sampleDirect / pdfDirect / eval                 src/emitters/area.cpp:158-183
+//   Shape::sampleDirect / pdfDirect                            src/librender/shape.cpp:102-126
+//   TriMesh::samplePosition, Triangle::sample                  src/librender/trimesh.cpp:412-423, src/libcore/triangle.cpp:24-60
+//   DiscreteDistribution::sampleReuse                          include/mitsuba/core/pmf.h:124-188
+//   PerspectiveCamera::sampleRay + Transform::lookAt           src/sensors/perspective.cpp:271-298, transform.cpp:191-214
+// The kd-tree (sahkdtree3.h) is replaced by a binned-SAH BVH: only the closest hit matters.
+#pragma once
+#include <limits>
+#include <vector>
+
+#include "orc_bsdf.h"
+
+namespace orc {
+
+constexpr float kInf = std::numeric_limits<float>::infinity();
+
+struct Ray {
+    V3 o, d;
+    float mint, maxt;
+};
+
+struct TriAccel {
+    uint32_t k;
+    float n_u, n_v, n_d, a_u, a_v, b_nu, b_nv, c_nu, c_nv;
+    uint32_t prim;
+    int load(V3 A, V3 B, V3 C) {
+        static const int waldModulo[4] = {1, 2, 0, 1};
+        V3 b = C - A, c = B - A, N = cross(c, b);
+        k = 0;
+        for (int j = 0; j < 3; j++)
+            if (std::fabs(N[j]) > std::fabs(N[(int)k])) k = j;
+        int u = waldModulo[k], v = waldModulo[k + 1];
+        float n_k = N[(int)k], denom = b[u] * c[v] - b[v] * c[u];
+        if (denom == 0) {
+            k = 3;
+            return 1;
+        }
+        n_u = N[u] / n_k;
+        n_v = N[v] / n_k;
+        n_d = dot(A, N) / n_k;
+        b_nu = b[u] / denom;
+        b_nv = -b[v] / denom;
+        a_u = A[u];
+        a_v = A[v];
+        c_nu = c[v] / denom;
+        c_nv = -c[u] / denom;
+        return 0;
+    }
+    bool intersect(const Ray &r, float mint, float maxt, float &u, float &v, float &t) const {
+        float o_u, o_v, o_k, d_u, d_v, d_k;
+        switch (k) {
+            case 0: o_u = r.o.y; o_v = r.o.z; o_k = r.o.x; d_u = r.d.y; d_v = r.d.z; d_k = r.d.x; break;
+            case 1: o_u = r.o.z; o_v = r.o.x; o_k = r.o.y; d_u = r.d.z; d_v = r.d.x; d_k = r.d.y; break;
+            case 2: o_u = r.o.x; o_v = r.o.y; o_k = r.o.z; d_u = r.d.x; d_v = r.d.y; d_k = r.d.z; break;
+            default: return false;
+        }
+        t = (n_d - o_u * n_u - o_v * n_v - o_k) / (d_u * n_u + d_v * n_v + d_k);
+        if (!(t >= mint && t <= maxt)) return false;
+        float hu = o_u + t * d_u - a_u, hv = o_v + t * d_v - a_v;
+        u = hv * b_nu + hu * b_nv;
+        v = hu * c_nu + hv * c_nv;
+        return u >= 0 && v >= 0 && u + v <= 1.0f;
+    }
+};
+
+struct AABB {
+    V3 lo{kInf, kInf, kInf}, hi{-kInf, -kInf, -kInf};
+    void expand(V3 p) {
+        lo = V3(std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z));
+        hi = V3(std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z));
+    }
+    void expand(const AABB &b) { expand(b.lo); expand(b.hi); }
+    float area() const {
+        V3 e = hi - lo;
+        if (e.x < 0) return 0;
+        return 2 * (e.x * e.y + e.y * e.z + e.z * e.x);
+    }
+    // AABB::rayIntersect (include/mitsuba/core/aabb.h): slab test, returns near/far (may be < 0)
+    bool rayIntersect(const Ray &r, float &nearT, float &farT) const {
+        nearT = -kInf;
+        farT = kInf;
+        for (int i = 0; i < 3; i++) {
+            float o = r.o[i], d = r.d[i], mn = lo[i], mx = hi[i];
+            if (d == 0) {
+                if (o < mn || o > mx) return false;
+            } else {
+                float t1 = (mn - o) / d, t2 = (mx - o) / d;
+                if (t1 > t2) std::swap(t1, t2);
+                nearT = std::max(t1, nearT);
+                farT = std::min(t2, farT);
+                if (!(nearT <= farT)) return false;
+            }
+        }
+        return true;
+    }
+};
+
+struct Its {
+    bool valid = false;
+    float t = kInf;
+    V3 p, geoN, uv;
+    Frame sh;
+    V3 wi;
+    uint32_t prim = 0, shape = 0;
+    V3 toLocal(V3 v) const { return sh.toLocal(v); }
+    V3 toWorld(V3 v) const { return sh.toWorld(v); }
+};
+
+struct BvhNode {
+    AABB box;
+    uint32_t left_or_first, count;  // count > 0 -> leaf
+};
+
+struct Camera {
+    V3 o, left, up, dir;
+    float tanHalf, aspect, nearC, farC;
+    uint32_t W, H;
+};
+
+struct Scene {
+    std::vector<V3> pos, nrm;
+    std::vector<uint32_t> idx;
+    std::vector<uint32_t> triShape;
+    std::vector<pg_shape> shapes;
+    std::vector<Material> mats;
+    std::vector<pg_emitter> emitters;
+    std::vector<std::vector<float>> emCdf;  // per emitter: normalized triangle-area CDF
+    std::vector<float> emArea;
+    std::vector<TriAccel> accel;  // in BVH order
+    std::vector<BvhNode> nodes;
+    AABB bounds;
+    Camera cam;
+
+    void build(const pg_scene_desc &d);
+    bool intersect(const Ray &ray, Its &its) const;
+    bool occluded(const Ray &ray) const;
+    bool traverse(const Ray &r, float mint, float maxt, bool any, float &t, float &u, float &v, uint32_t &prim) const;
+    void fill(const Ray &r, float t, float u, float v, uint32_t prim, Its &its) const;
+    Ray cameraRay(float sx, float sy) const;
+};
+
+inline Ray Scene::cameraRay(float px, float py) const {
+    // sampleToCamera for fovAxis=x: screen = (1 - 2 sx, (1 - 2 sy)/aspect) scaled by tan(fov/2)
+    float sx = px / (float)cam.W, sy = py / (float)cam.H;
+    V3 nearP((1.0f - 2.0f * sx) * cam.tanHalf, (1.0f - 2.0f * sy) / cam.aspect * cam.tanHalf, 1.0f);
+    V3 d = normalize(nearP);
+    float invZ = 1.0f / d.z;
+    Ray r;
+    r.mint = cam.nearC * invZ;
+    r.maxt = cam.farC * invZ;
+    r.o = cam.o;
+    r.d = cam.left * d.x + cam.up * d.y + cam.dir * d.z;
+    return r;
+}
+
+inline void Scene::build(const pg_scene_desc &d) {
+    pos.resize(d.num_vertices);
+    for (uint32_t i = 0; i < d.num_vertices; ++i) pos[i] = V3(d.positions[3 * i], d.positions[3 * i + 1], d.positions[3 * i + 2]);
+    if (d.normals) {
+        nrm.resize(d.num_vertices);
+        for (uint32_t i = 0; i < d.num_vertices; ++i) nrm[i] = V3(d.normals[3 * i], d.normals[3 * i + 1], d.normals[3 * i + 2]);
+    }
+    idx.assign(d.indices, d.indices + 3 * (size_t)d.num_triangles);
+    shapes.assign(d.shapes, d.shapes + d.num_shapes);
+    triShape.assign(d.num_triangles, 0);
+    for (uint32_t s = 0; s < d.num_shapes; ++s)
+        for (uint32_t t = 0; t < shapes[s].tri_count; ++t) triShape[shapes[s].tri_begin + t] = s;
+    for (uint32_t m = 0; m < d.num_materials; ++m) mats.push_back(makeMaterial(d.materials[m]));
+    emitters.assign(d.emitters, d.emitters + d.num_emitters);
+    for (auto &e : emitters) {
+        const pg_shape &sh = shapes[e.shape];
+        // area CDF: double accumulation of fp32 triangle areas, normalized, stored as fp32
+        std::vector<float> cdf(sh.tri_count + 1, 0.0f);
+        double acc = 0;
+        std::vector<double> cd(sh.tri_count + 1, 0.0);
+        for (uint32_t t = 0; t < sh.tri_count; ++t) {
+            uint32_t tri = sh.tri_begin + t;
+            V3 a = pos[idx[3 * tri]], b = pos[idx[3 * tri + 1]], c = pos[idx[3 * tri + 2]];
+            acc += (double)(0.5f * length(cross(b - a, c - a)));
+            cd[t + 1] = acc;
+        }
+        for (uint32_t t = 0; t <= sh.tri_count; ++t) cdf[t] = (float)(cd[t] / acc);
+        cdf[sh.tri_count] = 1.0f;
+        emCdf.push_back(cdf);
+        emArea.push_back((float)acc);
+    }
+    // camera (Transform::lookAt)
+    const pg_camera &c = d.camera;
+    V3 o(c.origin[0], c.origin[1], c.origin[2]), tg(c.target[0], c.target[1], c.target[2]), up(c.up[0], c.up[1], c.up[2]);
+    cam.o = o;
+    cam.dir = normalize(tg - o);
+    cam.left = normalize(cross(up, cam.dir));
+    cam.up = cross(cam.dir, cam.left);
+    cam.tanHalf = std::tan(c.fov_x_deg * kPi / 360.0f);
+    cam.W = c.width;
+    cam.H = c.height;
+    cam.aspect = (float)c.width / (float)c.height;
+    cam.nearC = c.near_clip;
+    cam.farC = c.far_clip;
+
+    // ---- binned SAH BVH over triangle bounds
+    uint32_t nt = d.num_triangles;
+    std::vector<AABB> tb(nt);
+    std::vector<V3> cen(nt);
+    for (uint32_t t = 0; t < nt; ++t) {
+        for (int j = 0; j < 3; ++j) tb[t].expand(pos[idx[3 * t + j]]);
+        bounds.expand(tb[t]);
+        cen[t] = (tb[t].lo + tb[t].hi) * 0.5f;
+    }
+    std::vector<uint32_t> order(nt);
+    for (uint32_t t = 0; t < nt; ++t) order[t] = t;
+    nodes.clear();
+    nodes.reserve(2 * (size_t)nt + 1);
+    struct Job { uint32_t node, first, count; };
+    std::vector<Job> stack;
+    nodes.push_back(BvhNode{});
+    stack.push_back({0, 0, nt});
+    while (!stack.empty()) {
+        Job j = stack.back();
+        stack.pop_back();
+        AABB box, cb;
+        for (uint32_t i = j.first; i < j.first + j.count; ++i) {
+            box.expand(tb[order[i]]);
+            cb.expand(cen[order[i]]);
+        }
+        nodes[j.node].box = box;
+        bool leaf = j.count <= 4;
+        uint32_t mid = 0;
+        if (!leaf) {
+            const int B = 16;
+            float best = kInf;
+            int bestAxis = -1, bestBin = -1;
+            for (int ax = 0; ax < 3; ++ax) {
+                float lo = cb.lo[ax], hi = cb.hi[ax];
+                if (!(hi > lo)) continue;
+                AABB bb[B];
+                uint32_t bc[B] = {0};
+                for (uint32_t i = j.first; i < j.first + j.count; ++i) {
+                    int b = (int)((cen[order[i]][ax] - lo) / (hi - lo) * B);
+                    b = std::min(std::max(b, 0), B - 1);
+                    bb[b].expand(tb[order[i]]);
+                    bc[b]++;
+                }
+                AABB la[B];
+                uint32_t lc[B];
+                AABB acc;
+                uint32_t n = 0;
+                for (int b = 0; b < B; ++b) {
+                    acc.expand(bb[b]);
+                    n += bc[b];
+                    la[b] = acc;
+                    lc[b] = n;
+                }
+                acc = AABB();
+                n = 0;
+                for (int b = B - 1; b > 0; --b) {
+                    acc.expand(bb[b]);
+                    n += bc[b];
+                    float cost = la[b - 1].area() * lc[b - 1] + acc.area() * n;
+                    if (lc[b - 1] > 0 && n > 0 && cost < best) {
+                        best = cost;
+                        bestAxis = ax;
+                        bestBin = b;
+                    }
+                }
+            }
+            if (bestAxis < 0 || best >= box.area() * j.count) {
+                if (j.count <= 16 || bestAxis < 0) {
+                    leaf = true;
+                    if (bestAxis < 0 && j.count > 16) {  // all centroids equal: split in the middle
+                        leaf = false;
+                        mid = j.first + j.count / 2;
+                    }
+                }
+            }
+            if (!leaf && bestAxis >= 0) {
+                float lo = cb.lo[bestAxis], hi = cb.hi[bestAxis];
+                auto it = std::partition(order.begin() + j.first, order.begin() + j.first + j.count, [&](uint32_t t) {
+                    int b = (int)((cen[t][bestAxis] - lo) / (hi - lo) * B);
+                    b = std::min(std::max(b, 0), B - 1);
+                    return b < bestBin;
+                });
+                mid = (uint32_t)(it - order.begin());
+                if (mid == j.first || mid == j.first + j.count) mid = j.first + j.count / 2;
+            }
+        }
+        if (leaf) {
+            nodes[j.node].left_or_first = j.first;
+            nodes[j.node].count = j.count;
+        } else {
+            uint32_t l = (uint32_t)nodes.size();
+            nodes.push_back(BvhNode{});
+            nodes.push_back(BvhNode{});
+            nodes[j.node].left_or_first = l;
+            nodes[j.node].count = 0;
+            stack.push_back({l, j.first, mid - j.first});
+            stack.push_back({l + 1, mid, j.first + j.count - mid});
+        }
+    }
+    accel.resize(nt);
+    for (uint32_t i = 0; i < nt; ++i) {
+        uint32_t t = order[i];
+        accel[i].load(pos[idx[3 * t]], pos[idx[3 * t + 1]], pos[idx[3 * t + 2]]);
+        accel[i].prim = t;
+    }
+}
+
+inline bool Scene::traverse(const Ray &r, float mint, float maxt, bool any, float &tBest, float &uBest, float &vBest,
+                            uint32_t &prim) const {
+    if (nodes.empty()) return false;
+    V3 inv(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    uint32_t stack[128];
+    int sp = 0;
+    stack[sp++] = 0;
+    bool hit = false;
+    float far = maxt;
+    while (sp > 0) {
+        const BvhNode &n = nodes[stack[--sp]];
+        // slab test against [mint, far]
+        float t0 = mint, t1 = far;
+        bool ok = true;
+        for (int a = 0; a < 3 && ok; ++a) {
+            float ta = (n.box.lo[a] - r.o[a]) * inv[a], tb = (n.box.hi[a] - r.o[a]) * inv[a];
+            if (ta > tb) std::swap(ta, tb);
+            if (std::isnan(ta) || std::isnan(tb)) continue;  // degenerate slab with d == 0 and o on the plane
+            t0 = std::max(t0, ta);
+            t1 = std::min(t1, tb);
+            if (t0 > t1) ok = false;
+        }
+        if (!ok) continue;
+        if (n.count > 0) {
+            for (uint32_t i = n.left_or_first; i < n.left_or_first + n.count; ++i) {
+                float u, v, t;
+                if (accel[i].intersect(r, mint, far, u, v, t)) {
+                    if (any) return true;
+                    far = t;
+                    tBest = t;
+                    uBest = u;
+                    vBest = v;
+                    prim = accel[i].prim;
+                    hit = true;
+                }
+            }
+        } else {
+            stack[sp++] = n.left_or_first + 1;
+            stack[sp++] = n.left_or_first;
+        }
+    }
+    return hit;
+}
+
+inline void Scene::fill(const Ray &r, float t, float u, float v, uint32_t prim, Its &its) const {
+    uint32_t i0 = idx[3 * prim], i1 = idx[3 * prim + 1], i2 = idx[3 * prim + 2];
+    V3 p0 = pos[i0], p1 = pos[i1], p2 = pos[i2];
+    float b0 = 1 - u - v, b1 = u, b2 = v;
+    its.valid = true;
+    its.t = t;
+    its.p = p0 * b0 + p1 * b1 + p2 * b2;
+    V3 side1 = p1 - p0, side2 = p2 - p0;
+    V3 fn = cross(side1, side2);
+    float len = length(fn);
+    if (!isZero(fn)) fn = fn / len;
+    V3 shn;
+    if (!nrm.empty()) {
+        shn = normalize(nrm[i0] * b0 + nrm[i1] * b1 + nrm[i2] * b2);
+        if (dot(fn, shn) < 0) fn = -fn;
+    } else {
+        shn = fn;
+    }
+    its.geoN = fn;
+    its.sh = shadingFrame(shn, side1);
+    its.prim = prim;
+    its.shape = triShape[prim];
+    its.wi = its.sh.toLocal(-r.d);
+}
+
+// ShapeKDTree::rayIntersect(ray, its): AABB clip + adaptive epsilon (skdtree.cpp:112-142)
+inline bool Scene::intersect(const Ray &ray, Its &its) const {
+    its.valid = false;
+    float mint, maxt;
+    if (!bounds.rayIntersect(ray, mint, maxt)) return false;
+    float rayMinT = ray.mint;
+    if (rayMinT == kEpsilon)
+        rayMinT *= std::max(std::max(std::max(std::fabs(ray.o.x), std::fabs(ray.o.y)), std::fabs(ray.o.z)), kEpsilon);
+    if (rayMinT > mint) mint = rayMinT;
+    if (ray.maxt < maxt) maxt = ray.maxt;
+    if (!(maxt > mint)) return false;
+    float t, u, v;
+    uint32_t prim;
+    if (!traverse(ray, mint, maxt, false, t, u, v, prim)) return false;
+    fill(ray, t, u, v, prim, its);
+    return true;
+}
+
+// ShapeKDTree::rayIntersect(ray) shadow variant (skdtree.cpp:207-227)
+inline bool Scene::occluded(const Ray &ray) const {
+    float mint, maxt;
+    if (!bounds.rayIntersect(ray, mint, maxt)) return false;
+    float rayMinT = ray.mint;
+    if (rayMinT == kEpsilon) rayMinT *= std::max(std::max(std::fabs(ray.o.x), std::fabs(ray.o.y)), std::fabs(ray.o.z));
+    if (rayMinT > mint) mint = rayMinT;
+    if (ray.maxt < maxt) maxt = ray.maxt;
+    if (!(maxt > mint)) return false;
+    float t, u, v;
+    uint32_t prim;
+    return traverse(ray, mint, maxt, true, t, u, v, prim);
+}
+
+// DiscreteDistribution::sampleReuse (pmf.h:124-169) over a normalized CDF
+inline uint32_t sampleReuseCdf(const std::vector<float> &cdf, float &s) {
+    auto it = std::lower_bound(cdf.begin(), cdf.end(), s);
+    ptrdiff_t e = it - cdf.begin() - 1;
+    size_t index = std::min(cdf.size() - 2, (size_t)std::max((ptrdiff_t)0, e));
+    while (cdf[index + 1] - cdf[index] == 0 && index < cdf.size() - 2) ++index;
+    s = (s - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    return (uint32_t)index;
+}
+
+struct DirectRec {
+    V3 ref, refN, p, n, d;
+    float dist = 0, pdf = 0;
+    int emitter = -1;
+};
+
+// Scene::sampleEmitterDirect with visibility (scene.cpp:871-895)
+inline V3 sampleEmitterDirect(const Scene &S, DirectRec &dr, float sx, float sy) {
+    uint32_t ne = (uint32_t)S.emitters.size();
+    if (ne == 0) return V3(0.f);
+    // uniform emitter CDF (sampling weight 1 each): index = floor-ish, with reuse
+    float emPdf = 1.0f / (float)ne;
+    // uniform emitter pdf (every sampling weight is 1): sampleReuse on a uniform CDF
+    uint32_t ei = std::min((uint32_t)(sx * (float)ne), ne - 1);
+    sx = sx * (float)ne - (float)ei;
+    const pg_emitter &em = S.emitters[ei];
+    const pg_shape &sh = S.shapes[em.shape];
+    // TriMesh::samplePosition: triangle by area on sample.y (reuse), then Triangle::sample(sample)
+    uint32_t ti = sampleReuseCdf(S.emCdf[ei], sy);
+    uint32_t tri = sh.tri_begin + ti;
+    uint32_t i0 = S.idx[3 * tri], i1 = S.idx[3 * tri + 1], i2 = S.idx[3 * tri + 2];
+    V3 p0 = S.pos[i0], p1 = S.pos[i1], p2 = S.pos[i2];
+    float a = safe_sqrt(1.0f - sx);
+    float bx = 1 - a, by = a * sy;
+    V3 sideA = p1 - p0, sideB = p2 - p0;
+    V3 p = p0 + (sideA * bx) + (sideB * by);
+    V3 n;
+    if (!S.nrm.empty()) n = normalize(S.nrm[i0] * (1.0f - bx - by) + S.nrm[i1] * bx + S.nrm[i2] * by);
+    else n = normalize(cross(sideA, sideB));
+    dr.p = p;
+    dr.n = n;
+    dr.pdf = 1.0f / S.emArea[ei];
+    // Shape::sampleDirect
+    dr.d = p - dr.ref;
+    float distSq = lengthSq(dr.d);
+    dr.dist = std::sqrt(distSq);
+    dr.d = dr.d / dr.dist;
+    float dp = absDot(dr.d, dr.n);
+    dr.pdf *= dp != 0 ? (distSq / dp) : 0.0f;
+    // AreaLight::sampleDirect
+    V3 value;
+    if (dot(dr.d, dr.refN) >= 0 && dot(dr.d, dr.n) < 0 && dr.pdf != 0) {
+        value = V3(em.radiance[0], em.radiance[1], em.radiance[2]) / dr.pdf;
+    } else {
+        dr.pdf = 0;
+        return V3(0.f);
+    }
+    Ray sr{dr.ref, dr.d, kEpsilon, dr.dist * (1 - kShadowEpsilon)};
+    if (S.occluded(sr)) return V3(0.f);
+    dr.emitter = (int)ei;
+    dr.pdf *= emPdf;
+    return value / emPdf;
+}
+
+// Scene::pdfEmitterDirect for a BSDF-sampled hit on emitter `ei` (records.inl:170-178 setQuery)
+inline float pdfEmitterDirect(const Scene &S, int ei, V3 refN, V3 d, V3 n, float dist) {
+    if (!(dot(d, refN) >= 0 && dot(d, n) < 0)) return 0.0f;
+    float pdfPos = 1.0f / S.emArea[ei];
+    return pdfPos * (dist * dist) / absDot(d, n) * (1.0f / (float)S.emitters.size());
+}
+
+inline V3 emitterLe(const Scene &S, const Its &its, V3 w) {
+    int e = S.shapes[its.shape].emitter;
+    if (e < 0) return V3(0.f);
+    if (dot(its.sh.n, w) <= 0) return V3(0.f);
+    const pg_emitter &em = S.emitters[e];
+    return V3(em.radiance[0], em.radiance[1], em.radiance[2]);
+}
+
+}  // namespace orc
