@@ -1,0 +1,203 @@
+"""Benchmark: Mpaths/s of the SD-tree guided integrator on the Veach ajar-door-class scene (C3).
+
+A step is one complete guided render job of C3 (BASELINE.json configs[2]): 1280x720, five training
+progressions of 1, 2, 4, 8, 16 spp (training-record write, RCCL all-gather of records across ranks,
+fixed-point splat, SD-tree refit) followed by the 1024-spp final render with the trained tree —
+(31 + 1024) x 921,600 = 972.3 M camera paths per step.  Inputs (scene, BVH, path buffers) are
+resident in HBM before timing starts.  With N ranks the image tiles are sharded (total work fixed:
+"strong" scaling); value = all paths of the job / max-over-ranks wall time.
+
+Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md §8d /
+DESIGN.md §"Measurement", over its HIP-event-measured average duration), and on rank 0 at N=1 the
+CPU oracle timed on a bounded sample of the same job (kind "port"), plus the equal-spp relative RMSE
+between GPU and CPU on that sample.
+
+  python bench.py [--gpus N --steps K --warmup W] [--spp 1024] [--no-cpu] [--quick]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# algorithmic bytes per unit (DESIGN.md §"Measurement"; SURVEY.md §8d decomposition of B_seg)
+BYTES_TRACE_PER_RAY = 52      # queue id 4 + ray o/tmin 16 + ray d/tmax 16 + hit write 16
+BYTES_SHADOW_PER_RAY = 84     # queue id 4 + shadow ray 32 + contribution 16 + radiance RMW 32
+BYTES_SHADE_PER_VERTEX = 488  # path state read 96 + write 96 + tri gather 80 + material 32 + shadow write 48
+#                               + emitter-tri gather 80 + training vertex 48 + queue writes 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--scene", default="ajar_door")
+    ap.add_argument("--width", type=int, default=1280)
+    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--spp", type=int, default=1024)
+    ap.add_argument("--train", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    if a.quick:
+        a.width, a.height, a.spp, a.steps, a.warmup = 320, 180, 64, 1, 1
+    import pgload
+    pg = pgload.load()
+    from mitsuba_path_guiding_amd import distributed as D
+    from mitsuba_path_guiding_amd.integrator import GuidedPathTracer
+
+    rank, world, local = D.env_rank()
+    world = max(world, 1)
+    if world > 1:
+        D.init("nccl")
+    import torch
+
+    on_dev = torch.cuda.is_available()
+    scene = pg.scenes.SCENES[a.scene](a.width, a.height)
+    exchange = D.make_exchange(on_dev) if world > 1 else None
+    # one progression for the final render (the device chunks it into waves of <= 4M paths)
+    integ = GuidedPathTracer({"trainingIterations": a.train, "samplesPerProgression": a.spp}, device=local,
+                             rank=rank, world_size=world, exchange=exchange)
+    integ.preprocess(scene)
+    dev = integ.dev
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+        if on_dev:
+            torch.cuda.synchronize()
+
+    def job():
+        integ.reset()
+        integ.render(a.spp)
+
+    for _ in range(a.warmup):
+        job()
+    barrier()
+    s0 = dev.stats()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        job()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    s1 = dev.stats()
+    if world > 1:
+        elapsed = D.max_over_ranks(elapsed, on_dev)
+    paths_per_job = (2 ** a.train - 1 + a.spp) * a.width * a.height
+    total_paths = paths_per_job * a.steps
+    value = total_paths / elapsed / 1e6
+
+    # ---- roofline of the dominant kernel (this rank's HIP-event timings over the timed region)
+    d = {k: s1[k] - s0[k] for k in s1}
+    kernels = {
+        "pg_trace_closest": (d["trace_ms"], d["segments"] * BYTES_TRACE_PER_RAY, d["trace_launches"]),
+        "pg_shade": (d["shade_ms"], d["segments"] * BYTES_SHADE_PER_VERTEX, d["trace_launches"]),
+        "pg_trace_shadow": (d["shadow_ms"], d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["trace_launches"]),
+    }
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    ms, nbytes, launches = kernels[dom]
+    achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            pj = json.load(open(pmc))
+            if dom in pj.get("kernels", {}):
+                traffic = pj["kernels"][dom].get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": dom,
+                "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
+                "avg_launch_ms": round(ms / max(launches, 1), 4)}
+
+    # ---- CPU baseline (oracle, rank 0, N = 1, bounded sample) + equal-spp RMSE on the sample
+    cpu = None
+    rmse = None
+    if rank == 0 and world == 1 and not a.no_cpu:
+        cpu, rmse = cpu_baseline(pg, scene, integ, a)
+
+    if rank == 0:
+        line = {
+            "metric": "Mpaths/sec + equal-spp RMSE vs CPU ref, ajar-door scene at 1/2/4/8 GPUs",
+            "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"C3 {a.scene} {a.width}x{a.height}, guided SD-tree, {a.train} training "
+                                   f"iterations (1..{2 ** (a.train - 1)} spp) + {a.spp} spp render",
+                       "scene": a.scene, "triangles": scene.num_triangles, "width": a.width, "height": a.height,
+                       "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
+                       "parallelism": f"tile-shard x{world}, RCCL all-gather of records"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "rmse_vs_cpu": rmse,
+            "segments_per_path": round(d["segments"] / max(d["paths"], 1), 3),
+            "kernel_ms_per_step": {k: round(v[0] / a.steps, 2) for k, v in kernels.items()},
+        }
+        print(json.dumps(line), flush=True)
+    integ.postprocess()
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+def cpu_baseline(pg, scene, integ, a):
+    """Time the oracle (CPU restatement, all host cores) on a bounded sample of the same job: the
+    guided final render of the first tiles with the GPU-trained SD-tree, then compare GPU vs CPU at
+    equal spp on those pixels."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py as O  # checker / CPU baseline only
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16 threads
+    osc = O.OracleScene(pg.capi, scene)
+    tree = O.OracleSDTree(osc)
+    tree.deserialize(integ.dev.get_sdtree())
+    cfg = pg.capi.default_config(guiding=1)
+    W = scene.width
+    T = 32
+    tiles = []
+    for ty in range(0, scene.height, T):
+        for tx in range(0, W, T):
+            tiles.append([(y * W + x) for y in range(ty, min(ty + T, scene.height)) for x in range(tx, min(tx + T, W))])
+    spp = 64
+    off = 2 ** a.train - 1
+    # calibrate on one tile from the image centre, then size the sample to ~cpu_seconds
+    mid = len(tiles) // 2
+    t = time.perf_counter()
+    O.render(osc, cfg, spp, off, sdtree=tree, pixels=np.array(tiles[mid], np.uint32), nthreads=cores)
+    per_tile = time.perf_counter() - t
+    ntiles = int(max(1, min(len(tiles), a.cpu_seconds / max(per_tile, 1e-3))))
+    sel = [tiles[(mid + i) % len(tiles)] for i in range(ntiles)]
+    pix = np.array([p for tl in sel for p in tl], np.uint32)
+    t = time.perf_counter()
+    c_rgbw, _, st = O.render(osc, cfg, spp, off, sdtree=tree, pixels=pix, nthreads=cores)
+    dt = time.perf_counter() - t
+    cpu = {"value": round(float(st[0]) / dt / 1e6, 4), "unit": "Mpaths/s", "cores": cores, "kind": "port",
+           "sample": f"{ntiles} tiles of 32x32 ({len(pix)} px) x {spp} spp of the guided C3 final render "
+                     f"with the GPU-trained SD-tree ({int(st[0])} paths, {dt:.1f} s)"}
+    # equal-spp GPU render of the same sample indices (fresh film; timed region is over)
+    integ.dev.reset_film()
+    integ.dev.render_pass(spp, off, False)
+    g_rgbw, _ = integ.dev.read_film()
+    g = g_rgbw.reshape(-1, 4)[pix]
+    c = c_rgbw.reshape(-1, 4)[pix]
+    gm = g[:, :3] / np.maximum(g[:, 3:4], 1)
+    cm = c[:, :3] / np.maximum(c[:, 3:4], 1)
+    rmse = float(np.sqrt(np.mean((gm - cm) ** 2)) / max(float(np.sqrt(np.mean(cm ** 2))), 1e-12))
+    return cpu, {"relative_rmse": round(rmse, 6), "spp": spp, "pixels": int(len(pix)),
+                 "note": "same RNG streams on both sides; differences come from fp32 libm/FMA divergence"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,117 @@
+"""Multi-GPU plumbing: one process per GPU, torch.distributed over RCCL (backend "nccl") on MI355X,
+gloo on CPU for tests.  Replaces the reference's master/worker TCP/SSH scheduler
+(include/mitsuba/core/sched_remote.h:50-236) for the ONE data-parallel hot path:
+
+  * image tiles are sharded statically across ranks inside the C-ABI context (pg_config.rank /
+    world_size, 32x32 tiles dealt round-robin; the RNG is keyed by the global pixel, so results do
+    not depend on the number of ranks);
+  * before each SD-tree refit (postprogression) every rank all-gathers the training records of all
+    ranks (counts first, then one all_gather of the padded record buffers) and splats them in rank
+    order.  The splat is exact integer arithmetic, so every rank refits a bit-identical tree;
+  * at the end the film tiles are sum-reduced to rank 0 (tiles are disjoint, so the sum is a gather).
+
+The exchange takes any object with the Device record interface (record_count / get_records /
+splat_records), which lets the gloo tests run it against a CPU stand-in.
+"""
+import os
+
+import numpy as np
+
+RECORD_BYTES = 32
+
+
+def env_rank():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def init(backend=None):
+    """Initialise the default process group from the torchrun environment (127.0.0.1 rendezvous)."""
+    import torch
+    import torch.distributed as dist
+    rank, world, local = env_rank()
+    if world <= 1 or dist.is_initialized():
+        return rank, world, local
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29512")
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local
+
+
+def make_exchange(on_device):
+    """Returns exchange(dev): all-gather every rank's records and splat them into dev.
+
+    on_device=True: records move device->device (RCCL over xGMI); False: through host memory (gloo).
+    """
+    import torch
+    import torch.distributed as dist
+
+    def exchange(dev):
+        world = dist.get_world_size()
+        n_local = int(dev.record_count())
+        tdev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+        counts = torch.zeros(world, dtype=torch.int64, device=tdev)
+        mine = torch.tensor([n_local], dtype=torch.int64, device=tdev)
+        dist.all_gather_into_tensor(counts, mine)
+        counts = counts.cpu().tolist()
+        maxn = max(counts)
+        if maxn == 0:
+            return counts
+        if on_device:
+            buf = torch.empty(maxn * RECORD_BYTES, dtype=torch.uint8, device=tdev)
+            torch.cuda.synchronize()
+            dev.get_records(dst_ptr=buf.data_ptr(), max_records=n_local)
+            gathered = torch.empty(world * maxn * RECORD_BYTES, dtype=torch.uint8, device=tdev)
+            dist.all_gather_into_tensor(gathered, buf)
+            torch.cuda.synchronize()
+            base = gathered.data_ptr()
+            for r in range(world):
+                if counts[r]:
+                    dev.splat_records(device_ptr=base + r * maxn * RECORD_BYTES, count=counts[r])
+        else:
+            host = np.zeros(maxn * RECORD_BYTES, np.uint8)
+            local = dev.get_records()
+            host[: len(local)] = local
+            buf = torch.from_numpy(host)
+            gathered = torch.empty(world * maxn * RECORD_BYTES, dtype=torch.uint8)
+            dist.all_gather_into_tensor(gathered, buf)
+            g = gathered.numpy()
+            for r in range(world):
+                if counts[r]:
+                    off = r * maxn * RECORD_BYTES
+                    dev.splat_records(g[off: off + counts[r] * RECORD_BYTES])
+        return counts
+
+    return exchange
+
+
+def reduce_film(rgbw, sumsq, on_device):
+    """Sum-reduce the (disjoint-tile) films of all ranks to rank 0; returns numpy arrays on rank 0."""
+    import torch
+    import torch.distributed as dist
+    tdev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+    t = torch.from_numpy(np.stack([rgbw, sumsq])).to(tdev)
+    dist.reduce(t, dst=0)
+    out = t.cpu().numpy()
+    return out[0], out[1]
+
+
+def max_over_ranks(value, on_device):
+    import torch
+    import torch.distributed as dist
+    tdev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+    t = torch.tensor([float(value)], dtype=torch.float64, device=tdev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(value, on_device):
+    import torch
+    import torch.distributed as dist
+    tdev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+    t = torch.tensor([float(value)], dtype=torch.float64, device=tdev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())

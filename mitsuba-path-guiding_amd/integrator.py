@@ -259,6 +259,19 @@ class GuidedPathTracer(ProgressivePathTracer):
         super().__init__(props, device, rank, world_size)
         self.training_iterations = int(self.props.get("trainingIterations", 5))
         self.exchange = exchange  # callable(dev) -> None: all-gather + splat into dev (N > 1)
+        self.initial_tree = None
+
+    def preprocess(self, scene):
+        super().preprocess(scene)
+        self.initial_tree = self.dev.get_sdtree()
+        return True
+
+    def reset(self):
+        """Start a new job on the uploaded scene: untrained SD-tree, empty film, sample index 0."""
+        self.dev.put_sdtree(self.initial_tree)
+        self.dev.reset_film()
+        self.sample_offset = 0
+        self.progression = 0
 
     def train(self):
         for it in range(self.training_iterations):
