@@ -513,9 +513,15 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     c->rec_host_count = 0;
     c->num_tris = nt;
     c->num_mats = d->num_materials;
+    // Scene::getAABB(): the kd-tree's slightly enlarged bounds (gkdtree.h:1213-1220,
+    // MTS_KD_AABB_EPSILON = 1e-3); the SD-tree covers this box
     for (int a = 0; a < 3; ++a) {
-        c->scene_lo[a] = bvh.lo[a];
-        c->scene_hi[a] = bvh.hi[a];
+        const float eps = 1e-3f;
+        float lo = bvh.lo[a], hi = bvh.hi[a];
+        lo = lo - ((hi - lo) * eps + eps);
+        hi = hi + ((hi - lo) * eps + eps);
+        c->scene_lo[a] = lo;
+        c->scene_hi[a] = hi;
     }
     c->sd.reset(c->scene_lo, c->scene_hi);
     if ((s = uploadSd(c))) return s;

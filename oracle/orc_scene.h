@@ -213,6 +213,12 @@ inline void Scene::build(const pg_scene_desc &d) {
         bounds.expand(tb[t]);
         cen[t] = (tb[t].lo + tb[t].hi) * 0.5f;
     }
+    // the kd-tree's slightly enlarged scene AABB (gkdtree.h:1213-1220, MTS_KD_AABB_EPSILON = 1e-3)
+    {
+        const float eps = 1e-3f;
+        bounds.lo = bounds.lo - ((bounds.hi - bounds.lo) * eps + V3(eps));
+        bounds.hi = bounds.hi + ((bounds.hi - bounds.lo) * eps + V3(eps));
+    }
     std::vector<uint32_t> order(nt);
     for (uint32_t t = 0; t < nt; ++t) order[t] = t;
     nodes.clear();

@@ -1,0 +1,122 @@
+"""World-size-2 gloo test of the multi-rank training path (CPU): tile sharding + the record
+all-gather of mitsuba_path_guiding_amd.distributed + splat + refit must leave every rank with the
+same SD-tree, bit for bit, and that tree must equal a single-rank training on the whole image
+(the splat is exact fixed-point arithmetic, so the order of gathered records cannot matter).
+
+The per-rank "device" here is a CPU stand-in built on the oracle (test double): the exchange code
+under test only needs the Device record interface (record_count / get_records / splat_records).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RES, ITERS, THR = 48, 3, 300.0
+
+
+def tile_shard(W, H, rank, world, T=32):
+    """pg_upload_scene's shard: 32x32 tiles dealt round-robin, row-major inside a tile."""
+    tx, ty = (W + T - 1) // T, (H + T - 1) // T
+    pix = []
+    for t in range(tx * ty):
+        if t % world != rank:
+            continue
+        x0, y0 = (t % tx) * T, (t // tx) * T
+        for y in range(y0, min(y0 + T, H)):
+            for x in range(x0, min(x0 + T, W)):
+                pix.append(y * W + x)
+    return np.array(pix, np.uint32)
+
+
+class OracleShardDevice:
+    def __init__(self, pg, O, scene, cfg, rank, world):
+        self.pg, self.O, self.cfg = pg, O, cfg
+        self.osc = O.OracleScene(pg.capi, scene)
+        self.tree = O.OracleSDTree(self.osc)
+        self.pixels = tile_shard(scene.width, scene.height, rank, world)
+        self.pending = np.zeros(0, np.uint8)
+
+    def render_pass(self, spp, offset, record):
+        self.O.render(self.osc, self.cfg, spp, offset, record=record, sdtree=self.tree, pixels=self.pixels,
+                      nthreads=1)
+        self.pending = self.tree.take_records(self.pg.capi)
+
+    def record_count(self):
+        return len(self.pending) // 32
+
+    def get_records(self, dst_ptr=None, max_records=None):
+        assert dst_ptr is None
+        return self.pending
+
+    def splat_records(self, recs=None, device_ptr=None, count=None):
+        self.tree.splat_bytes(recs)
+
+    def refit(self, it):
+        self.tree.refit(it, self.cfg)
+        self.pending = np.zeros(0, np.uint8)
+
+
+def _worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import pgload
+    import oracle_py as O
+    pg = pgload.load()
+    from mitsuba_path_guiding_amd import distributed as D
+    D.init("gloo")
+    sc = pg.scenes.cornell(RES, RES)
+    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=THR, rank=rank, world_size=world)
+    dev = OracleShardDevice(pg, O, sc, cfg, rank, world)
+    exchange = D.make_exchange(on_device=False)
+    off = 0
+    for it in range(ITERS):
+        dev.render_pass(2 ** it, off, True)
+        off += 2 ** it
+        counts = exchange(dev)
+        assert len(counts) == world
+        dev.refit(it)
+    np.save(os.path.join(outdir, f"tree{rank}.npy"), dev.tree.serialize())
+    import torch.distributed as dist
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_rank_exchange_gives_identical_trees(pg, O, tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    t0 = np.load(tmp_path / "tree0.npy")
+    t1 = np.load(tmp_path / "tree1.npy")
+    assert np.array_equal(t0, t1)
+    # single rank over the whole image, same sample indices -> same record multiset -> same tree
+    sc = pg.scenes.cornell(RES, RES)
+    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=THR)
+    osc = O.OracleScene(pg.capi, sc)
+    tree = O.OracleSDTree(osc)
+    off = 0
+    for it in range(ITERS):
+        O.render(osc, cfg, 2 ** it, off, record=True, sdtree=tree, nthreads=2)
+        off += 2 ** it
+        tree.splat_pending()
+        tree.refit(it, cfg)
+    assert np.array_equal(tree.serialize(), t0)
+
+
+def test_shard_covers_image_once():
+    W, H = 100, 70
+    parts = [tile_shard(W, H, r, 3) for r in range(3)]
+    allp = np.concatenate(parts)
+    assert len(allp) == W * H and len(np.unique(allp)) == W * H

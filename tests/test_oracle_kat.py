@@ -1,0 +1,130 @@
+"""Pins the CPU oracle against the reference's own known-answer tests and fixtures.
+
+  * src/tests/test_dgeom.cpp:36-121 — triangle-hit differential geometry (tests/golden/dgeom_kat.json)
+  * src/tests/test_kd.cpp:86-130 + data/tests/bunny.ply — rays between random points of the bunny's
+    bounding sphere; the oracle's BVH must find the same closest hits as a brute-force TriAccel-free
+    (Moeller-Trumbore, float64) reference over all 69,451 faces.
+  * determinism of the oracle film against its committed golden output.
+"""
+import json
+import os
+
+import numpy as np
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _single_triangle_scene(pg, V, N):
+    s = pg.scenes.Scene()
+    m = s.add_material(pg.scenes.material("diffuse"))
+    s.add_mesh(np.asarray(V, np.float32), np.array([[0, 1, 2]], np.uint32), N, material=m)
+    s.set_camera((0.2, 0.2, -2), (0.2, 0.2, 0), (0, 1, 0), 40, 8, 8)
+    return s.finalize()
+
+
+def test_dgeom_kat(pg, O):
+    kat = json.load(open(os.path.join(GOLDEN, "dgeom_kat.json")))
+    for case in kat["cases"]:
+        V = np.array(case["vertices"], np.float32)
+        if case["normals"] is None:
+            N = np.tile(np.array([[0, 0, 1]], np.float32), (3, 1))  # TriMesh face normal
+        else:
+            N = np.array(case["normals"], np.float32)
+        sc = _single_triangle_scene(pg, V, N)
+        osc = O.OracleScene(pg.capi, sc)
+        r = np.array([[*case["ray_o"], 1e-4, *case["ray_d"], np.inf]], np.float32)
+        h = osc.intersect(r)[0]
+        eps = case["eps"]
+        assert h[15].view(np.uint32) == 0
+        assert np.allclose(h[0:3], case["p"], atol=eps)
+        assert np.allclose(h[4:7], case["geoN"], atol=eps)
+        assert np.allclose(h[10:13], case["dpdu"], atol=eps)
+        if case["normals"] is None:
+            assert np.allclose(h[7:10], case["shN"], atol=eps)
+            assert np.allclose(h[13:15], case["uv"], atol=eps)
+        else:
+            b = np.array(case["bary"], np.float32)
+            n = (np.array(case["normals"], np.float32) * b[:, None]).sum(0)
+            n /= np.linalg.norm(n)
+            assert np.allclose(h[7:10], n, atol=eps)  # normalize(n0*.7 + n1*.1 + n2*.2)
+            assert np.allclose(h[13:15], b[1:], atol=eps)
+
+
+def _brute_force(V, F, o, d):
+    """float64 Moeller-Trumbore over all faces; returns (t, face) per ray."""
+    p0, p1, p2 = V[F[:, 0]].astype(np.float64), V[F[:, 1]].astype(np.float64), V[F[:, 2]].astype(np.float64)
+    e1, e2 = p1 - p0, p2 - p0
+    ts = np.full(len(o), np.inf)
+    fs = np.full(len(o), -1)
+    for i in range(len(o)):
+        pv = np.cross(d[i], e2)
+        det = np.einsum("ij,ij->i", e1, pv)
+        ok = np.abs(det) > 1e-12
+        inv = np.where(ok, 1.0 / np.where(ok, det, 1.0), 0.0)
+        tv = o[i] - p0
+        u = np.einsum("ij,ij->i", tv, pv) * inv
+        qv = np.cross(tv, e1)
+        v = (qv @ d[i]) * inv
+        t = np.einsum("ij,ij->i", e2, qv) * inv
+        hit = ok & (u >= 0) & (v >= 0) & (u + v <= 1) & (t > 1e-6)
+        if hit.any():
+            j = np.argmin(np.where(hit, t, np.inf))
+            ts[i], fs[i] = t[j], j
+    return ts, fs
+
+
+def _bunny_scene(pg):
+    z = np.load(os.path.join(GOLDEN, "bunny.npz"))
+    V, F = z["positions"], z["faces"]
+    s = pg.scenes.Scene()
+    m = s.add_material(pg.scenes.material("diffuse"))
+    s.add_mesh(V, F, material=m)
+    c = V.mean(0)
+    s.set_camera(tuple(c + np.array([0, 0, 1.0])), tuple(c), (0, 1, 0), 40, 8, 8)
+    return s.finalize(), V, F
+
+
+def bunny_sphere_rays(V, n, seed):
+    """test_kd.cpp:86-130: segments between random points on the bounding sphere."""
+    rng = np.random.default_rng(seed)
+    lo, hi = V.min(0), V.max(0)
+    c = (lo + hi) / 2
+    r = np.linalg.norm(hi - lo) / 2
+    a = rng.normal(size=(n, 3))
+    b = rng.normal(size=(n, 3))
+    a = c + r * a / np.linalg.norm(a, axis=1, keepdims=True)
+    b = c + r * b / np.linalg.norm(b, axis=1, keepdims=True)
+    d = b - a
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3] = a
+    rays[:, 3] = 0.0
+    rays[:, 4:7] = d
+    rays[:, 7] = np.inf
+    return rays
+
+
+def test_bunny_raycast(pg, O):
+    sc, V, F = _bunny_scene(pg)
+    assert len(V) == 35947 and len(F) == 69451
+    osc = O.OracleScene(pg.capi, sc)
+    rays = bunny_sphere_rays(V, 400, 11)
+    h = osc.trace(rays)
+    prim = h[:, 1].view(np.uint32)
+    t, f = _brute_force(V, F, rays[:, 0:3].astype(np.float64), rays[:, 4:7].astype(np.float64))
+    hit_o = prim != 0xFFFFFFFF
+    hit_b = f >= 0
+    assert (hit_o == hit_b).mean() >= 0.995
+    both = hit_o & hit_b
+    assert both.sum() > 50
+    assert (prim[both] == f[both]).mean() >= 0.99
+    assert np.allclose(h[both, 0], t[both], rtol=1e-4, atol=1e-6)
+
+
+def test_oracle_film_golden(pg, O):
+    z = np.load(os.path.join(GOLDEN, "film_cornell.npz"))
+    sc = pg.scenes.cornell(32, 32)
+    rgbw, sq, st = O.render(O.OracleScene(pg.capi, sc), pg.capi.default_config(), 16, 0, nthreads=2)
+    assert np.array_equal(st, z["stats"])
+    assert np.allclose(rgbw, z["rgbw"], rtol=1e-5, atol=1e-6)
+    assert np.allclose(sq, z["sumsq"], rtol=1e-5, atol=1e-6)
