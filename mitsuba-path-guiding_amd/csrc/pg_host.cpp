@@ -22,6 +22,10 @@
 namespace {
 
 constexpr uint32_t kStackDepth = 48;  // must match STACK_DEPTH in pg_kernels.hip
+constexpr uint32_t kMaxBounces = 1100;     // > gpu_depth_cap default (1024) + 2
+constexpr uint32_t kShadowOffset = 1104;   // shadow[b] lives at counters[kShadowOffset + b]
+constexpr uint32_t kCounterWords = 2 * 1104;
+constexpr uint32_t kFirstPoll = 12, kPollEvery = 6;
 
 struct DevBuf {
     void *p = nullptr;
@@ -66,7 +70,7 @@ struct Ctx {
     // path state
     uint32_t P = 0;
     int vtx_slots = 0;
-    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, counters;
+    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, counters, stack_ovf;
     uint32_t *h_counter = nullptr;  // pinned
     // film
     DevBuf film, film_sq;
@@ -221,7 +225,8 @@ SDDev sdView(const Ctx *c) {
 PathDev pathView(const Ctx *c) {
     return PathDev{c->ray_o.as<float4>(), c->ray_d.as<float4>(), c->hit.as<float4>(), c->thr.as<float4>(),
                    c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(), c->sh_o.as<float4>(),
-                   c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->P};
+                   c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->stack_ovf.as<uint32_t>(),
+                   c->P};
 }
 
 pg_status uploadSd(Ctx *c) {
@@ -283,6 +288,7 @@ pg_status ensurePaths(Ctx *c, uint32_t want) {
     HIPC(c, c->q0.alloc((size_t)P * 4));
     HIPC(c, c->q1.alloc((size_t)P * 4));
     HIPC(c, c->qs.alloc((size_t)P * 4));
+    HIPC(c, c->stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
     if (vslots > 0) HIPC(c, c->vtx.alloc((size_t)vslots * P * 48));
     c->P = P;
     c->vtx_slots = vslots;
@@ -359,7 +365,7 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     if (c->cfg.tile_size == 0) c->cfg.tile_size = 32;
     if (c->cfg.gpu_depth_cap <= 0) c->cfg.gpu_depth_cap = 1024;
     if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_counter, 16, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc((void **)&c->h_counter, (8 + kCounterWords) * 4, hipHostMallocDefault) != hipSuccess) {
         delete c;
         return fail(nullptr, PG_ERR_HIP, "pg_create: stream/pinned allocation failed");
     }
@@ -507,7 +513,7 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     HIPC(c, c->film_sq.alloc(fb));
     HIPC(c, hipMemsetAsync(c->film.p, 0, fb, c->stream));
     HIPC(c, hipMemsetAsync(c->film_sq.p, 0, fb, c->stream));
-    HIPC(c, c->counters.alloc(64));
+    HIPC(c, c->counters.alloc(kCounterWords * 4));
     HIPC(c, c->rec_count.alloc(16));
     HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 16, c->stream));
     c->rec_host_count = 0;
@@ -560,7 +566,11 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const SceneDev sc = sceneView(c);
     const SDDev sd = sdView(c);
     const PathDev pv = pathView(c);
-    uint32_t *cnt = c->counters.as<uint32_t>();  // [0],[1] ping-pong live counts, [2] shadow count
+    // per-bounce device counters: live[b] (queue length entering bounce b) and shadow[b]; the
+    // kernels read them on the device, so the host only synchronizes every few bounces
+    uint32_t *live = c->counters.as<uint32_t>();
+    uint32_t *shcnt = live + kShadowOffset;
+    const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     uint32_t layersPer = std::max<uint32_t>(1, c->P / npix);
     uint32_t pixPer = std::min(npix, c->P);
@@ -571,49 +581,53 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             uint32_t np = std::min(pixPer, npix - pb);
             uint32_t n = np * nl;
             if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
-            uint32_t *qin = c->q0.as<uint32_t>(), *qout = c->q1.as<uint32_t>();
-            int cin = 0;
-            pg_launch_camera(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + l0, qin);
+            uint32_t *qbuf[2] = {c->q0.as<uint32_t>(), c->q1.as<uint32_t>()};
+            HIPC(c, hipMemsetAsync(live, 0, kCounterWords * 4, c->stream));
             c->h_counter[0] = n;
-            HIPC(c, hipMemcpyAsync(cnt, c->h_counter, 4, hipMemcpyHostToDevice, c->stream));
-            uint32_t live = n;
-            for (uint32_t bounce = 0; live > 0; ++bounce) {
-                HIPC(c, hipMemsetAsync(cnt + (1 - cin), 0, 4, c->stream));
-                HIPC(c, hipMemsetAsync(cnt + 2, 0, 4, c->stream));
-                EventPair et = nextEvents(c);
+            HIPC(c, hipMemcpyAsync(live, c->h_counter, 4, hipMemcpyHostToDevice, c->stream));
+            pg_launch_camera(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + l0, qbuf[0]);
+            uint32_t b = 0;
+            for (;;) {
+                EventPair et = nextEvents(c), es = nextEvents(c), ew = nextEvents(c);
                 HIPC(c, hipEventRecord(et.a, c->stream));
-                pg_launch_trace(c->stream, sc, pv, qin, cnt + cin, live);
+                pg_launch_trace(c->stream, sc, pv, qbuf[b & 1], live + b, n);
                 HIPC(c, hipEventRecord(et.b, c->stream));
-                EventPair es = nextEvents(c);
                 HIPC(c, hipEventRecord(es.a, c->stream));
-                pg_launch_shade(c->stream, g, sc, sd, pv, qin, cnt + cin, live, qout, cnt + (1 - cin), c->qs.as<uint32_t>(),
-                                cnt + 2);
+                pg_launch_shade(c->stream, g, sc, sd, pv, qbuf[b & 1], live + b, n, qbuf[(b + 1) & 1], live + b + 1,
+                                c->qs.as<uint32_t>(), shcnt + b);
                 HIPC(c, hipEventRecord(es.b, c->stream));
-                EventPair ew = nextEvents(c);
                 HIPC(c, hipEventRecord(ew.a, c->stream));
-                pg_launch_shadow(c->stream, sc, pv, c->qs.as<uint32_t>(), cnt + 2, live);
+                pg_launch_shadow(c->stream, sc, pv, c->qs.as<uint32_t>(), shcnt + b, n);
                 HIPC(c, hipEventRecord(ew.b, c->stream));
-                HIPC(c, hipGetLastError());
-                HIPC(c, hipMemcpyAsync(c->h_counter, cnt, 12, hipMemcpyDeviceToHost, c->stream));
-                HIPC(c, hipStreamSynchronize(c->stream));
-                float ms = 0;
-                (void)hipEventElapsedTime(&ms, et.a, et.b);
-                c->stats.trace_ms += ms;
-                c->stats.trace_launches++;
-                (void)hipEventElapsedTime(&ms, es.a, es.b);
-                c->stats.shade_ms += ms;
-                (void)hipEventElapsedTime(&ms, ew.a, ew.b);
-                c->stats.shadow_ms += ms;
-                c->evused = 0;
-                c->stats.segments += live;
-                c->stats.shadow_rays += c->h_counter[2];
-                live = c->h_counter[1 - cin];
-                std::swap(qin, qout);
-                cin = 1 - cin;
-                if (bounce > (uint32_t)c->cfg.gpu_depth_cap + 2) break;
+                ++b;
+                // poll the live count after kFirstPoll bounces, then every kPollEvery
+                if (b >= maxBounces || (b >= kFirstPoll && (b - kFirstPoll) % kPollEvery == 0)) {
+                    HIPC(c, hipGetLastError());
+                    HIPC(c, hipMemcpyAsync(c->h_counter + 4, live + b, 4, hipMemcpyDeviceToHost, c->stream));
+                    HIPC(c, hipStreamSynchronize(c->stream));
+                    if (c->h_counter[4] == 0 || b >= maxBounces) break;
+                }
             }
+            // per-bounce statistics and kernel times of this chunk
+            HIPC(c, hipMemcpyAsync(c->h_counter + 8, live, kCounterWords * 4, hipMemcpyDeviceToHost, c->stream));
             pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
                            c->film_sq.as<float4>());
+            HIPC(c, hipStreamSynchronize(c->stream));
+            for (uint32_t k = 0; k < b; ++k) {
+                c->stats.segments += c->h_counter[8 + k];
+                c->stats.shadow_rays += c->h_counter[8 + kShadowOffset + k];
+            }
+            for (size_t e = 0; e + 2 < c->evused; e += 3) {
+                float ms = 0;
+                (void)hipEventElapsedTime(&ms, c->evpool[e].a, c->evpool[e].b);
+                c->stats.trace_ms += ms;
+                (void)hipEventElapsedTime(&ms, c->evpool[e + 1].a, c->evpool[e + 1].b);
+                c->stats.shade_ms += ms;
+                (void)hipEventElapsedTime(&ms, c->evpool[e + 2].a, c->evpool[e + 2].b);
+                c->stats.shadow_ms += ms;
+                c->stats.trace_launches++;
+            }
+            c->evused = 0;
             if (rec) {
                 // bound: every slot can emit at most max_vertices records
                 if ((s = ensureRecords(c, c->rec_host_count + (uint64_t)n * g.max_vertices))) return s;
@@ -809,11 +823,12 @@ pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hi
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_trace_rays: no scene");
     HIPC(c, hipSetDevice(c->cfg.device));
     if (!n) return PG_OK;
-    DevBuf r, h;
+    DevBuf r, h, ovf;
     HIPC(c, r.alloc(n * 32));
     HIPC(c, h.alloc(n * 16));
+    HIPC(c, ovf.alloc(pg_stack_overflow_words((n + 127) / 128 * 128) * 4));
     HIPC(c, hipMemcpyAsync(r.p, rays, n * 32, hipMemcpyHostToDevice, c->stream));
-    pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, any_hit, h.as<float>());
+    pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, any_hit, h.as<float>(), ovf.as<uint32_t>());
     HIPC(c, hipGetLastError());
     HIPC(c, hipMemcpyAsync(hits, h.p, n * 16, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));

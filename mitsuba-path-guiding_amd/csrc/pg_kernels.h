@@ -20,6 +20,7 @@ struct PathDev {
     uint4 *pinfo;
     float4 *sh_o, *sh_d, *sh_c;
     float4 *vtx;       // [max_vertices][P][3]
+    uint32_t *stack_ovf;  // traversal-stack overflow ring, pg_stack_overflow_words(0) words
     uint32_t P;        // capacity (slot stride of vtx)
 };
 
@@ -50,7 +51,10 @@ void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uin
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
                       unsigned long long *rec_count, unsigned long long rec_capacity);
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n);
-void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits);
+void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits,
+                          uint32_t *ovf);
+// words of traversal-stack overflow storage for a launch of max_threads (0 = persistent grid)
+size_t pg_stack_overflow_words(uint64_t max_threads);
 void pg_launch_bsdf_query(hipStream_t s, const GMat *mat, const float *wi, const float *u, const float *wog,
                           uint32_t n, float *out);
 void pg_launch_sd_pdf(hipStream_t s, const SDDev &sd, const float *pos, const float *dir, uint32_t n, float *out);

@@ -12,8 +12,12 @@
 using namespace pgd;
 
 #define TRACE_BLOCK 128
-#define STACK_DEPTH 48
+#define STACK_DEPTH 48  // total traversal stack (the BVH builder bounds the depth below this)
+#define LDS_STACK 16    // top entries in LDS (8 KiB per block); deeper entries spill to a global ring
 #define SHADE_BLOCK 256
+// persistent grid-stride launches: enough blocks to fill 256 CUs at full occupancy
+#define TRACE_MAX_BLOCKS (256 * 16)
+#define SHADE_MAX_BLOCKS (256 * 8)
 
 namespace {
 
@@ -21,10 +25,25 @@ namespace {
 // BVH traversal (binned-SAH BVH2, 64-B nodes; Woop unit-triangle test, 48-B triangles).
 // Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142, sahkdtree3.h:178-308)
 // with the same contract: closest t in [tmin, tmax] (any hit for shadow rays).
+// Stack: entries [0, LDS_STACK) in LDS (column per thread, stride TRACE_BLOCK: conflict-free),
+// deeper entries in a per-thread column of a global overflow ring (stride = launched threads).
+struct TStack {
+    uint32_t *lds;
+    uint32_t *ovf;
+    uint32_t ostride;
+    __device__ __forceinline__ void put(int i, uint32_t v) {
+        if (i < LDS_STACK) lds[i * TRACE_BLOCK] = v;
+        else ovf[(size_t)(i - LDS_STACK) * ostride] = v;
+    }
+    __device__ __forceinline__ uint32_t get(int i) const {
+        return i < LDS_STACK ? lds[i * TRACE_BLOCK] : ovf[(size_t)(i - LDS_STACK) * ostride];
+    }
+};
+
 template <bool ANY>
 __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
                                          float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                         uint32_t *__restrict__ stk) {
+                                         TStack stk) {
     const float eps = 1e-30f;
     f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
                  1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
@@ -57,7 +76,7 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
                     nearC = ch1;
                     farC = ch0;
                 }
-                if (sp < STACK_DEPTH) stk[(sp++) * TRACE_BLOCK] = (uint32_t)farC;
+                if (sp < STACK_DEPTH) stk.put(sp++, (uint32_t)farC);
                 node = nearC;
                 continue;
             } else if (h0) {
@@ -96,7 +115,7 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
             }
         }
         if (sp == 0) break;
-        node = (int)stk[(--sp) * TRACE_BLOCK];
+        node = (int)stk.get(--sp);
     }
     return found;
 }
@@ -233,42 +252,53 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
 }
 
 // closest hit for every queued path: hit[slot] = (t, BVH-order triangle | ~0, u, v)
+// Persistent grid-stride launches read the live count from device memory, so the host never
+// waits for a bounce to finish before launching the next one.
+__device__ __forceinline__ TStack threadStack(uint32_t *lds, uint32_t *ovf) {
+    const uint32_t gtid = blockIdx.x * TRACE_BLOCK + threadIdx.x;
+    return TStack{lds + threadIdx.x, ovf + gtid, gridDim.x * TRACE_BLOCK};
+}
+
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
                                                        const uint32_t *__restrict__ count) {
-    __shared__ uint32_t stack[STACK_DEPTH * TRACE_BLOCK];
-    uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x;
-    if (i >= *count) return;
-    uint32_t slot = queue[i];
-    float4 o = p.ray_o[slot], d = p.ray_d[slot];
-    float tmax = d.w;
-    uint32_t tri = 0xFFFFFFFFu;
-    float u = 0, v = 0;
-    bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stack + threadIdx.x);
-    p.hit[slot] = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, p.stack_ovf);
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
+        uint32_t slot = queue[i];
+        float4 o = p.ray_o[slot], d = p.ray_d[slot];
+        float tmax = d.w;
+        uint32_t tri = 0xFFFFFFFFu;
+        float u = 0, v = 0;
+        bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+        p.hit[slot] = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+    }
 }
 
 // any hit for queued shadow rays; unoccluded -> add the NEE contribution to L (and to the
 // training vertex's radiance snapshot, so its record excludes light arriving from elsewhere)
 __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
                                                         const uint32_t *__restrict__ count) {
-    __shared__ uint32_t stack[STACK_DEPTH * TRACE_BLOCK];
-    uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x;
-    if (i >= *count) return;
-    uint32_t slot = queue[i];
-    float4 o = p.sh_o[slot], d = p.sh_d[slot];
-    float tmax = d.w;
-    uint32_t tri;
-    float u, v;
-    bool occ = traverse<true>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stack + threadIdx.x);
-    if (!occ) {
-        float4 c = p.sh_c[slot];
-        float4 L = p.rad[slot];
-        p.rad[slot] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
-        uint32_t vi = __float_as_uint(c.w);
-        if (vi != 0xFFFFFFFFu) {
-            float4 *vl = p.vtx + ((size_t)vi * p.P + slot) * 3 + 2;
-            float4 a = *vl;
-            *vl = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w);
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, p.stack_ovf);
+    const uint32_t n = *count;
+    for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
+        uint32_t slot = queue[i];
+        float4 o = p.sh_o[slot], d = p.sh_d[slot];
+        float tmax = d.w;
+        uint32_t tri;
+        float u, v;
+        bool occ = traverse<true>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+        if (!occ) {
+            float4 c = p.sh_c[slot];
+            float4 L = p.rad[slot];
+            p.rad[slot] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
+            uint32_t vi = __float_as_uint(c.w);
+            if (vi != 0xFFFFFFFFu) {
+                float4 *vl = p.vtx + ((size_t)vi * p.P + slot) * 3 + 2;
+                float4 a = *vl;
+                *vl = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w);
+            }
         }
     }
 }
@@ -280,11 +310,14 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                                                        uint32_t *__restrict__ queue_out, uint32_t *__restrict__ count_out,
                                                        uint32_t *__restrict__ shadow_queue,
                                                        uint32_t *__restrict__ shadow_count) {
-    uint32_t i = blockIdx.x * SHADE_BLOCK + threadIdx.x;
+    const uint32_t n = *count_in;
+    // block-uniform loop bound, so every wave reaches the ballots of waveAppend together
+    for (uint32_t base = blockIdx.x * SHADE_BLOCK; base < n; base += gridDim.x * SHADE_BLOCK) {
+    const uint32_t i = base + threadIdx.x;
     bool alive = false, shadow = false, dirtyL = false;
     uint32_t slot = 0;
     f3 L = mk1(0.f);
-    if (i < *count_in) {
+    if (i < n) {
         slot = queue_in[i];
         do {
             uint4 pi = p.pinfo[slot];
@@ -449,6 +482,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
     }
     waveAppend(alive, slot, queue_out, count_out);
     waveAppend(shadow, slot, shadow_queue, shadow_count);
+    }
 }
 
 // film: box-filtered accumulation of every layer's sample into its pixel, in sample order
@@ -564,8 +598,9 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
 
 // ---- unit-level kernels used by the parity tests ---------------------------------------------
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const float *__restrict__ rays, uint32_t n,
-                                                            int any, float *__restrict__ hits) {
-    __shared__ uint32_t stack[STACK_DEPTH * TRACE_BLOCK];
+                                                            int any, float *__restrict__ hits, uint32_t *ovf) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, ovf);
     uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x;
     if (i >= n) return;
     const float *r = rays + 8 * (size_t)i;
@@ -575,12 +610,12 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const f
     float u = 0, v = 0;
     float *h = hits + 4 * (size_t)i;
     if (any) {
-        bool occ = traverse<true>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stack + threadIdx.x);
+        bool occ = traverse<true>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stk);
         h[0] = occ ? 1.0f : 0.0f;
         h[1] = h[2] = h[3] = 0.0f;
         return;
     }
-    bool hit = traverse<false>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stack + threadIdx.x);
+    bool hit = traverse<false>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stk);
     uint32_t orig = hit ? __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w) : 0xFFFFFFFFu;
     h[0] = hit ? tmax : 0.0f;
     h[1] = __uint_as_float(orig);
@@ -644,6 +679,11 @@ __global__ __launch_bounds__(256) void k_sd_sample(SDDev sd, const float *pos, c
 // =============================================================================================
 static inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b - 1) / b); }
 
+size_t pg_stack_overflow_words(uint64_t max_threads) {
+    if (max_threads == 0) max_threads = (uint64_t)TRACE_MAX_BLOCKS * TRACE_BLOCK;
+    return (size_t)(STACK_DEPTH - LDS_STACK) * max_threads;
+}
+
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
                       uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, uint32_t *queue) {
     uint64_t n = (uint64_t)npix * nlayers;
@@ -654,19 +694,19 @@ void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const u
 void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
                      uint32_t max_count) {
     if (!max_count) return;
-    hipLaunchKernelGGL(k_trace, dim3(blocks(max_count, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
+    hipLaunchKernelGGL(k_trace, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
 }
 void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
                      const uint32_t *queue_in, const uint32_t *count_in, uint32_t max_count, uint32_t *queue_out,
                      uint32_t *count_out, uint32_t *shadow_queue, uint32_t *shadow_count) {
     if (!max_count) return;
-    hipLaunchKernelGGL(k_shade, dim3(blocks(max_count, SHADE_BLOCK)), dim3(SHADE_BLOCK), 0, s, g, sc, sd, p, queue_in,
+    hipLaunchKernelGGL(k_shade, dim3(min(blocks(max_count, SHADE_BLOCK), (uint32_t)SHADE_MAX_BLOCKS)), dim3(SHADE_BLOCK), 0, s, g, sc, sd, p, queue_in,
                        count_in, queue_out, count_out, shadow_queue, shadow_count);
 }
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
                       uint32_t max_count) {
     if (!max_count) return;
-    hipLaunchKernelGGL(k_shadow, dim3(blocks(max_count, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
+    hipLaunchKernelGGL(k_shadow, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
 }
 void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
                     uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq) {
@@ -684,9 +724,10 @@ void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsi
     if (!n) return;
     hipLaunchKernelGGL(k_splat, dim3(blocks(n, 256)), dim3(256), 0, s, sd, recs, n);
 }
-void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits) {
+void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits,
+                          uint32_t *ovf) {
     if (!n) return;
-    hipLaunchKernelGGL(k_trace_rays, dim3(blocks(n, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, rays, n, any, hits);
+    hipLaunchKernelGGL(k_trace_rays, dim3(blocks(n, TRACE_BLOCK)), dim3(TRACE_BLOCK), 0, s, sc, rays, n, any, hits, ovf);
 }
 void pg_launch_bsdf_query(hipStream_t s, const GMat *mat, const float *wi, const float *u, const float *wog, uint32_t n,
                           float *out) {
