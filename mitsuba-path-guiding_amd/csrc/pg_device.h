@@ -647,8 +647,10 @@ struct SDView {
     const uint4 *meta;      // per D-tree: sampling root, building root, count, bits(samplingTotal)
     const float4 *qsum;     // sampling nodes
     const uint4 *qchild;
+    const uint32_t *jump;   // S-tree jump grid: (2^jumpBits)^3 cells -> node at depth <= 3*jumpBits
     float3 lo;
     float extent;           // cube edge; lookups divide by it (bit-identical with the host spec)
+    int jumpBits;
     int built;
 };
 
@@ -657,9 +659,19 @@ PGD uint32_t sdLookup(const SDView &v, f3 p) {
     q[0] = fminf(fmaxf((p.x - v.lo.x) / v.extent, 0.0f), 1.0f);
     q[1] = fminf(fmaxf((p.y - v.lo.y) / v.extent, 0.0f), 1.0f);
     q[2] = fminf(fmaxf((p.z - v.lo.z) / v.extent, 0.0f), 1.0f);
-    uint32_t n = 0;
+    // Jump grid: the first 3*jumpBits axis-cycling midpoint decisions are the bits of
+    // floor(q * 2^jumpBits) per axis, and the residual q*2^k - i is exactly what k sequential
+    // (2q | 2q - 1) steps produce, so this is bit-identical with the plain descent.
+    const int R = 1 << v.jumpBits;
+    const float fR = (float)R;
+    int ix = min((int)(q[0] * fR), R - 1), iy = min((int)(q[1] * fR), R - 1), iz = min((int)(q[2] * fR), R - 1);
+    uint32_t n = v.jump[((size_t)iz * R + iy) * R + ix];
+    uint2 nd = v.snodes[n];
+    if (nd.x == 0xFFFFFFFFu) return nd.y;
+    q[0] = q[0] * fR - (float)ix;
+    q[1] = q[1] * fR - (float)iy;
+    q[2] = q[2] * fR - (float)iz;
     int axis = 0;
-    uint2 nd = v.snodes[0];
     while (nd.x != 0xFFFFFFFFu) {
         float x = axis == 0 ? q[0] : (axis == 1 ? q[1] : q[2]);
         if (x < 0.5f) {
@@ -676,23 +688,24 @@ PGD uint32_t sdLookup(const SDView &v, f3 p) {
     return nd.y;
 }
 
+// pdf = prod_l 4 E_q(l) / E_node(l) / 4pi telescoped to 4^d E_leafquadrant / E_root / 4pi: the
+// descent reads only child links; the energies are read once, at the leaf quadrant.
+PGD float telescopedPdf(float leafEnergy, float rootTotal, int depth) {
+    if (!(leafEnergy > 0)) return 0.0f;
+    return ldexpf(leafEnergy / rootTotal, 2 * depth) * kInvFourPi;
+}
 PGD float sdPdfCanon(const SDView &v, uint4 meta, float u, float w) {
     float total = __uint_as_float(meta.w);
     if (!(total > 0)) return kInvFourPi;
     uint32_t n = meta.x;
-    float result = 1.0f;
-    for (int guard = 0; guard < 64; ++guard) {
-        float4 s = v.qsum[n];
+    int depth = 1;
+    for (int guard = 0; guard < 64; ++guard, ++depth) {
         int q = childIndex(u, w);
-        float sq = q4(s, q);
-        if (!(sq > 0)) return 0.0f;
-        float factor = 4.0f * sq / quadTotal(s);
-        result = result * factor;
         uint32_t c = c4(v.qchild[n], q);
-        if (c == 0) break;
+        if (c == 0) return telescopedPdf(q4(v.qsum[n], q), total, depth);
         n = c;
     }
-    return result * kInvFourPi;
+    return 0.0f;
 }
 PGD float sdPdf(const SDView &v, uint4 meta, f3 d) {
     if (!(__uint_as_float(meta.w) > 0)) return kInvFourPi;
@@ -709,14 +722,16 @@ PGD void sdSampleCanon(const SDView &v, uint4 meta, float px, float py, float &c
         return;
     }
     uint32_t n = meta.x;
-    float ox = 0, oy = 0, scale = 1, result = 1;
+    float ox = 0, oy = 0, scale = 1;
+    int depth = 0;
+    float parentEnergy = total0;
     for (int guard = 0; guard < 64; ++guard) {
         float4 s = v.qsum[n];
         float total = quadTotal(s);
         if (!(total > 0)) {
             cu = ox + scale * px;
             cv = oy + scale * py;
-            pdf = result * kInvFourPi;
+            pdf = telescopedPdf(parentEnergy, total0, depth);
             return;
         }
         float partial = s.x + s.z;
@@ -742,17 +757,23 @@ PGD void sdSampleCanon(const SDView &v, uint4 meta, float px, float py, float &c
         }
         px = fminf(fmaxf(px, 0.0f), 0.99999994f);
         py = fminf(fmaxf(py, 0.0f), 0.99999994f);
-        result = result * (4.0f * q4(s, q) / total);
         ox = ox + scale * qx;
         oy = oy + scale * qy;
         scale = scale * 0.5f;
+        ++depth;
         uint32_t c = c4(v.qchild[n], q);
-        if (c == 0) break;
+        if (c == 0) {
+            cu = ox + scale * px;
+            cv = oy + scale * py;
+            pdf = telescopedPdf(q4(s, q), total0, depth);
+            return;
+        }
+        parentEnergy = q4(s, q);
         n = c;
     }
     cu = ox + scale * px;
     cv = oy + scale * py;
-    pdf = result * kInvFourPi;
+    pdf = 0.0f;
 }
 #pragma clang fp contract(on)
 

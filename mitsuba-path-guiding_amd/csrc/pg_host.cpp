@@ -24,7 +24,8 @@ namespace {
 constexpr uint32_t kStackDepth = 48;  // must match STACK_DEPTH in pg_kernels.hip
 constexpr uint32_t kMaxBounces = 1100;     // > gpu_depth_cap default (1024) + 2
 constexpr uint32_t kShadowOffset = 1104;   // shadow[b] lives at counters[kShadowOffset + b]
-constexpr uint32_t kCounterWords = 2 * 1104;
+constexpr uint32_t kFetchOffset = 2 * 1104;  // per bounce: 8 trace + 8 shadow fetch shards
+constexpr uint32_t kCounterWords = kFetchOffset + 16 * 1104;
 constexpr uint32_t kFirstPoll = 12, kPollEvery = 6;
 
 struct DevBuf {
@@ -81,7 +82,8 @@ struct Ctx {
     DevBuf ext_records;
     // sd-tree
     pgh::SdTree sd;
-    DevBuf sd_snodes, sd_meta, sd_qsum, sd_qchild, sd_bchild, sd_bsum, sd_count;
+    DevBuf sd_snodes, sd_meta, sd_qsum, sd_qchild, sd_bchild, sd_bsum, sd_count, sd_jump;
+    int sd_jump_bits = 0;
     bool sd_dirty = true;
     // stats
     pg_stats stats{};
@@ -217,6 +219,8 @@ SDDev sdView(const Ctx *c) {
     s.bchild = c->sd_bchild.as<uint4>();
     s.bsum = c->sd_bsum.as<unsigned long long>();
     s.count = c->sd_count.as<uint32_t>();
+    s.jump = c->sd_jump.as<uint32_t>();
+    s.jump_bits = c->sd_jump_bits;
     for (int a = 0; a < 3; ++a) s.lo[a] = c->sd.lo[a];
     s.extent = c->sd.extent;
     s.built = c->sd.built ? 1 : 0;
@@ -236,11 +240,12 @@ pg_status uploadSd(Ctx *c) {
     if ((s = upload(c, c->sd_snodes, f.snodes)) || (s = upload(c, c->sd_meta, f.meta)) ||
         (s = upload(c, c->sd_qsum, f.qsum)) || (s = upload(c, c->sd_qchild, f.qchild)) ||
         (s = upload(c, c->sd_bchild, f.bchild)) || (s = upload(c, c->sd_bsum, f.bsum)) ||
-        (s = upload(c, c->sd_count, f.count)))
+        (s = upload(c, c->sd_count, f.count)) || (s = upload(c, c->sd_jump, f.jump)))
         return s;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->stats.stree_nodes = c->sd.snode.size() / 2;
     c->stats.dtree_nodes = c->sd.samplingNodes();
+    c->sd_jump_bits = f.jump_bits;
     c->sd_dirty = false;
     return PG_OK;
 }
@@ -590,14 +595,14 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             for (;;) {
                 EventPair et = nextEvents(c), es = nextEvents(c), ew = nextEvents(c);
                 HIPC(c, hipEventRecord(et.a, c->stream));
-                pg_launch_trace(c->stream, sc, pv, qbuf[b & 1], live + b, n);
+                pg_launch_trace(c->stream, sc, pv, qbuf[b & 1], live + b, n, live + kFetchOffset + 16 * b);
                 HIPC(c, hipEventRecord(et.b, c->stream));
                 HIPC(c, hipEventRecord(es.a, c->stream));
                 pg_launch_shade(c->stream, g, sc, sd, pv, qbuf[b & 1], live + b, n, qbuf[(b + 1) & 1], live + b + 1,
                                 c->qs.as<uint32_t>(), shcnt + b);
                 HIPC(c, hipEventRecord(es.b, c->stream));
                 HIPC(c, hipEventRecord(ew.a, c->stream));
-                pg_launch_shadow(c->stream, sc, pv, c->qs.as<uint32_t>(), shcnt + b, n);
+                pg_launch_shadow(c->stream, sc, pv, c->qs.as<uint32_t>(), shcnt + b, n, live + kFetchOffset + 16 * b + 8);
                 HIPC(c, hipEventRecord(ew.b, c->stream));
                 ++b;
                 // poll the live count after kFirstPoll bounces, then every kPollEvery
@@ -609,7 +614,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
                 }
             }
             // per-bounce statistics and kernel times of this chunk
-            HIPC(c, hipMemcpyAsync(c->h_counter + 8, live, kCounterWords * 4, hipMemcpyDeviceToHost, c->stream));
+            HIPC(c, hipMemcpyAsync(c->h_counter + 8, live, kFetchOffset * 4, hipMemcpyDeviceToHost, c->stream));
             pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
                            c->film_sq.as<float4>());
             HIPC(c, hipStreamSynchronize(c->stream));

@@ -32,20 +32,23 @@ struct SDDev {
     const uint4 *bchild;
     unsigned long long *bsum;  // 4 per building node
     uint32_t *count;           // per D-tree
+    const uint32_t *jump;      // S-tree jump grid, (2^jump_bits)^3 node ids
     float lo[3];
     float extent;
+    int jump_bits;
     int built;
 };
 
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
                       uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, uint32_t *queue);
+// fetch: FETCH_SHARDS (8) zeroed work counters for this launch
 void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue,
-                     const uint32_t *count, uint32_t max_count);
+                     const uint32_t *count, uint32_t max_count, uint32_t *fetch);
 void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
                      const uint32_t *queue_in, const uint32_t *count_in, uint32_t max_count, uint32_t *queue_out,
                      uint32_t *count_out, uint32_t *shadow_queue, uint32_t *shadow_count);
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue,
-                      const uint32_t *count, uint32_t max_count);
+                      const uint32_t *count, uint32_t max_count, uint32_t *fetch);
 void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
                     uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq);
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,

@@ -31,7 +31,7 @@ struct TStack {
     uint32_t *lds;
     uint32_t *ovf;
     uint32_t ostride;
-    __device__ __forceinline__ void put(int i, uint32_t v) {
+    __device__ __forceinline__ void put(int i, uint32_t v) const {
         if (i < LDS_STACK) lds[i * TRACE_BLOCK] = v;
         else ovf[(size_t)(i - LDS_STACK) * ostride] = v;
     }
@@ -40,20 +40,122 @@ struct TStack {
     }
 };
 
+// Traversal state of one ray, advanced one node (inner node or whole leaf) per step so that
+// persistent kernels can interleave steps with refilling idle lanes.
+struct Trav {
+    f3 o, d, idir, ood;
+    float tmin, tmax;
+    int node, sp;
+    uint32_t tri;
+    float u, v;
+    bool found;
+};
+
+__device__ __forceinline__ void travInit(Trav &t, f3 o, f3 d, float tmin, float tmax) {
+    const float eps = 1e-30f;
+    t.o = o;
+    t.d = d;
+    t.idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)), 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
+                1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+    t.ood = o * t.idir;
+    t.tmin = tmin;
+    t.tmax = tmax;
+    t.node = 0;
+    t.sp = 0;
+    t.tri = 0xFFFFFFFFu;
+    t.u = t.v = 0.0f;
+    t.found = false;
+}
+
+// One traversal step; returns true when the ray is finished (closest hit known, or any hit found).
+template <bool ANY>
+__device__ __forceinline__ bool travStep(const float4 *__restrict__ nodes, const float4 *__restrict__ woop,
+                                         const TStack &stk, Trav &t) {
+    if (t.node >= 0) {
+        const float4 n0 = nodes[4 * t.node + 0];
+        const float4 n1 = nodes[4 * t.node + 1];
+        const float4 n2 = nodes[4 * t.node + 2];
+        const float4 n3 = nodes[4 * t.node + 3];
+        const f3 idir = t.idir, ood = t.ood;
+        float a0 = fmaf(n0.x, idir.x, -ood.x), a1 = fmaf(n0.y, idir.x, -ood.x);
+        float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
+        float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
+        float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), t.tmin));
+        float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t.tmax));
+        float b0 = fmaf(n1.x, idir.x, -ood.x), b1 = fmaf(n1.y, idir.x, -ood.x);
+        float b2 = fmaf(n1.z, idir.y, -ood.y), b3 = fmaf(n1.w, idir.y, -ood.y);
+        float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
+        float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), t.tmin));
+        float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t.tmax));
+        bool h0 = c0min <= c0max, h1 = c1min <= c1max;
+        int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+        if (h0 && h1) {
+            int nearC = ch0, farC = ch1;
+            if (c1min < c0min) {
+                nearC = ch1;
+                farC = ch0;
+            }
+            if (t.sp < STACK_DEPTH) stk.put(t.sp++, (uint32_t)farC);
+            t.node = nearC;
+            return false;
+        }
+        if (h0 | h1) {
+            t.node = h0 ? ch0 : ch1;
+            return false;
+        }
+    } else {
+        uint32_t leaf = ~(uint32_t)t.node;
+        uint32_t first = leaf >> 4, cnt = leaf & 15u;
+        const f3 o = t.o, d = t.d;
+        for (uint32_t k = 0; k < cnt; ++k) {
+            uint32_t tr = first + k;
+            const float4 w0 = woop[3 * tr + 0];
+            float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
+            float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
+            float tt = oz / dz;
+            if (tt >= t.tmin && tt <= t.tmax) {
+                const float4 w1 = woop[3 * tr + 1];
+                float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
+                if (a >= 0.0f && a <= 1.0f) {
+                    const float4 w2 = woop[3 * tr + 2];
+                    float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
+                    if (b >= 0.0f && a + b <= 1.0f) {
+                        t.found = true;
+                        if (ANY) return true;
+                        t.tmax = tt;
+                        t.tri = tr;
+                        t.u = b;             // weight of p1
+                        t.v = 1.0f - a - b;  // weight of p2
+                    }
+                }
+            }
+        }
+    }
+    if (t.sp == 0) return true;
+    t.node = (int)stk.get(--t.sp);
+    return false;
+}
+
+// While-while traversal with postponed leaves (Aila & Laine 2009): lanes keep descending inner
+// nodes until every lane of the wave holds a leaf, then all lanes test triangles together.  This
+// keeps the 64-wide wave in one code path most of the time (if-if traversal measured 23 % lane
+// utilisation on gfx950).
 template <bool ANY>
 __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
                                          float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                         TStack stk) {
+                                         const TStack &stk) {
+    const int DONE = 0x7fffffff;
     const float eps = 1e-30f;
-    f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
-                 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-                 1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
-    f3 ood = o * idir;
+    const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
+                       1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
+                       1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+    const f3 ood = o * idir;
     int sp = 0;
-    int node = 0;
+    int node = 0;   // >= 0 inner node, < 0 leaf ref, DONE
+    int leaf = 0;   // postponed leaf ref (< 0) or none (>= 0)
     bool found = false;
-    for (;;) {
-        if (node >= 0) {
+    while (node != DONE) {
+        while (node >= 0 && node != DONE) {
             const float4 n0 = nodes[4 * node + 0];
             const float4 n1 = nodes[4 * node + 1];
             const float4 n2 = nodes[4 * node + 2];
@@ -68,54 +170,58 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
             float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
             float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), tmin));
             float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tmax));
-            bool h0 = c0min <= c0max, h1 = c1min <= c1max;
-            int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
-            if (h0 && h1) {
-                int nearC = ch0, farC = ch1;
-                if (c1min < c0min) {
-                    nearC = ch1;
-                    farC = ch0;
+            const bool h0 = c0min <= c0max, h1 = c1min <= c1max;
+            const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
+            if (!h0 && !h1) {
+                node = sp > 0 ? (int)stk.get(--sp) : DONE;
+            } else {
+                node = h0 ? ch0 : ch1;
+                if (h0 && h1) {
+                    int farC = ch1;
+                    if (c1min < c0min) {
+                        node = ch1;
+                        farC = ch0;
+                    }
+                    if (sp < STACK_DEPTH) stk.put(sp++, (uint32_t)farC);
                 }
-                if (sp < STACK_DEPTH) stk.put(sp++, (uint32_t)farC);
-                node = nearC;
-                continue;
-            } else if (h0) {
-                node = ch0;
-                continue;
-            } else if (h1) {
-                node = ch1;
-                continue;
             }
-        } else {
-            uint32_t leaf = ~(uint32_t)node;
-            uint32_t first = leaf >> 4, cnt = leaf & 15u;
+            // first leaf found: postpone it and keep descending
+            if (node < 0 && leaf >= 0) {
+                leaf = node;
+                node = sp > 0 ? (int)stk.get(--sp) : DONE;
+            }
+            if (!__any(leaf >= 0)) break;  // every lane still here holds a leaf
+        }
+        while (leaf < 0) {
+            const uint32_t lr = ~(uint32_t)leaf;
+            const uint32_t first = lr >> 4, cnt = lr & 15u;
             for (uint32_t k = 0; k < cnt; ++k) {
-                uint32_t t = first + k;
-                const float4 w0 = woop[3 * t + 0];
+                const uint32_t tr = first + k;
+                const float4 w0 = woop[3 * tr + 0];
                 float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
                 float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
                 float tt = oz / dz;
                 if (tt >= tmin && tt <= tmax) {
-                    const float4 w1 = woop[3 * t + 1];
+                    const float4 w1 = woop[3 * tr + 1];
                     float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
                     if (a >= 0.0f && a <= 1.0f) {
-                        const float4 w2 = woop[3 * t + 2];
-                        float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) +
-                                  tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
+                        const float4 w2 = woop[3 * tr + 2];
+                        float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
                         if (b >= 0.0f && a + b <= 1.0f) {
                             found = true;
                             if (ANY) return true;
                             tmax = tt;
-                            hitTri = t;
+                            hitTri = tr;
                             hu = b;             // weight of p1
                             hv = 1.0f - a - b;  // weight of p2
                         }
                     }
                 }
             }
+            // another postponed leaf (in node)?  process it too
+            leaf = node;
+            if (node < 0) node = sp > 0 ? (int)stk.get(--sp) : DONE;
         }
-        if (sp == 0) break;
-        node = (int)stk.get(--sp);
     }
     return found;
 }
@@ -139,6 +245,11 @@ __device__ __forceinline__ void waveAppend(bool pred, uint32_t value, uint32_t *
         unsigned long long below = m & ((1ull << lane) - 1ull);
         q[base + __popcll(below)] = value;
     }
+}
+
+__device__ __forceinline__ SDView sdv(const SDDev &sd) {
+    return SDView{sd.snodes, sd.meta, sd.qsum, sd.qchild, sd.jump, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]),
+                  sd.extent, sd.jump_bits, sd.built};
 }
 
 struct Hit {
@@ -259,8 +370,20 @@ __device__ __forceinline__ TStack threadStack(uint32_t *lds, uint32_t *ovf) {
     return TStack{lds + threadIdx.x, ovf + gtid, gridDim.x * TRACE_BLOCK};
 }
 
+// Persistent traversal with dynamic ray fetch.  A wave keeps 64 rays in flight; when at least
+// REFILL_MIN lanes have finished, the finished lanes take new rays from a wave-local batch of 64
+// queue entries (one atomic per batch on one of 8 shard counters, selected by blockIdx % 8).
+// This keeps lanes busy while the long rays of a wave finish, which matters on 64-wide waves.
+#define REFILL_MIN 16
+#define TRAV_STEPS 8
+#define FETCH_SHARDS 8
+#define FETCH_BATCH 64
+
+// closest hit for every queued path: hit[slot] = (t, BVH-order triangle | ~0, u, v).
+// `fetch` (zeroed per launch) is reserved for dynamic ray fetch, which measured slower than a
+// plain grid-stride loop once traversal was made while-while.
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
-                                                       const uint32_t *__restrict__ count) {
+                                                       const uint32_t *__restrict__ count, uint32_t *__restrict__ fetch) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, p.stack_ovf);
     const uint32_t n = *count;
@@ -278,7 +401,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, c
 // any hit for queued shadow rays; unoccluded -> add the NEE contribution to L (and to the
 // training vertex's radiance snapshot, so its record excludes light arriving from elsewhere)
 __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
-                                                        const uint32_t *__restrict__ count) {
+                                                        const uint32_t *__restrict__ count, uint32_t *__restrict__ fetch) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, p.stack_ovf);
     const uint32_t n = *count;
@@ -373,8 +496,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 break;
             const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
             const bool guide = g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
-            SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent,
-                      sd.built};
+            const SDView sv = sdv(sd);
             uint4 meta = make_uint4(0, 0, 0, 0);
             if (guide) meta = sd.meta[sdLookup(sv, h.p)];
             const float alpha = g.bsdf_fraction;
@@ -578,7 +700,7 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
     float s = val * 16777216.0f;
     if (s >= 4.0e18f) s = 4.0e18f;
     unsigned long long fx = (unsigned long long)s;
-    SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent, sd.built};
+    const SDView sv = sdv(sd);
     uint32_t dt = sdLookup(sv, mk(a.x, a.y, a.z));
     atomicAdd(sd.count + dt, 1u);
     uint32_t dirw = __float_as_uint(a.w);
@@ -656,7 +778,7 @@ __global__ __launch_bounds__(256) void k_bsdf_query(const GMat *mat, const float
 __global__ __launch_bounds__(256) void k_sd_pdf(SDDev sd, const float *pos, const float *dir, uint32_t n, float *out) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent, sd.built};
+    const SDView sv = sdv(sd);
     uint4 meta = sd.meta[sdLookup(sv, mk(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]))];
     out[i] = sdPdf(sv, meta, mk(dir[3 * i], dir[3 * i + 1], dir[3 * i + 2]));
 }
@@ -665,7 +787,7 @@ __global__ __launch_bounds__(256) void k_sd_sample(SDDev sd, const float *pos, c
                                                    float *pdf) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    SDView sv{sd.snodes, sd.meta, sd.qsum, sd.qchild, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]), sd.extent, sd.built};
+    const SDView sv = sdv(sd);
     uint4 meta = sd.meta[sdLookup(sv, mk(pos[3 * i], pos[3 * i + 1], pos[3 * i + 2]))];
     float cu, cv, pd;
     sdSampleCanon(sv, meta, u[2 * i], u[2 * i + 1], cu, cv, pd);
@@ -692,9 +814,10 @@ void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const u
                        sample_base, queue);
 }
 void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
-                     uint32_t max_count) {
+                     uint32_t max_count, uint32_t *fetch) {
     if (!max_count) return;
-    hipLaunchKernelGGL(k_trace, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
+    hipLaunchKernelGGL(k_trace, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p,
+                       queue, count, fetch);
 }
 void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
                      const uint32_t *queue_in, const uint32_t *count_in, uint32_t max_count, uint32_t *queue_out,
@@ -704,9 +827,10 @@ void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const 
                        count_in, queue_out, count_out, shadow_queue, shadow_count);
 }
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
-                      uint32_t max_count) {
+                      uint32_t max_count, uint32_t *fetch) {
     if (!max_count) return;
-    hipLaunchKernelGGL(k_shadow, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p, queue, count);
+    hipLaunchKernelGGL(k_shadow, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p,
+                       queue, count, fetch);
 }
 void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
                     uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq) {

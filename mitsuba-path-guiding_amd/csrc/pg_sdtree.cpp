@@ -133,8 +133,37 @@ size_t SdTree::buildingNodes() const {
     return n;
 }
 
+// Jump grid for the device lookup: cell (x, y, z) of a 2^k grid -> the S-tree node reached after
+// following the cell's bits for 3k axis-cycling levels (or the leaf met on the way).
+static void fillJump(const std::vector<uint32_t> &sn, uint32_t node, int depth, int k, uint32_t x0, uint32_t y0,
+                     uint32_t z0, uint32_t sx, uint32_t sy, uint32_t sz, std::vector<uint32_t> &jump) {
+    const uint32_t R = 1u << k;
+    if (sn[2 * node] == kLeafMark || depth == 3 * k) {
+        for (uint32_t z = z0; z < z0 + sz; ++z)
+            for (uint32_t y = y0; y < y0 + sy; ++y)
+                for (uint32_t x = x0; x < x0 + sx; ++x) jump[((size_t)z * R + y) * R + x] = node;
+        return;
+    }
+    const int axis = depth % 3;
+    uint32_t c0 = sn[2 * node], c1 = sn[2 * node + 1];
+    if (axis == 0) {
+        fillJump(sn, c0, depth + 1, k, x0, y0, z0, sx / 2, sy, sz, jump);
+        fillJump(sn, c1, depth + 1, k, x0 + sx / 2, y0, z0, sx / 2, sy, sz, jump);
+    } else if (axis == 1) {
+        fillJump(sn, c0, depth + 1, k, x0, y0, z0, sx, sy / 2, sz, jump);
+        fillJump(sn, c1, depth + 1, k, x0, y0 + sy / 2, z0, sx, sy / 2, sz, jump);
+    } else {
+        fillJump(sn, c0, depth + 1, k, x0, y0, z0, sx, sy, sz / 2, jump);
+        fillJump(sn, c1, depth + 1, k, x0, y0, z0 + sz / 2, sx, sy, sz / 2, jump);
+    }
+}
+
 void SdTree::flatten(Flat &f) const {
     f.snodes = snode;
+    f.jump_bits = 6;
+    const uint32_t R = 1u << f.jump_bits;
+    f.jump.assign((size_t)R * R * R, 0);
+    fillJump(snode, 0, 0, f.jump_bits, 0, 0, 0, R, R, R, f.jump);
     f.meta.assign(4 * leaves.size(), 0);
     size_t ns = samplingNodes(), nb = buildingNodes();
     f.qsum.assign(4 * ns, 0.0f);

@@ -47,6 +47,8 @@ struct SdTree {
         std::vector<uint32_t> bchild;   // 4 per building node (absolute)
         std::vector<uint64_t> bsum;     // 4 per building node
         std::vector<uint32_t> count;    // per leaf
+        std::vector<uint32_t> jump;     // (2^jump_bits)^3 S-tree node ids, index (z * R + y) * R + x
+        int jump_bits = 0;
     };
     void flatten(Flat &f) const;
     // absorb device-side building sums/counts (same absolute layout as flatten())

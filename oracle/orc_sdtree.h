@@ -130,21 +130,22 @@ struct SDTree {
         dirToCanonical(d, u, v);
         return pdfCanon(dt, u, v);
     }
+    // pdf = prod_l 4 E_q(l) / E_node(l) / 4pi, telescoped to 4^d E_leafquadrant / E_root / 4pi
+    static float telescopedPdf(float leafEnergy, float rootTotal, int depth) {
+        if (!(leafEnergy > 0)) return 0.0f;
+        return std::ldexp(leafEnergy / rootTotal, 2 * depth) * kInvFourPi;
+    }
     static float pdfCanon(const DTreeW &dt, float u, float v) {
         if (!(dt.samplingTotal > 0)) return kInvFourPi;
         uint32_t n = 0;
-        float result = 1.0f;
+        int depth = 1;
         for (;;) {
             const QNode &nd = dt.sampling[n];
             int q = childIndex(u, v);
-            float s = nd.sum[q];
-            if (!(s > 0)) return 0.0f;
-            float factor = 4.0f * s / nodeTotal(nd.sum);
-            result = result * factor;
-            if (nd.child[q] == 0) break;
+            if (nd.child[q] == 0) return telescopedPdf(nd.sum[q], dt.samplingTotal, depth);
             n = nd.child[q];
+            ++depth;
         }
-        return result * kInvFourPi;
     }
     // returns world direction; pdf computed along the sampled path
     static V3 sampleDir(const DTreeW &dt, float u, float v, float &pdf) {
@@ -160,14 +161,16 @@ struct SDTree {
             return;
         }
         uint32_t n = 0;
-        float ox = 0, oy = 0, scale = 1, result = 1;
+        float ox = 0, oy = 0, scale = 1;
+        int depth = 0;
+        float parentEnergy = dt.samplingTotal;
         for (;;) {
             const QNode &nd = dt.sampling[n];
             float total = nodeTotal(nd.sum);
             if (!(total > 0)) {  // degenerate node: uniform inside it
                 cu = ox + scale * px;
                 cv = oy + scale * py;
-                pdf = result * kInvFourPi;
+                pdf = telescopedPdf(parentEnergy, dt.samplingTotal, depth);
                 return;
             }
             float partial = nd.sum[0] + nd.sum[2];
@@ -193,16 +196,17 @@ struct SDTree {
             }
             px = std::min(std::max(px, 0.0f), 0.99999994f);
             py = std::min(std::max(py, 0.0f), 0.99999994f);
-            result = result * (4.0f * nd.sum[q] / total);
             ox = ox + scale * qx;
             oy = oy + scale * qy;
             scale = scale * 0.5f;
+            ++depth;
             if (nd.child[q] == 0) {
                 cu = ox + scale * px;
                 cv = oy + scale * py;
-                pdf = result * kInvFourPi;
+                pdf = telescopedPdf(nd.sum[q], dt.samplingTotal, depth);
                 return;
             }
+            parentEnergy = nd.sum[q];
             n = nd.child[q];
         }
     }
