@@ -369,8 +369,9 @@ PGD float plasticProbSpec(const GMat &M, float Fi) {
 }
 
 // f * cos(theta_o), solid-angle measure (BSDF::eval with ESolidAngle)
+template <int MODEL = -1>
 PGD f3 bsdfEval1(const GMat &M, f3 wi, f3 wo) {
-    switch (M.model) {
+    switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
         case PG_BSDF_DIFFUSE:  // diffuse.cpp:116-124
             if (wi.z <= 0 || wo.z <= 0) return mk1(0.f);
             return diffOf(M) * (kInvPi * wo.z);
@@ -411,8 +412,9 @@ PGD f3 bsdfEval1(const GMat &M, f3 wi, f3 wo) {
     }
 }
 
+template <int MODEL = -1>
 PGD float bsdfPdf1(const GMat &M, f3 wi, f3 wo) {
-    switch (M.model) {
+    switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
         case PG_BSDF_DIFFUSE:
             if (wi.z <= 0 || wo.z <= 0) return 0.0f;
             return cosineHemispherePdf(wo);
@@ -458,8 +460,9 @@ PGD float bsdfPdf1(const GMat &M, f3 wi, f3 wo) {
 }
 
 // BSDF::sample(bRec, pdf, sample) -> weight = f*cos/pdf; u2 = component sample (roughdielectric)
+template <int MODEL = -1>
 PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
-    switch (M.model) {
+    switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
         case PG_BSDF_DIFFUSE: {  // diffuse.cpp:139-153
             if (wi.z <= 0) return mk1(0.f);
             bs.wo = squareToCosineHemisphere(u0, u1);
@@ -577,20 +580,23 @@ PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
 }
 
 // twosided adapter (twosided.cpp:116-190)
+template <int MODEL = -1>
 PGD f3 bsdfEval(const GMat &M, f3 wi, f3 wo) {
     if ((M.flags & PG_MAT_TWOSIDED) && !(wi.z > 0)) {
         wi.z = -wi.z;
         wo.z = -wo.z;
     }
-    return bsdfEval1(M, wi, wo);
+    return bsdfEval1<MODEL>(M, wi, wo);
 }
+template <int MODEL = -1>
 PGD float bsdfPdf(const GMat &M, f3 wi, f3 wo) {
     if ((M.flags & PG_MAT_TWOSIDED) && !(wi.z > 0)) {
         wi.z = -wi.z;
         wo.z = -wo.z;
     }
-    return bsdfPdf1(M, wi, wo);
+    return bsdfPdf1<MODEL>(M, wi, wo);
 }
+template <int MODEL = -1>
 PGD f3 bsdfSample(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
     bool flipped = false;
     if ((M.flags & PG_MAT_TWOSIDED) && wi.z < 0) {
@@ -600,7 +606,7 @@ PGD f3 bsdfSample(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
     bs.pdf = 0;
     bs.type = 0;
     bs.eta = 1;
-    f3 r = bsdfSample1(M, wi, u0, u1, u2, bs);
+    f3 r = bsdfSample1<MODEL>(M, wi, u0, u1, u2, bs);
     if (flipped && !isZero(r) && bs.pdf != 0) bs.wo.z = -bs.wo.z;
     return r;
 }

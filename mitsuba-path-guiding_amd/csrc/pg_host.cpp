@@ -23,10 +23,24 @@ namespace {
 
 constexpr uint32_t kStackDepth = 48;  // must match STACK_DEPTH in pg_kernels.hip
 constexpr uint32_t kMaxBounces = 1100;     // > gpu_depth_cap default (1024) + 2
-constexpr uint32_t kShadowOffset = 1104;   // shadow[b] lives at counters[kShadowOffset + b]
-constexpr uint32_t kFetchOffset = 2 * 1104;  // per bounce: 8 trace + 8 shadow fetch shards
-constexpr uint32_t kCounterWords = kFetchOffset + 16 * 1104;
-constexpr uint32_t kFirstPoll = 12, kPollEvery = 6;
+// per-bounce device counters (words): [0, 64) shard counts of the live queue entering the bounce,
+// [64, 128) shadow-queue shard counts, [128, 512) shard counts of the PG_NUM_CLASSES material-class
+// queues followed by the escaped-path counts
+constexpr uint32_t kBounceWords = 512;
+constexpr uint32_t kShadowCounts = PG_QSHARDS, kClassCounts = 2 * PG_QSHARDS;
+static_assert(kClassCounts + (PG_NUM_CLASSES + 1) * PG_QSHARDS <= kBounceWords, "counter layout");
+constexpr uint32_t kCounterWords = kBounceWords * (kMaxBounces + 1);
+
+// shading-queue class of a BSDF model (one specialised k_shade per class)
+int materialClass(uint32_t model) {
+    switch (model) {
+        case PG_BSDF_DIFFUSE: return PG_CLASS_DIFFUSE;
+        case PG_BSDF_ROUGHCONDUCTOR: return PG_CLASS_ROUGHCONDUCTOR;
+        case PG_BSDF_ROUGHDIELECTRIC: return PG_CLASS_ROUGHDIELECTRIC;
+        case PG_BSDF_PLASTIC: return PG_CLASS_PLASTIC;
+        default: return PG_CLASS_DELTA;
+    }
+}
 
 struct DevBuf {
     void *p = nullptr;
@@ -61,7 +75,7 @@ struct Ctx {
     // scene
     bool has_scene = false;
     GParams g{};
-    DevBuf nodes, woop, tshade, mats, ems, emtri, emcdf;
+    DevBuf nodes, woop, tshade, tclass, mats, ems, emtri, emcdf;
     uint32_t num_tris = 0, num_mats = 0;
     std::vector<GMat> host_mats;
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
@@ -72,6 +86,7 @@ struct Ctx {
     uint32_t P = 0;
     int vtx_slots = 0;
     DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, counters, stack_ovf;
+    DevBuf class_q;            // PG_NUM_CLASSES queues of P entries
     uint32_t *h_counter = nullptr;  // pinned
     // film
     DevBuf film, film_sq;
@@ -207,7 +222,8 @@ pg_status upload(Ctx *c, DevBuf &b, const std::vector<T> &v) {
 }
 
 SceneDev sceneView(const Ctx *c) {
-    return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->tshade.as<float4>(), c->mats.as<GMat>(),
+    return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->tshade.as<float4>(), c->tclass.as<uint8_t>(),
+                    c->mats.as<GMat>(),
                     c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>()};
 }
 SDDev sdView(const Ctx *c) {
@@ -290,10 +306,12 @@ pg_status ensurePaths(Ctx *c, uint32_t want) {
     HIPC(c, c->sh_o.alloc(f4));
     HIPC(c, c->sh_d.alloc(f4));
     HIPC(c, c->sh_c.alloc(f4));
-    HIPC(c, c->q0.alloc((size_t)P * 4));
-    HIPC(c, c->q1.alloc((size_t)P * 4));
-    HIPC(c, c->qs.alloc((size_t)P * 4));
+    const size_t qbytes = (size_t)PG_QSHARDS * pg_queue_stride(P) * 4;
+    HIPC(c, c->q0.alloc(qbytes));
+    HIPC(c, c->q1.alloc(qbytes));
+    HIPC(c, c->qs.alloc(qbytes));
     HIPC(c, c->stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
+    HIPC(c, c->class_q.alloc((size_t)PG_NUM_CLASSES * qbytes));
     if (vslots > 0) HIPC(c, c->vtx.alloc((size_t)vslots * P * 48));
     c->P = P;
     c->vtx_slots = vslots;
@@ -428,9 +446,11 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     if (!pgh::buildBvh(d->positions, d->indices, nt, kStackDepth, bvh))
         return fail(c, PG_ERR_INVALID, "pg_upload_scene: BVH deeper than the traversal stack");
     std::vector<float> shade((size_t)20 * nt);
+    std::vector<uint8_t> tclass(nt);
     for (uint32_t k = 0; k < nt; ++k) {
         uint32_t t = bvh.order[k];
         packShade(&shade[20 * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
+        tclass[k] = (uint8_t)materialClass(d->materials[triBits[t] & 0xFFFFu].type);
     }
     // emitters: compact triangle array + area CDF (double accumulation of fp32 areas)
     std::vector<GEmitter> ems;
@@ -471,6 +491,7 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
 
     pg_status s;
     if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) || (s = upload(c, c->tshade, shade)) ||
+        (s = upload(c, c->tclass, tclass)) ||
         (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||
         (s = upload(c, c->emcdf, emcdf)))
         return s;
@@ -571,11 +592,10 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const SceneDev sc = sceneView(c);
     const SDDev sd = sdView(c);
     const PathDev pv = pathView(c);
-    // per-bounce device counters: live[b] (queue length entering bounce b) and shadow[b]; the
-    // kernels read them on the device, so the host only synchronizes every few bounces
-    uint32_t *live = c->counters.as<uint32_t>();
-    uint32_t *shcnt = live + kShadowOffset;
+    uint32_t *counters = c->counters.as<uint32_t>();
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
+    const uint32_t qstride = pg_queue_stride(c->P);
+    auto queue = [&](uint32_t *items, uint32_t *counts) { return Queue{items, counts, qstride}; };
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     uint32_t layersPer = std::max<uint32_t>(1, c->P / npix);
     uint32_t pixPer = std::min(npix, c->P);
@@ -587,41 +607,72 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             uint32_t n = np * nl;
             if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
             uint32_t *qbuf[2] = {c->q0.as<uint32_t>(), c->q1.as<uint32_t>()};
-            HIPC(c, hipMemsetAsync(live, 0, kCounterWords * 4, c->stream));
-            c->h_counter[0] = n;
-            HIPC(c, hipMemcpyAsync(live, c->h_counter, 4, hipMemcpyHostToDevice, c->stream));
-            pg_launch_camera(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + l0, qbuf[0]);
+            HIPC(c, hipMemsetAsync(counters, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, c->stream));
+            pg_launch_camera(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + l0,
+                             queue(qbuf[0], counters));
             uint32_t b = 0;
+            uint32_t bound = pg_camera_shard_count(n, 0);  // largest shard entering bounce b
             for (;;) {
+                uint32_t *cb = counters + (size_t)kBounceWords * b;
+                const Queue live = queue(qbuf[b & 1], cb);
                 EventPair et = nextEvents(c), es = nextEvents(c), ew = nextEvents(c);
+                // closest hit + partition of the live queue by the hit's material class; the class
+                // counts are read back: this one host round trip per bounce sizes every following
+                // launch exactly (device-sized grids of mostly empty blocks cost more than the sync)
+                Queue cls[PG_NUM_CLASSES + 1];
+                for (int k = 0; k <= PG_NUM_CLASSES; ++k)
+                    cls[k] = queue(k < PG_NUM_CLASSES ? c->class_q.as<uint32_t>() + (size_t)k * PG_QSHARDS * qstride
+                                                      : nullptr,
+                                   cb + kClassCounts + k * PG_QSHARDS);
                 HIPC(c, hipEventRecord(et.a, c->stream));
-                pg_launch_trace(c->stream, sc, pv, qbuf[b & 1], live + b, n, live + kFetchOffset + 16 * b);
+                pg_launch_trace(c->stream, sc, pv, live, bound, cls);
                 HIPC(c, hipEventRecord(et.b, c->stream));
+                uint32_t *hc = c->h_counter + 8 + (size_t)kBounceWords * b + kClassCounts;
+                HIPC(c, hipMemcpyAsync(hc, cb + kClassCounts, (PG_NUM_CLASSES + 1) * PG_QSHARDS * 4,
+                                       hipMemcpyDeviceToHost, c->stream));
+                HIPC(c, hipStreamSynchronize(c->stream));
                 HIPC(c, hipEventRecord(es.a, c->stream));
-                pg_launch_shade(c->stream, g, sc, sd, pv, qbuf[b & 1], live + b, n, qbuf[(b + 1) & 1], live + b + 1,
-                                c->qs.as<uint32_t>(), shcnt + b);
-                HIPC(c, hipEventRecord(es.b, c->stream));
-                HIPC(c, hipEventRecord(ew.a, c->stream));
-                pg_launch_shadow(c->stream, sc, pv, c->qs.as<uint32_t>(), shcnt + b, n, live + kFetchOffset + 16 * b + 8);
-                HIPC(c, hipEventRecord(ew.b, c->stream));
-                ++b;
-                // poll the live count after kFirstPoll bounces, then every kPollEvery
-                if (b >= maxBounces || (b >= kFirstPoll && (b - kFirstPoll) % kPollEvery == 0)) {
-                    HIPC(c, hipGetLastError());
-                    HIPC(c, hipMemcpyAsync(c->h_counter + 4, live + b, 4, hipMemcpyDeviceToHost, c->stream));
-                    HIPC(c, hipStreamSynchronize(c->stream));
-                    if (c->h_counter[4] == 0 || b >= maxBounces) break;
+                uint32_t clsMax[PG_NUM_CLASSES], shardLive[PG_QSHARDS] = {};
+                uint64_t nlive = 0;
+                for (int k = 0; k <= PG_NUM_CLASSES; ++k) {
+                    uint32_t m = 0;
+                    for (int sh = 0; sh < PG_QSHARDS; ++sh) {
+                        const uint32_t v = hc[k * PG_QSHARDS + sh];
+                        c->stats.segments += v;
+                        if (k == PG_NUM_CLASSES) continue;
+                        m = std::max(m, v);
+                        shardLive[sh] += v;
+                        nlive += v;
+                    }
+                    if (k < PG_NUM_CLASSES) clsMax[k] = m;
                 }
+                ++b;
+                if (nlive == 0) {
+                    HIPC(c, hipEventRecord(es.b, c->stream));
+                    HIPC(c, hipEventRecord(ew.a, c->stream));
+                    HIPC(c, hipEventRecord(ew.b, c->stream));
+                    break;
+                }
+                const Queue next = queue(qbuf[b & 1], cb + kBounceWords);
+                const Queue shq = queue(c->qs.as<uint32_t>(), cb + kShadowCounts);
+                for (int k = 0; k < PG_NUM_CLASSES; ++k)
+                    pg_launch_shade_class(c->stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
+                HIPC(c, hipEventRecord(es.b, c->stream));
+                bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
+                HIPC(c, hipEventRecord(ew.a, c->stream));
+                pg_launch_shadow(c->stream, sc, pv, shq, bound);
+                HIPC(c, hipEventRecord(ew.b, c->stream));
+                if (b >= maxBounces) break;
             }
-            // per-bounce statistics and kernel times of this chunk
-            HIPC(c, hipMemcpyAsync(c->h_counter + 8, live, kFetchOffset * 4, hipMemcpyDeviceToHost, c->stream));
+            // shadow-ray counts and kernel times of this chunk
+            HIPC(c, hipMemcpyAsync(c->h_counter + 8, counters, (size_t)kBounceWords * b * 4, hipMemcpyDeviceToHost,
+                                   c->stream));
             pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
                            c->film_sq.as<float4>());
             HIPC(c, hipStreamSynchronize(c->stream));
-            for (uint32_t k = 0; k < b; ++k) {
-                c->stats.segments += c->h_counter[8 + k];
-                c->stats.shadow_rays += c->h_counter[8 + kShadowOffset + k];
-            }
+            for (uint32_t k = 0; k < b; ++k)
+                for (int sh = 0; sh < PG_QSHARDS; ++sh)
+                    c->stats.shadow_rays += c->h_counter[8 + (size_t)kBounceWords * k + kShadowCounts + sh];
             for (size_t e = 0; e + 2 < c->evused; e += 3) {
                 float ms = 0;
                 (void)hipEventElapsedTime(&ms, c->evpool[e].a, c->evpool[e].b);

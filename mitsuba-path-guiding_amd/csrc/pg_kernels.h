@@ -9,6 +9,7 @@ struct SceneDev {
     const float4 *nodes;    // BVH2, PG_BVH_NODE_F4 float4 per node
     const float4 *woop;     // 3 float4 per BVH-order triangle
     const float4 *tshade;   // PG_TRI_SHADE_F4 float4 per BVH-order triangle
+    const uint8_t *tclass;  // PG_CLASS_* of the triangle's material, per BVH-order triangle
     const GMat *mats;
     const GEmitter *ems;
     const float4 *emtri;    // PG_TRI_SHADE_F4 float4 per emitter triangle
@@ -39,16 +40,35 @@ struct SDDev {
     int built;
 };
 
+// Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).
+// Appends are wave-aggregated atomics on the shard's own counter: one counter per queue serialized
+// every append of the chip (58k returning atomics on one address: 658 us; on 64 addresses: 18 us,
+// tools/atomic_bench.hip).  A path keeps the shard the camera gave it until it terminates, so
+// each queue's shard s is bounded by the camera queue's shard s (stride = pg_queue_stride(P)).
+#define PG_QSHARDS 64
+struct Queue {
+    uint32_t *items;
+    uint32_t *counts;  // PG_QSHARDS
+    uint32_t stride;
+};
+// camera layout: slot -> shard (slot >> 6) & 63, entry ((slot >> 12) << 6) | (slot & 63)
+__host__ __device__ inline uint32_t pg_queue_stride(uint32_t capacity) { return 64u * ((capacity + 4095u) / 4096u); }
+__host__ __device__ inline uint32_t pg_camera_shard_count(uint32_t n, uint32_t s) {
+    int rem = (int)(n & 4095u) - 64 * (int)s;
+    return 64u * (n >> 12) + (uint32_t)(rem < 0 ? 0 : rem > 64 ? 64 : rem);
+}
+
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
-                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, uint32_t *queue);
-// fetch: FETCH_SHARDS (8) zeroed work counters for this launch
-void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue,
-                     const uint32_t *count, uint32_t max_count, uint32_t *fetch);
-void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
-                     const uint32_t *queue_in, const uint32_t *count_in, uint32_t max_count, uint32_t *queue_out,
-                     uint32_t *count_out, uint32_t *shadow_queue, uint32_t *shadow_count);
-void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue,
-                      const uint32_t *count, uint32_t max_count, uint32_t *fetch);
+                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q);
+// closest hit for the live queue, partitioned by the hit's material class: class c < PG_NUM_CLASSES
+// goes to class_queues[c] (shard s -> shard s); escaped paths are only counted, in
+// class_queues[PG_NUM_CLASSES].counts.  max_shard: upper bound of the largest shard count (sizes
+// the grid; the kernels read the counts).
+void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
+                     const Queue *class_queues);
+void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
+                           const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shadow);
+void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);
 void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
                     uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq);
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,

@@ -17,7 +17,6 @@ using namespace pgd;
 #define SHADE_BLOCK 256
 // persistent grid-stride launches: enough blocks to fill 256 CUs at full occupancy
 #define TRACE_MAX_BLOCKS (256 * 16)
-#define SHADE_MAX_BLOCKS (256 * 8)
 
 namespace {
 
@@ -39,102 +38,6 @@ struct TStack {
         return i < LDS_STACK ? lds[i * TRACE_BLOCK] : ovf[(size_t)(i - LDS_STACK) * ostride];
     }
 };
-
-// Traversal state of one ray, advanced one node (inner node or whole leaf) per step so that
-// persistent kernels can interleave steps with refilling idle lanes.
-struct Trav {
-    f3 o, d, idir, ood;
-    float tmin, tmax;
-    int node, sp;
-    uint32_t tri;
-    float u, v;
-    bool found;
-};
-
-__device__ __forceinline__ void travInit(Trav &t, f3 o, f3 d, float tmin, float tmax) {
-    const float eps = 1e-30f;
-    t.o = o;
-    t.d = d;
-    t.idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)), 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-                1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
-    t.ood = o * t.idir;
-    t.tmin = tmin;
-    t.tmax = tmax;
-    t.node = 0;
-    t.sp = 0;
-    t.tri = 0xFFFFFFFFu;
-    t.u = t.v = 0.0f;
-    t.found = false;
-}
-
-// One traversal step; returns true when the ray is finished (closest hit known, or any hit found).
-template <bool ANY>
-__device__ __forceinline__ bool travStep(const float4 *__restrict__ nodes, const float4 *__restrict__ woop,
-                                         const TStack &stk, Trav &t) {
-    if (t.node >= 0) {
-        const float4 n0 = nodes[4 * t.node + 0];
-        const float4 n1 = nodes[4 * t.node + 1];
-        const float4 n2 = nodes[4 * t.node + 2];
-        const float4 n3 = nodes[4 * t.node + 3];
-        const f3 idir = t.idir, ood = t.ood;
-        float a0 = fmaf(n0.x, idir.x, -ood.x), a1 = fmaf(n0.y, idir.x, -ood.x);
-        float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
-        float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
-        float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), t.tmin));
-        float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), t.tmax));
-        float b0 = fmaf(n1.x, idir.x, -ood.x), b1 = fmaf(n1.y, idir.x, -ood.x);
-        float b2 = fmaf(n1.z, idir.y, -ood.y), b3 = fmaf(n1.w, idir.y, -ood.y);
-        float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
-        float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), t.tmin));
-        float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), t.tmax));
-        bool h0 = c0min <= c0max, h1 = c1min <= c1max;
-        int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
-        if (h0 && h1) {
-            int nearC = ch0, farC = ch1;
-            if (c1min < c0min) {
-                nearC = ch1;
-                farC = ch0;
-            }
-            if (t.sp < STACK_DEPTH) stk.put(t.sp++, (uint32_t)farC);
-            t.node = nearC;
-            return false;
-        }
-        if (h0 | h1) {
-            t.node = h0 ? ch0 : ch1;
-            return false;
-        }
-    } else {
-        uint32_t leaf = ~(uint32_t)t.node;
-        uint32_t first = leaf >> 4, cnt = leaf & 15u;
-        const f3 o = t.o, d = t.d;
-        for (uint32_t k = 0; k < cnt; ++k) {
-            uint32_t tr = first + k;
-            const float4 w0 = woop[3 * tr + 0];
-            float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
-            float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-            float tt = oz / dz;
-            if (tt >= t.tmin && tt <= t.tmax) {
-                const float4 w1 = woop[3 * tr + 1];
-                float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
-                if (a >= 0.0f && a <= 1.0f) {
-                    const float4 w2 = woop[3 * tr + 2];
-                    float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
-                    if (b >= 0.0f && a + b <= 1.0f) {
-                        t.found = true;
-                        if (ANY) return true;
-                        t.tmax = tt;
-                        t.tri = tr;
-                        t.u = b;             // weight of p1
-                        t.v = 1.0f - a - b;  // weight of p2
-                    }
-                }
-            }
-        }
-    }
-    if (t.sp == 0) return true;
-    t.node = (int)stk.get(--t.sp);
-    return false;
-}
 
 // While-while traversal with postponed leaves (Aila & Laine 2009): lanes keep descending inner
 // nodes until every lane of the wave holds a leaf, then all lanes test triangles together.  This
@@ -335,9 +238,11 @@ __device__ __forceinline__ f3 sampleEmitter(const GParams &g, const SceneDev &sc
 // camera rays: PerspectiveCamera::sampleRay (perspective.cpp:271-298) for (pixel, sample) slots
 __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint32_t *__restrict__ local_pixels,
                                                 uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
-                                                uint32_t sample_base, uint32_t *__restrict__ queue) {
+                                                uint32_t sample_base, Queue q) {
     uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    if (slot >= npix * nlayers) return;
+    const uint32_t n = npix * nlayers;
+    if (slot < PG_QSHARDS) q.counts[slot] = pg_camera_shard_count(n, slot);
+    if (slot >= n) return;
     uint32_t layer = slot / npix, lp = slot - layer * npix;
     uint32_t pix = local_pixels[pix_begin + lp];
     uint32_t sample = sample_base + layer;
@@ -359,54 +264,75 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     p.rad[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.prev[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.pinfo[slot] = make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u);
-    queue[slot] = slot;
+    q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
 }
 
-// closest hit for every queued path: hit[slot] = (t, BVH-order triangle | ~0, u, v)
-// Persistent grid-stride launches read the live count from device memory, so the host never
-// waits for a bounce to finish before launching the next one.
 __device__ __forceinline__ TStack threadStack(uint32_t *lds, uint32_t *ovf) {
     const uint32_t gtid = blockIdx.x * TRACE_BLOCK + threadIdx.x;
     return TStack{lds + threadIdx.x, ovf + gtid, gridDim.x * TRACE_BLOCK};
 }
 
-// Persistent traversal with dynamic ray fetch.  A wave keeps 64 rays in flight; when at least
-// REFILL_MIN lanes have finished, the finished lanes take new rays from a wave-local batch of 64
-// queue entries (one atomic per batch on one of 8 shard counters, selected by blockIdx % 8).
-// This keeps lanes busy while the long rays of a wave finish, which matters on 64-wide waves.
-#define REFILL_MIN 16
-#define TRAV_STEPS 8
-#define FETCH_SHARDS 8
-#define FETCH_BATCH 64
-
 // closest hit for every queued path: hit[slot] = (t, BVH-order triangle | ~0, u, v).
-// `fetch` (zeroed per launch) is reserved for dynamic ray fetch, which measured slower than a
-// plain grid-stride loop once traversal was made while-while.
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
-                                                       const uint32_t *__restrict__ count, uint32_t *__restrict__ fetch) {
+// Grid-stride over the queue shard blockIdx % PG_QSHARDS.  (A persistent variant with dynamic
+// ray fetch into finished lanes measured slower once traversal was made while-while.)
+struct ClassQueues {
+    Queue q[PG_NUM_CLASSES + 1];
+};
+
+// wave-aggregated append of `slot` to class queue `cls` (< 0: none), shard s: one atomic per class
+// present in the wave; class PG_NUM_CLASSES (escaped paths) is counted only
+__device__ __forceinline__ void classAppend(int cls, uint32_t slot, const ClassQueues &cqs, uint32_t s) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long pending = __ballot(cls >= 0);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int c = __shfl(cls, leader);
+        const unsigned long long mine = __ballot(cls == c);
+        const Queue &cq = cqs.q[c];
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(cq.counts + s, (uint32_t)__popcll(mine));
+        b = __shfl(b, leader);
+        if (cls == c && c < PG_NUM_CLASSES)
+            cq.items[(size_t)s * cq.stride + b + __popcll(mine & ((1ull << lane) - 1ull))] = slot;
+        pending &= ~mine;
+    }
+}
+
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, Queue q, ClassQueues cqs) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, p.stack_ovf);
-    const uint32_t n = *count;
-    for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
-        uint32_t slot = queue[i];
-        float4 o = p.ray_o[slot], d = p.ray_d[slot];
-        float tmax = d.w;
-        uint32_t tri = 0xFFFFFFFFu;
-        float u = 0, v = 0;
-        bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
-        p.hit[slot] = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+    const uint32_t n = q.counts[s];
+    const uint32_t *items = q.items + (size_t)s * q.stride;
+    // block-uniform loop bound, so whole waves reach the class ballots together
+    for (uint32_t base = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK; base < n; base += gridDim.x / PG_QSHARDS * TRACE_BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        int cls = -1;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = items[i];
+            float4 o = p.ray_o[slot], d = p.ray_d[slot];
+            float tmax = d.w;
+            uint32_t tri = 0xFFFFFFFFu;
+            float u = 0, v = 0;
+            bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+            p.hit[slot] = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+            cls = h ? (int)sc.tclass[tri] : PG_NUM_CLASSES;
+        }
+        classAppend(cls, slot, cqs, s);
     }
 }
 
 // any hit for queued shadow rays; unoccluded -> add the NEE contribution to L (and to the
 // training vertex's radiance snapshot, so its record excludes light arriving from elsewhere)
-__global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, const uint32_t *__restrict__ queue,
-                                                        const uint32_t *__restrict__ count, uint32_t *__restrict__ fetch) {
+__global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, Queue q) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, p.stack_ovf);
-    const uint32_t n = *count;
-    for (uint32_t i = blockIdx.x * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x * TRACE_BLOCK) {
-        uint32_t slot = queue[i];
+    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+    const uint32_t n = q.counts[s];
+    const uint32_t *items = q.items + (size_t)s * q.stride;
+    for (uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x / PG_QSHARDS * TRACE_BLOCK) {
+        uint32_t slot = items[i];
         float4 o = p.sh_o[slot], d = p.sh_d[slot];
         float tmax = d.w;
         uint32_t tri;
@@ -427,21 +353,24 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
 }
 
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
-__global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, SDDev sd, PathDev p,
-                                                       const uint32_t *__restrict__ queue_in,
-                                                       const uint32_t *__restrict__ count_in,
-                                                       uint32_t *__restrict__ queue_out, uint32_t *__restrict__ count_out,
-                                                       uint32_t *__restrict__ shadow_queue,
-                                                       uint32_t *__restrict__ shadow_count) {
-    const uint32_t n = *count_in;
-    // block-uniform loop bound, so every wave reaches the ballots of waveAppend together
-    for (uint32_t base = blockIdx.x * SHADE_BLOCK; base < n; base += gridDim.x * SHADE_BLOCK) {
+// MODEL >= 0 compiles only that BSDF model's code (material-class queues filled by k_trace);
+// CAN_GUIDE = false drops the SD-tree code for classes that are never guided (delta lobes).
+template <int MODEL, bool CAN_GUIDE>
+__global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue in,
+                                                       Queue out, Queue shq) {
+    // one item per thread (a grid-stride loop here cost ~45 VGPRs of hoisted invariants): block b
+    // takes row b / PG_QSHARDS of shard b % PG_QSHARDS; rows past the shard's count exit at once
+    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+    const uint32_t n = in.counts[s];
+    {
+    const uint32_t base = (blockIdx.x / PG_QSHARDS) * SHADE_BLOCK;
+    if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
     bool alive = false, shadow = false, dirtyL = false;
     uint32_t slot = 0;
     f3 L = mk1(0.f);
     if (i < n) {
-        slot = queue_in[i];
+        slot = in.items[(size_t)s * in.stride + i];
         do {
             uint4 pi = p.pinfo[slot];
             const uint32_t pix = pi.x, sample = pi.y;
@@ -495,7 +424,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 (g.strict_normals && dot(rd, h.geoN) * h.wi.z >= 0))
                 break;
             const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
-            const bool guide = g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
+            const bool guide = CAN_GUIDE && g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
             const SDView sv = sdv(sd);
             uint4 meta = make_uint4(0, 0, 0, 0);
             if (guide) meta = sd.meta[sdLookup(sv, h.p)];
@@ -511,9 +440,9 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, neeD, neeDist, emPdf);
                 if (!isZero(value)) {
                     f3 woL = h.sh.toLocal(neeD);
-                    f3 bsdfVal = bsdfEval(M, h.wi, woL);
+                    f3 bsdfVal = bsdfEval<MODEL>(M, h.wi, woL);
                     if (!isZero(bsdfVal) && (!g.strict_normals || dot(h.geoN, neeD) * woL.z > 0)) {
-                        float bp = bsdfPdf(M, h.wi, woL);
+                        float bp = bsdfPdf<MODEL>(M, h.wi, woL);
                         if (guide) bp = alpha * bp + (1 - alpha) * sdPdf(sv, meta, neeD);
                         float w = miWeight(emPdf, bp);
                         neeC = T * value * bsdfVal * w;
@@ -532,10 +461,10 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 rng2(key, sample, dimOf(depth, SLOT_BSDF), b0, b1);
                 float b2 = rng1(key, sample, dimOf(depth, SLOT_COMP));
                 if (!guide) {
-                    weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+                    weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
                     woPdf = bs.pdf;
                 } else if (rng1(key, sample, dimOf(depth, SLOT_GUIDE_CHOICE)) < alpha) {
-                    weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+                    weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
                     if (isZero(weight)) {
                         ok = false;
                     } else {
@@ -549,8 +478,8 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                     sdSampleCanon(sv, meta, g0, g1, cu, cv, dPdf);
                     f3 dW = canonicalToDir(cu, cv);
                     f3 woL = h.sh.toLocal(dW);
-                    f3 f = bsdfEval(M, h.wi, woL);
-                    float bp = bsdfPdf(M, h.wi, woL);
+                    f3 f = bsdfEval<MODEL>(M, h.wi, woL);
+                    float bp = bsdfPdf<MODEL>(M, h.wi, woL);
                     woPdf = alpha * bp + (1 - alpha) * dPdf;
                     if (!(woPdf > 0) || isZero(f)) {
                         ok = false;
@@ -602,8 +531,8 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
         } while (false);
         if (dirtyL) p.rad[slot] = f4(L, 0.0f);
     }
-    waveAppend(alive, slot, queue_out, count_out);
-    waveAppend(shadow, slot, shadow_queue, shadow_count);
+    waveAppend(alive, slot, out.items + (size_t)s * out.stride, out.counts + s);
+    waveAppend(shadow, slot, shq.items + (size_t)s * shq.stride, shq.counts + s);
     }
 }
 
@@ -807,30 +736,50 @@ size_t pg_stack_overflow_words(uint64_t max_threads) {
 }
 
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
-                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, uint32_t *queue) {
+                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q) {
     uint64_t n = (uint64_t)npix * nlayers;
     if (!n) return;
     hipLaunchKernelGGL(k_camera, dim3(blocks(n, 256)), dim3(256), 0, s, g, p, local_pixels, pix_begin, npix, nlayers,
-                       sample_base, queue);
+                       sample_base, q);
 }
-void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
-                     uint32_t max_count, uint32_t *fetch) {
-    if (!max_count) return;
-    hipLaunchKernelGGL(k_trace, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p,
-                       queue, count, fetch);
+// grid of a sharded launch: PG_QSHARDS x rows (rows capped for persistent grid-stride kernels)
+static inline dim3 shardGrid(uint32_t max_shard, uint32_t block, uint32_t max_rows) {
+    const uint32_t rows = blocks(max_shard, block);
+    return dim3(PG_QSHARDS * (rows < max_rows ? rows : max_rows));
 }
-void pg_launch_shade(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
-                     const uint32_t *queue_in, const uint32_t *count_in, uint32_t max_count, uint32_t *queue_out,
-                     uint32_t *count_out, uint32_t *shadow_queue, uint32_t *shadow_count) {
-    if (!max_count) return;
-    hipLaunchKernelGGL(k_shade, dim3(min(blocks(max_count, SHADE_BLOCK), (uint32_t)SHADE_MAX_BLOCKS)), dim3(SHADE_BLOCK), 0, s, g, sc, sd, p, queue_in,
-                       count_in, queue_out, count_out, shadow_queue, shadow_count);
+void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
+                     const Queue *class_queues) {
+    if (!max_shard) return;
+    ClassQueues cq;
+    for (int c = 0; c <= PG_NUM_CLASSES; ++c) cq.q[c] = class_queues[c];
+    hipLaunchKernelGGL(k_trace, shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS), dim3(TRACE_BLOCK), 0,
+                       s, sc, p, q, cq);
 }
-void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, const uint32_t *queue, const uint32_t *count,
-                      uint32_t max_count, uint32_t *fetch) {
-    if (!max_count) return;
-    hipLaunchKernelGGL(k_shadow, dim3(min(blocks(max_count, TRACE_BLOCK), (uint32_t)TRACE_MAX_BLOCKS)), dim3(TRACE_BLOCK), 0, s, sc, p,
-                       queue, count, fetch);
+void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
+                           const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shq) {
+    if (!max_shard) return;
+    dim3 grid = shardGrid(max_shard, SHADE_BLOCK, 0xFFFFFFFFu), block(SHADE_BLOCK);
+    switch (cls) {
+        case PG_CLASS_DIFFUSE:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_DIFFUSE, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_ROUGHCONDUCTOR:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHCONDUCTOR, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_ROUGHDIELECTRIC:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHDIELECTRIC, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_PLASTIC:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_PLASTIC, false>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        default:  // delta lobes: conductor, dielectric (runtime switch, never guided)
+            hipLaunchKernelGGL((k_shade<-1, false>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+    }
+}
+void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard) {
+    if (!max_shard) return;
+    hipLaunchKernelGGL(k_shadow, shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS), dim3(TRACE_BLOCK), 0,
+                       s, sc, p, q);
 }
 void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
                     uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq) {

@@ -46,6 +46,14 @@ static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 #define PG_BVH_NODE_F4 4
 #define PG_LEAF_MAX 8
 
+// Material classes of the per-bounce shading queues (k_classify -> k_shade<MODEL>)
+#define PG_CLASS_DIFFUSE 0
+#define PG_CLASS_ROUGHCONDUCTOR 1
+#define PG_CLASS_ROUGHDIELECTRIC 2
+#define PG_CLASS_PLASTIC 3
+#define PG_CLASS_DELTA 4
+#define PG_NUM_CLASSES 5
+
 // Path-state flags (pinfo.z high bits)
 #define PF_SCATTERED 0x1u
 #define PF_EMITTED_QUERY 0x2u
