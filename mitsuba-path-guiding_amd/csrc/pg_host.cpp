@@ -67,6 +67,29 @@ struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
+// One in-flight chunk of paths: its own stream, path state, queues and counters.  pg_render_pass
+// interleaves PG_LANES lanes, so while the host waits for one lane's per-bounce class counts the
+// GPU runs the other lane's kernels (and a lane's sparse late bounces overlap the other's).
+#define PG_LANES 2
+struct Lane {
+    hipStream_t stream = nullptr;
+    uint32_t P = 0;
+    int vtx_slots = 0;
+    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
+    uint32_t *h_counts = nullptr;  // pinned: per-bounce class counts of the running chunk
+    uint32_t *h_stats = nullptr;   // pinned: counters of the last finished chunk
+    std::vector<EventPair> ev[2];  // kernel-timing events: running chunk / last finished chunk
+    size_t evused[2] = {0, 0};
+    int evcur = 0;
+    hipEvent_t ready = nullptr;    // class counts of the current bounce are on the host
+    hipEvent_t done = nullptr;     // last finished chunk's statistics copy
+    bool stats_pending = false;
+    uint32_t stats_bounces = 0;
+    // running chunk
+    bool active = false;
+    uint32_t b = 0, bound = 0, n = 0, pb = 0, np = 0, nl = 0, layer0 = 0;
+};
+
 struct Ctx {
     pg_config cfg{};
     std::string err;
@@ -83,11 +106,11 @@ struct Ctx {
     std::vector<uint32_t> local_pixels;
     DevBuf d_local_pixels;
     // path state
-    uint32_t P = 0;
-    int vtx_slots = 0;
-    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, counters, stack_ovf;
-    DevBuf class_q;            // PG_NUM_CLASSES queues of P entries
-    uint32_t *h_counter = nullptr;  // pinned
+    Lane lanes[PG_LANES];
+    hipEvent_t film_order = nullptr;  // last chunk's film + record commit (keeps them in chunk order)
+    hipEvent_t pass_start = nullptr;
+    uint64_t rec_bound = 0;           // upper bound of the device-side record count
+    EventPair timing;                 // context-stream kernel timing (splat)
     // film
     DevBuf film, film_sq;
     // records
@@ -102,8 +125,6 @@ struct Ctx {
     bool sd_dirty = true;
     // stats
     pg_stats stats{};
-    std::vector<EventPair> evpool;
-    size_t evused = 0;
 };
 
 thread_local std::string g_tls_err;
@@ -242,7 +263,7 @@ SDDev sdView(const Ctx *c) {
     s.built = c->sd.built ? 1 : 0;
     return s;
 }
-PathDev pathView(const Ctx *c) {
+PathDev pathView(const Lane *c) {
     return PathDev{c->ray_o.as<float4>(), c->ray_d.as<float4>(), c->hit.as<float4>(), c->thr.as<float4>(),
                    c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(), c->sh_o.as<float4>(),
                    c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->stack_ovf.as<uint32_t>(),
@@ -278,43 +299,53 @@ pg_status downloadSd(Ctx *c) {
     return PG_OK;
 }
 
-EventPair nextEvents(Ctx *c) {
-    if (c->evused == c->evpool.size()) {
+EventPair nextEvents(Lane *l) {
+    std::vector<EventPair> &pool = l->ev[l->evcur];
+    if (l->evused[l->evcur] == pool.size()) {
         EventPair e;
         (void)hipEventCreate(&e.a);
         (void)hipEventCreate(&e.b);
-        c->evpool.push_back(e);
+        pool.push_back(e);
     }
-    return c->evpool[c->evused++];
+    return pool[l->evused[l->evcur]++];
 }
 
-// path-state capacity for a pass over `total` paths
+// path-state capacity of every lane for chunks of up to `want` paths
 pg_status ensurePaths(Ctx *c, uint32_t want) {
-    uint32_t P = want;
     int vslots = (c->cfg.guiding ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0);
-    if (P <= c->P && vslots <= c->vtx_slots) return PG_OK;
-    P = std::max(P, c->P);
-    vslots = std::max(vslots, c->vtx_slots);
-    size_t f4 = (size_t)P * 16;
-    HIPC(c, c->ray_o.alloc(f4));
-    HIPC(c, c->ray_d.alloc(f4));
-    HIPC(c, c->hit.alloc(f4));
-    HIPC(c, c->thr.alloc(f4));
-    HIPC(c, c->rad.alloc(f4));
-    HIPC(c, c->prev.alloc(f4));
-    HIPC(c, c->pinfo.alloc(f4));
-    HIPC(c, c->sh_o.alloc(f4));
-    HIPC(c, c->sh_d.alloc(f4));
-    HIPC(c, c->sh_c.alloc(f4));
-    const size_t qbytes = (size_t)PG_QSHARDS * pg_queue_stride(P) * 4;
-    HIPC(c, c->q0.alloc(qbytes));
-    HIPC(c, c->q1.alloc(qbytes));
-    HIPC(c, c->qs.alloc(qbytes));
-    HIPC(c, c->stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
-    HIPC(c, c->class_q.alloc((size_t)PG_NUM_CLASSES * qbytes));
-    if (vslots > 0) HIPC(c, c->vtx.alloc((size_t)vslots * P * 48));
-    c->P = P;
-    c->vtx_slots = vslots;
+    for (Lane &l : c->lanes) {
+        if (!l.stream) {
+            HIPC(c, hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
+            HIPC(c, hipEventCreateWithFlags(&l.ready, hipEventDisableTiming));
+            HIPC(c, hipEventCreateWithFlags(&l.done, hipEventDisableTiming));
+            HIPC(c, hipHostMalloc((void **)&l.h_counts, kCounterWords * 4, hipHostMallocDefault));
+            HIPC(c, hipHostMalloc((void **)&l.h_stats, kCounterWords * 4, hipHostMallocDefault));
+            HIPC(c, l.counters.alloc(kCounterWords * 4));
+            HIPC(c, l.stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
+        }
+        if (want <= l.P && vslots <= l.vtx_slots) continue;
+        const uint32_t P = std::max(want, l.P);
+        const int vs = std::max(vslots, l.vtx_slots);
+        size_t f4 = (size_t)P * 16;
+        HIPC(c, l.ray_o.alloc(f4));
+        HIPC(c, l.ray_d.alloc(f4));
+        HIPC(c, l.hit.alloc(f4));
+        HIPC(c, l.thr.alloc(f4));
+        HIPC(c, l.rad.alloc(f4));
+        HIPC(c, l.prev.alloc(f4));
+        HIPC(c, l.pinfo.alloc(f4));
+        HIPC(c, l.sh_o.alloc(f4));
+        HIPC(c, l.sh_d.alloc(f4));
+        HIPC(c, l.sh_c.alloc(f4));
+        const size_t qbytes = (size_t)PG_QSHARDS * pg_queue_stride(P) * 4;
+        HIPC(c, l.q0.alloc(qbytes));
+        HIPC(c, l.q1.alloc(qbytes));
+        HIPC(c, l.qs.alloc(qbytes));
+        HIPC(c, l.class_q.alloc((size_t)PG_NUM_CLASSES * qbytes));
+        if (vs > 0) HIPC(c, l.vtx.alloc((size_t)vs * P * 48));
+        l.P = P;
+        l.vtx_slots = vs;
+    }
     return PG_OK;
 }
 
@@ -388,7 +419,8 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     if (c->cfg.tile_size == 0) c->cfg.tile_size = 32;
     if (c->cfg.gpu_depth_cap <= 0) c->cfg.gpu_depth_cap = 1024;
     if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void **)&c->h_counter, (8 + kCounterWords) * 4, hipHostMallocDefault) != hipSuccess) {
+        hipEventCreateWithFlags(&c->film_order, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->pass_start, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return fail(nullptr, PG_ERR_HIP, "pg_create: stream/pinned allocation failed");
     }
@@ -401,11 +433,23 @@ pg_status pg_destroy(void *ctx) {
     if (!c) return PG_OK;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (auto &e : c->evpool) {
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
+    for (Lane &l : c->lanes) {
+        if (l.stream) (void)hipStreamSynchronize(l.stream);
+        for (auto &pool : l.ev)
+            for (auto &e : pool) {
+                (void)hipEventDestroy(e.a);
+                (void)hipEventDestroy(e.b);
+            }
+        if (l.ready) (void)hipEventDestroy(l.ready);
+        if (l.done) (void)hipEventDestroy(l.done);
+        if (l.h_counts) (void)hipHostFree(l.h_counts);
+        if (l.h_stats) (void)hipHostFree(l.h_stats);
+        if (l.stream) (void)hipStreamDestroy(l.stream);
     }
-    if (c->h_counter) (void)hipHostFree(c->h_counter);
+    if (c->timing.a) (void)hipEventDestroy(c->timing.a);
+    if (c->timing.b) (void)hipEventDestroy(c->timing.b);
+    if (c->film_order) (void)hipEventDestroy(c->film_order);
+    if (c->pass_start) (void)hipEventDestroy(c->pass_start);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PG_OK;
@@ -539,7 +583,6 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     HIPC(c, c->film_sq.alloc(fb));
     HIPC(c, hipMemsetAsync(c->film.p, 0, fb, c->stream));
     HIPC(c, hipMemsetAsync(c->film_sq.p, 0, fb, c->stream));
-    HIPC(c, c->counters.alloc(kCounterWords * 4));
     HIPC(c, c->rec_count.alloc(16));
     HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 16, c->stream));
     c->rec_host_count = 0;
@@ -573,7 +616,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const bool rec = record && c->cfg.guiding;
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
     uint64_t total = (uint64_t)npix * spp;
-    uint32_t want = (uint32_t)std::min<uint64_t>(total, cap);
+    // paths per lane: split small passes so that both lanes get work
+    uint32_t want = (uint32_t)std::min<uint64_t>((total + PG_LANES - 1) / PG_LANES, cap);
     pg_status s;
     if ((s = ensurePaths(c, want))) return s;
     GParams g = c->g;
@@ -584,120 +628,189 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     g.strict_normals = c->cfg.strict_normals;
     g.guiding = c->cfg.guiding;
     g.record = rec ? 1 : 0;
-    g.max_vertices = rec ? std::min(c->cfg.record_max_vertices, c->vtx_slots) : 0;
+    g.max_vertices = rec ? std::min(c->cfg.record_max_vertices, c->lanes[0].vtx_slots) : 0;
     g.max_component_value = c->cfg.max_component_value;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
     g.seed = c->cfg.seed;
     g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
     const SceneDev sc = sceneView(c);
     const SDDev sd = sdView(c);
-    const PathDev pv = pathView(c);
-    uint32_t *counters = c->counters.as<uint32_t>();
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
-    const uint32_t qstride = pg_queue_stride(c->P);
-    auto queue = [&](uint32_t *items, uint32_t *counts) { return Queue{items, counts, qstride}; };
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
-    uint32_t layersPer = std::max<uint32_t>(1, c->P / npix);
-    uint32_t pixPer = std::min(npix, c->P);
-    for (uint32_t l0 = 0; l0 < spp; l0 += layersPer) {
-        uint32_t nl = std::min(layersPer, spp - l0);
-        if (npix > c->P) nl = 1;
-        for (uint32_t pb = 0; pb < npix; pb += pixPer) {
-            uint32_t np = std::min(pixPer, npix - pb);
-            uint32_t n = np * nl;
-            if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
-            uint32_t *qbuf[2] = {c->q0.as<uint32_t>(), c->q1.as<uint32_t>()};
-            HIPC(c, hipMemsetAsync(counters, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, c->stream));
-            pg_launch_camera(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + l0,
-                             queue(qbuf[0], counters));
-            uint32_t b = 0;
-            uint32_t bound = pg_camera_shard_count(n, 0);  // largest shard entering bounce b
-            for (;;) {
-                uint32_t *cb = counters + (size_t)kBounceWords * b;
-                const Queue live = queue(qbuf[b & 1], cb);
-                EventPair et = nextEvents(c), es = nextEvents(c), ew = nextEvents(c);
-                // closest hit + partition of the live queue by the hit's material class; the class
-                // counts are read back: this one host round trip per bounce sizes every following
-                // launch exactly (device-sized grids of mostly empty blocks cost more than the sync)
-                Queue cls[PG_NUM_CLASSES + 1];
-                for (int k = 0; k <= PG_NUM_CLASSES; ++k)
-                    cls[k] = queue(k < PG_NUM_CLASSES ? c->class_q.as<uint32_t>() + (size_t)k * PG_QSHARDS * qstride
-                                                      : nullptr,
-                                   cb + kClassCounts + k * PG_QSHARDS);
-                HIPC(c, hipEventRecord(et.a, c->stream));
-                pg_launch_trace(c->stream, sc, pv, live, bound, cls);
-                HIPC(c, hipEventRecord(et.b, c->stream));
-                uint32_t *hc = c->h_counter + 8 + (size_t)kBounceWords * b + kClassCounts;
-                HIPC(c, hipMemcpyAsync(hc, cb + kClassCounts, (PG_NUM_CLASSES + 1) * PG_QSHARDS * 4,
-                                       hipMemcpyDeviceToHost, c->stream));
-                HIPC(c, hipStreamSynchronize(c->stream));
-                HIPC(c, hipEventRecord(es.a, c->stream));
-                uint32_t clsMax[PG_NUM_CLASSES], shardLive[PG_QSHARDS] = {};
-                uint64_t nlive = 0;
-                for (int k = 0; k <= PG_NUM_CLASSES; ++k) {
-                    uint32_t m = 0;
-                    for (int sh = 0; sh < PG_QSHARDS; ++sh) {
-                        const uint32_t v = hc[k * PG_QSHARDS + sh];
-                        c->stats.segments += v;
-                        if (k == PG_NUM_CLASSES) continue;
-                        m = std::max(m, v);
-                        shardLive[sh] += v;
-                        nlive += v;
-                    }
-                    if (k < PG_NUM_CLASSES) clsMax[k] = m;
-                }
-                ++b;
-                if (nlive == 0) {
-                    HIPC(c, hipEventRecord(es.b, c->stream));
-                    HIPC(c, hipEventRecord(ew.a, c->stream));
-                    HIPC(c, hipEventRecord(ew.b, c->stream));
-                    break;
-                }
-                const Queue next = queue(qbuf[b & 1], cb + kBounceWords);
-                const Queue shq = queue(c->qs.as<uint32_t>(), cb + kShadowCounts);
-                for (int k = 0; k < PG_NUM_CLASSES; ++k)
-                    pg_launch_shade_class(c->stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
-                HIPC(c, hipEventRecord(es.b, c->stream));
-                bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
-                HIPC(c, hipEventRecord(ew.a, c->stream));
-                pg_launch_shadow(c->stream, sc, pv, shq, bound);
-                HIPC(c, hipEventRecord(ew.b, c->stream));
-                if (b >= maxBounces) break;
-            }
-            // shadow-ray counts and kernel times of this chunk
-            HIPC(c, hipMemcpyAsync(c->h_counter + 8, counters, (size_t)kBounceWords * b * 4, hipMemcpyDeviceToHost,
-                                   c->stream));
-            pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
-                           c->film_sq.as<float4>());
-            HIPC(c, hipStreamSynchronize(c->stream));
-            for (uint32_t k = 0; k < b; ++k)
-                for (int sh = 0; sh < PG_QSHARDS; ++sh)
-                    c->stats.shadow_rays += c->h_counter[8 + (size_t)kBounceWords * k + kShadowCounts + sh];
-            for (size_t e = 0; e + 2 < c->evused; e += 3) {
-                float ms = 0;
-                (void)hipEventElapsedTime(&ms, c->evpool[e].a, c->evpool[e].b);
-                c->stats.trace_ms += ms;
-                (void)hipEventElapsedTime(&ms, c->evpool[e + 1].a, c->evpool[e + 1].b);
-                c->stats.shade_ms += ms;
-                (void)hipEventElapsedTime(&ms, c->evpool[e + 2].a, c->evpool[e + 2].b);
-                c->stats.shadow_ms += ms;
-                c->stats.trace_launches++;
-            }
-            c->evused = 0;
-            if (rec) {
-                // bound: every slot can emit at most max_vertices records
-                if ((s = ensureRecords(c, c->rec_host_count + (uint64_t)n * g.max_vertices))) return s;
-                pg_launch_commit(c->stream, pv, n, g.max_vertices, c->records.as<pg_record>(),
-                                 c->rec_count.as<unsigned long long>(), c->rec_capacity);
-                unsigned long long rc = 0;
-                HIPC(c, hipMemcpyAsync(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost, c->stream));
-                HIPC(c, hipStreamSynchronize(c->stream));
-                c->stats.records += rc - c->rec_host_count;
-                c->rec_host_count = rc;
-            }
-            HIPC(c, hipGetLastError());
-            c->stats.paths += n;
+    const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
+    const uint32_t pixPer = std::min(npix, want);
+    uint32_t nextLayer = 0, nextPix = 0;  // chunk cursor
+    // the lanes start after everything already queued on the context stream (film reset, uploads)
+    HIPC(c, hipEventRecord(c->pass_start, c->stream));
+    HIPC(c, hipEventRecord(c->film_order, c->stream));
+    c->rec_bound = c->rec_host_count;
+
+    auto lqueue = [](const Lane &l, uint32_t *items, uint32_t *counts) {
+        return Queue{items, counts, pg_queue_stride(l.P)};
+    };
+    auto classQueues = [&](const Lane &l, uint32_t *cb, Queue *cls) {
+        for (int k = 0; k <= PG_NUM_CLASSES; ++k)
+            cls[k] = lqueue(l, k < PG_NUM_CLASSES ? l.class_q.as<uint32_t>() + (size_t)k * PG_QSHARDS * pg_queue_stride(l.P)
+                                                 : nullptr,
+                            cb + kClassCounts + k * PG_QSHARDS);
+    };
+    // trace of bounce l.b (closest hit + material-class partition), then the class counts to the host
+    auto launchTrace = [&](Lane &l) -> pg_status {
+        uint32_t *cb = l.counters.as<uint32_t>() + (size_t)kBounceWords * l.b;
+        Queue cls[PG_NUM_CLASSES + 1];
+        classQueues(l, cb, cls);
+        EventPair et = nextEvents(&l);
+        HIPC(c, hipEventRecord(et.a, l.stream));
+        pg_launch_trace(l.stream, sc, pathView(&l), lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb),
+                        l.bound, cls);
+        HIPC(c, hipEventRecord(et.b, l.stream));
+        HIPC(c, hipMemcpyAsync(l.h_counts + (size_t)kBounceWords * l.b + kClassCounts, cb + kClassCounts,
+                               (PG_NUM_CLASSES + 1) * PG_QSHARDS * 4, hipMemcpyDeviceToHost, l.stream));
+        HIPC(c, hipEventRecord(l.ready, l.stream));
+        return PG_OK;
+    };
+    // fold the last finished chunk's shadow counts and kernel times into the statistics
+    auto collectStats = [&](Lane &l) -> pg_status {
+        if (!l.stats_pending) return PG_OK;
+        HIPC(c, hipEventSynchronize(l.done));
+        for (uint32_t k = 0; k < l.stats_bounces; ++k)
+            for (int sh = 0; sh < PG_QSHARDS; ++sh)
+                c->stats.shadow_rays += l.h_stats[(size_t)kBounceWords * k + kShadowCounts + sh];
+        const int prev = l.evcur ^ 1;
+        std::vector<EventPair> &pool = l.ev[prev];
+        for (size_t e = 0; e + 2 < l.evused[prev]; e += 3) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, pool[e].a, pool[e].b);
+            c->stats.trace_ms += ms;
+            (void)hipEventElapsedTime(&ms, pool[e + 1].a, pool[e + 1].b);
+            c->stats.shade_ms += ms;
+            (void)hipEventElapsedTime(&ms, pool[e + 2].a, pool[e + 2].b);
+            c->stats.shadow_ms += ms;
+            c->stats.trace_launches++;
         }
+        l.evused[prev] = 0;
+        l.stats_pending = false;
+        return PG_OK;
+    };
+    // start the next chunk on lane l (false: no chunks left)
+    auto startChunk = [&](Lane &l) -> pg_status {
+        l.active = false;
+        if (nextLayer >= spp) return PG_OK;
+        if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+        uint32_t nl = std::min(layersPer, spp - nextLayer);
+        if (npix > want) nl = 1;
+        const uint32_t pb = nextPix, np = std::min(pixPer, npix - pb);
+        l.layer0 = nextLayer;
+        l.pb = pb;
+        l.np = np;
+        l.nl = nl;
+        l.n = np * nl;
+        nextPix += np;
+        if (nextPix >= npix) {
+            nextPix = 0;
+            nextLayer += nl;
+        }
+        l.b = 0;
+        l.bound = pg_camera_shard_count(l.n, 0);
+        l.active = true;
+        HIPC(c, hipStreamWaitEvent(l.stream, c->pass_start, 0));
+        HIPC(c, hipMemsetAsync(l.counters.p, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, l.stream));
+        pg_launch_camera(l.stream, g, pathView(&l), c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl,
+                         sample_offset + l.layer0, lqueue(l, l.q0.as<uint32_t>(), l.counters.as<uint32_t>()));
+        return launchTrace(l);
+    };
+    // film + record commit (in chunk order across lanes), statistics copy; then the next chunk
+    auto finishChunk = [&](Lane &l) -> pg_status {
+        pg_status st;
+        if ((st = collectStats(l))) return st;
+        const PathDev pv = pathView(&l);
+        HIPC(c, hipMemcpyAsync(l.h_stats, l.counters.p, (size_t)kBounceWords * l.b * 4, hipMemcpyDeviceToHost, l.stream));
+        HIPC(c, hipStreamWaitEvent(l.stream, c->film_order, 0));
+        pg_launch_film(l.stream, g, pv, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
+                       c->film_sq.as<float4>());
+        if (rec) {
+            // every slot can emit at most max_vertices records; grow the buffer (lanes idle) when the
+            // bound could overflow it
+            const uint64_t add = (uint64_t)l.n * g.max_vertices;
+            if (c->rec_bound + add > c->rec_capacity) {
+                for (Lane &o : c->lanes) HIPC(c, hipStreamSynchronize(o.stream));
+                unsigned long long rc = 0;
+                HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
+                c->stats.records += rc - c->rec_host_count;
+                c->rec_host_count = c->rec_bound = rc;
+                if ((st = ensureRecords(c, rc + add))) return st;
+            }
+            c->rec_bound += add;
+            pg_launch_commit(l.stream, pv, l.n, g.max_vertices, c->records.as<pg_record>(),
+                             c->rec_count.as<unsigned long long>(), c->rec_capacity);
+        }
+        HIPC(c, hipEventRecord(c->film_order, l.stream));
+        HIPC(c, hipEventRecord(l.done, l.stream));
+        HIPC(c, hipGetLastError());
+        l.stats_pending = true;
+        l.stats_bounces = l.b;
+        l.evcur ^= 1;
+        c->stats.paths += l.n;
+        return startChunk(l);
+    };
+    // one bounce's shading + shadow rays + next trace on lane l (class counts already on the host)
+    auto advance = [&](Lane &l) -> pg_status {
+        HIPC(c, hipEventSynchronize(l.ready));
+        uint32_t *cb = l.counters.as<uint32_t>() + (size_t)kBounceWords * l.b;
+        const uint32_t *hc = l.h_counts + (size_t)kBounceWords * l.b + kClassCounts;
+        uint32_t clsMax[PG_NUM_CLASSES], shardLive[PG_QSHARDS] = {};
+        uint64_t nlive = 0;
+        for (int k = 0; k <= PG_NUM_CLASSES; ++k) {
+            uint32_t m = 0;
+            for (int sh = 0; sh < PG_QSHARDS; ++sh) {
+                const uint32_t v = hc[k * PG_QSHARDS + sh];
+                c->stats.segments += v;
+                if (k == PG_NUM_CLASSES) continue;
+                m = std::max(m, v);
+                shardLive[sh] += v;
+                nlive += v;
+            }
+            if (k < PG_NUM_CLASSES) clsMax[k] = m;
+        }
+        ++l.b;
+        if (nlive == 0 || l.b >= maxBounces) return finishChunk(l);
+        Queue cls[PG_NUM_CLASSES + 1];
+        classQueues(l, cb, cls);
+        const PathDev pv = pathView(&l);
+        const Queue next = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb + kBounceWords);
+        const Queue shq = lqueue(l, l.qs.as<uint32_t>(), cb + kShadowCounts);
+        EventPair es = nextEvents(&l), ew = nextEvents(&l);
+        HIPC(c, hipEventRecord(es.a, l.stream));
+        for (int k = 0; k < PG_NUM_CLASSES; ++k)
+            pg_launch_shade_class(l.stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
+        HIPC(c, hipEventRecord(es.b, l.stream));
+        l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
+        HIPC(c, hipEventRecord(ew.a, l.stream));
+        pg_launch_shadow(l.stream, sc, pv, shq, l.bound);
+        HIPC(c, hipEventRecord(ew.b, l.stream));
+        return launchTrace(l);
+    };
+
+    for (Lane &l : c->lanes)
+        if ((s = startChunk(l))) return s;
+    for (;;) {
+        bool any = false;
+        for (Lane &l : c->lanes) {
+            if (!l.active) continue;
+            any = true;
+            if ((s = advance(l))) return s;
+        }
+        if (!any) break;
+    }
+    for (Lane &l : c->lanes) {
+        HIPC(c, hipStreamSynchronize(l.stream));
+        if ((s = collectStats(l))) return s;
+    }
+    if (rec) {
+        unsigned long long rc = 0;
+        HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
+        c->stats.records += rc - c->rec_host_count;
+        c->rec_host_count = c->rec_bound = rc;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
@@ -735,7 +848,11 @@ pg_status pg_splat_records(void *ctx, const void *src, uint64_t count, int32_t s
         HIPC(c, hipMemcpyAsync(c->ext_records.p, src, count * sizeof(pg_record), hipMemcpyHostToDevice, c->stream));
         dsrc = c->ext_records.as<pg_record>();
     }
-    EventPair e = nextEvents(c);
+    EventPair &e = c->timing;
+    if (!e.a) {
+        HIPC(c, hipEventCreate(&e.a));
+        HIPC(c, hipEventCreate(&e.b));
+    }
     HIPC(c, hipEventRecord(e.a, c->stream));
     pg_launch_splat(c->stream, sdView(c), dsrc, count);
     HIPC(c, hipEventRecord(e.b, c->stream));
@@ -744,7 +861,6 @@ pg_status pg_splat_records(void *ctx, const void *src, uint64_t count, int32_t s
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e.a, e.b);
     c->stats.other_ms += ms;
-    c->evused = 0;
     return PG_OK;
 }
 
