@@ -70,7 +70,7 @@ struct EventPair {
 // One in-flight chunk of paths: its own stream, path state, queues and counters.  pg_render_pass
 // interleaves PG_LANES lanes, so while the host waits for one lane's per-bounce class counts the
 // GPU runs the other lane's kernels (and a lane's sparse late bounces overlap the other's).
-#define PG_LANES 2
+#define PG_LANES 3
 struct Lane {
     hipStream_t stream = nullptr;
     uint32_t P = 0;
@@ -87,6 +87,8 @@ struct Lane {
     uint32_t stats_bounces = 0;
     // running chunk
     bool active = false;
+    bool traced = false;  // every path of the chunk terminated; film waits for its turn
+    uint32_t chunk = 0;   // chunk index within the pass (films accumulate in this order)
     uint32_t b = 0, bound = 0, n = 0, pb = 0, np = 0, nl = 0, layer0 = 0;
 };
 
@@ -639,7 +641,9 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
     const uint32_t pixPer = std::min(npix, want);
-    uint32_t nextLayer = 0, nextPix = 0;  // chunk cursor
+    uint32_t nextLayer = 0, nextPix = 0, nextChunk = 0;  // chunk cursor
+    uint32_t filmNext = 0;  // chunk whose film is next: films run in chunk order, so the float sums
+                            // of a pixel do not depend on which lane finishes first
     // the lanes start after everything already queued on the context stream (film reset, uploads)
     HIPC(c, hipEventRecord(c->pass_start, c->stream));
     HIPC(c, hipEventRecord(c->film_order, c->stream));
@@ -713,6 +717,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         l.b = 0;
         l.bound = pg_camera_shard_count(l.n, 0);
         l.active = true;
+        l.traced = false;
+        l.chunk = nextChunk++;
         HIPC(c, hipStreamWaitEvent(l.stream, c->pass_start, 0));
         HIPC(c, hipMemsetAsync(l.counters.p, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, l.stream));
         pg_launch_camera(l.stream, g, pathView(&l), c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl,
@@ -773,7 +779,21 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             if (k < PG_NUM_CLASSES) clsMax[k] = m;
         }
         ++l.b;
-        if (nlive == 0 || l.b >= maxBounces) return finishChunk(l);
+        if (nlive == 0 || l.b >= maxBounces) {
+            l.traced = true;
+            // finish this lane and every waiting lane whose turn comes after it, in chunk order
+            for (bool progress = true; progress;) {
+                progress = false;
+                for (Lane &o : c->lanes)
+                    if (o.active && o.traced && o.chunk == filmNext) {
+                        ++filmNext;
+                        pg_status st = finishChunk(o);
+                        if (st) return st;
+                        progress = true;
+                    }
+            }
+            return PG_OK;
+        }
         Queue cls[PG_NUM_CLASSES + 1];
         classQueues(l, cb, cls);
         const PathDev pv = pathView(&l);
@@ -793,14 +813,24 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
 
     for (Lane &l : c->lanes)
         if ((s = startChunk(l))) return s;
-    for (;;) {
-        bool any = false;
-        for (Lane &l : c->lanes) {
+    // advance whichever lane has its counts first (waiting on a fixed lane order leaves the GPU idle
+    // whenever the other lane is already ready)
+    for (uint32_t rr = 0;; ++rr) {
+        int active = 0, picked = -1;
+        for (int k = 0; k < PG_LANES; ++k) {
+            Lane &l = c->lanes[(rr + k) % PG_LANES];
             if (!l.active) continue;
-            any = true;
-            if ((s = advance(l))) return s;
+            ++active;
+            if (l.traced) continue;  // waiting for an earlier chunk's film
+            const hipError_t q = hipEventQuery(l.ready);
+            if (q == hipSuccess) {
+                picked = (int)((rr + k) % PG_LANES);
+                break;
+            }
+            if (q != hipErrorNotReady) HIPC(c, q);
         }
-        if (!any) break;
+        if (!active) break;
+        if (picked >= 0 && (s = advance(c->lanes[picked]))) return s;
     }
     for (Lane &l : c->lanes) {
         HIPC(c, hipStreamSynchronize(l.stream));
