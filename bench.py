@@ -8,7 +8,8 @@ resident in HBM before timing starts.  With N ranks the image tiles are sharded 
 "strong" scaling); value = all paths of the job / max-over-ranks wall time.
 
 Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md §8d /
-DESIGN.md §"Measurement", over its HIP-event-measured average duration), and on rank 0 at N=1 the
+DESIGN.md §"Measurement", over its HIP-event-measured average duration on a one-lane context, since
+the timed job overlaps three lanes), the timed-region pipeline figure, and on rank 0 at N=1 the
 CPU oracle timed on a bounded sample of the same job (kind "port"), plus the equal-spp relative RMSE
 between GPU and CPU on that sample.
 
@@ -99,29 +100,14 @@ def main():
     total_paths = paths_per_job * a.steps
     value = total_paths / elapsed / 1e6
 
-    # ---- roofline of the dominant kernel (this rank's HIP-event timings over the timed region)
+    # ---- timed-region pipeline figure: algorithmic bytes of trace + shade + shadow per wall second
     d = {k: s1[k] - s0[k] for k in s1}
-    kernels = {
-        "pg_trace_closest": (d["trace_ms"], d["segments"] * BYTES_TRACE_PER_RAY, d["trace_launches"]),
-        "pg_shade": (d["shade_ms"], d["segments"] * BYTES_SHADE_PER_VERTEX, d["trace_launches"]),
-        "pg_trace_shadow": (d["shadow_ms"], d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["trace_launches"]),
-    }
-    dom = max(kernels, key=lambda k: kernels[k][0])
-    ms, nbytes, launches = kernels[dom]
-    achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc):
-        try:
-            pj = json.load(open(pmc))
-            if dom in pj.get("kernels", {}):
-                traffic = pj["kernels"][dom].get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": dom,
-                "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
-                "avg_launch_ms": round(ms / max(launches, 1), 4)}
+    pipe_bytes = d["segments"] * (BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX) + d["shadow_rays"] * BYTES_SHADOW_PER_RAY
+    pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
+                "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
+                "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
+                "note": "all path kernels over the timed wall clock (3 path lanes run concurrently)"}
+    roofline = kernel_roofline(pg, scene, integ, local, a)
 
     # ---- CPU baseline (oracle, rank 0, N = 1, bounded sample) + equal-spp RMSE on the sample
     cpu = None
@@ -141,15 +127,60 @@ def main():
                        "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
                        "parallelism": f"tile-shard x{world}, RCCL all-gather of records"},
             "roofline": roofline,
+            "pipeline": pipeline,
             "cpu_baseline": cpu,
             "rmse_vs_cpu": rmse,
             "segments_per_path": round(d["segments"] / max(d["paths"], 1), 3),
-            "kernel_ms_per_step": {k: round(v[0] / a.steps, 2) for k, v in kernels.items()},
+            "kernel_event_ms_per_step": {k: round(d[k] / a.steps, 2) for k in ("trace_ms", "shade_ms", "shadow_ms")},
         }
         print(json.dumps(line), flush=True)
     integ.postprocess()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def kernel_roofline(pg, scene, integ, local, a, spp=32):
+    """Roofline of the dominant kernel.  The timed job runs three path lanes concurrently, so a HIP
+    event pair around one launch also covers the other lanes' kernels; per-kernel durations are
+    therefore measured on a one-lane context (same scene, same trained SD-tree, guided final-render
+    passes, launches serialized on one stream) right after the timed region."""
+    from mitsuba_path_guiding_amd.integrator import Device
+    cfg = pg.capi.default_config(guiding=1, device=local, path_lanes=1, rank=integ.dev.cfg.rank,
+                                 world_size=integ.dev.cfg.world_size)
+    dev = Device(cfg)
+    dev.upload(scene)
+    dev.put_sdtree(integ.dev.get_sdtree())
+    off = 2 ** a.train - 1
+    dev.render_pass(2, off)  # warm-up
+    s0 = dev.stats()
+    dev.render_pass(spp, off + 2)
+    s1 = dev.stats()
+    d = {k: s1[k] - s0[k] for k in s1}
+    kernels = {  # name: (total ms, algorithmic bytes, launches)
+        "k_trace": (d["trace_ms"], d["segments"] * BYTES_TRACE_PER_RAY, d["trace_launches"]),
+        "k_shade": (d["shade_ms"], d["segments"] * BYTES_SHADE_PER_VERTEX, d["shade_launches"]),
+        "k_shadow": (d["shadow_ms"], d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["trace_launches"]),
+    }
+    dev.close()
+    dom = max(kernels, key=lambda k: kernels[k][0])
+    ms, nbytes, launches = kernels[dom]
+    achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc):
+        try:
+            pj = json.load(open(pmc))
+            traffic = pj.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": dom,
+            "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
+            "avg_launch_ms": round(ms / max(launches, 1), 4),
+            "measured": f"1-lane context, guided {scene.width}x{scene.height} x {spp} spp with the trained tree",
+            "kernels": {k: {"ms": round(v[0], 2), "launches": int(v[2]),
+                            "achieved_gbs": round(v[1] / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else 0.0}
+                        for k, v in kernels.items()}}
 
 
 def cpu_baseline(pg, scene, integ, a):
@@ -172,12 +203,15 @@ def cpu_baseline(pg, scene, integ, a):
             tiles.append([(y * W + x) for y in range(ty, min(ty + T, scene.height)) for x in range(tx, min(tx + T, W))])
     spp = 64
     off = 2 ** a.train - 1
-    # calibrate on one tile from the image centre, then size the sample to ~cpu_seconds
+    # warm up on one tile, calibrate on 16 tiles from the image centre, then size the sample to
+    # ~cpu_seconds of work
     mid = len(tiles) // 2
+    O.render(osc, cfg, 4, off, sdtree=tree, pixels=np.array(tiles[mid], np.uint32), nthreads=cores)
+    cal = np.array([p for i in range(16) for p in tiles[(mid + i) % len(tiles)]], np.uint32)
     t = time.perf_counter()
-    O.render(osc, cfg, spp, off, sdtree=tree, pixels=np.array(tiles[mid], np.uint32), nthreads=cores)
-    per_tile = time.perf_counter() - t
-    ntiles = int(max(1, min(len(tiles), a.cpu_seconds / max(per_tile, 1e-3))))
+    O.render(osc, cfg, spp, off, sdtree=tree, pixels=cal, nthreads=cores)
+    per_tile = (time.perf_counter() - t) / 16
+    ntiles = int(max(1, min(len(tiles), a.cpu_seconds / max(per_tile, 1e-4))))
     sel = [tiles[(mid + i) % len(tiles)] for i in range(ntiles)]
     pix = np.array([p for tl in sel for p in tl], np.uint32)
     t = time.perf_counter()
@@ -195,8 +229,11 @@ def cpu_baseline(pg, scene, integ, a):
     gm = g[:, :3] / np.maximum(g[:, 3:4], 1)
     cm = c[:, :3] / np.maximum(c[:, 3:4], 1)
     rmse = float(np.sqrt(np.mean((gm - cm) ** 2)) / max(float(np.sqrt(np.mean(cm ** 2))), 1e-12))
-    return cpu, {"relative_rmse": round(rmse, 6), "spp": spp, "pixels": int(len(pix)),
-                 "note": "same RNG streams on both sides; differences come from fp32 libm/FMA divergence"}
+    rel = np.abs(gm - cm).max(-1) / np.maximum(cm.max(-1), 1e-3)
+    return cpu, {"relative_rmse": round(rmse, 6), "pixels_diverged_frac": round(float((rel > 1e-3).mean()), 6),
+                 "spp": spp, "pixels": int(len(pix)),
+                 "note": "same RNG streams on both sides; a path whose fp32 libm/FMA rounding flips one "
+                         "branch diverges, so the RMSE is dominated by the few diverged firefly pixels"}
 
 
 if __name__ == "__main__":

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 1
+#define PG_ABI_VERSION 2
 
 typedef int32_t pg_status;
 enum {
@@ -152,7 +152,7 @@ typedef struct pg_config {
     uint32_t tile_size;           /* 32 (Scene::setBlockSize default) */
     uint32_t max_paths_in_flight; /* 0 = auto */
     int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024) */
-    int32_t pad0;
+    int32_t path_lanes;           /* path chunks in flight on separate streams, 1..4 (0 = auto: 3) */
 } pg_config;
 
 /* Training record written per non-delta path vertex (SoA-free 32-byte AoS). */
@@ -170,13 +170,14 @@ typedef struct pg_stats {
     uint64_t segments;        /* path segments (extension rays) */
     uint64_t shadow_rays;
     uint64_t records;         /* training records written */
-    double trace_ms;          /* device time of the closest-hit kernel */
-    double shade_ms;
+    double trace_ms;          /* device time of the closest-hit kernel (HIP events; lanes overlap) */
+    double shade_ms;          /* device time of the shading kernels (all material classes) */
     double shadow_ms;
     double other_ms;
-    uint64_t trace_launches;
+    uint64_t trace_launches;  /* bounces launched (one trace + one shadow launch each) */
     uint64_t stree_nodes;
     uint64_t dtree_nodes;
+    uint64_t shade_launches;  /* material-class shading launches */
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

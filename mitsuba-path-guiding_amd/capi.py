@@ -62,7 +62,7 @@ class pg_config(C.Structure):
                 ("s_tree_threshold", C.c_float), ("d_tree_threshold", C.c_float), ("d_tree_max_depth", C.c_int32),
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
-                ("pad0", C.c_int32)]
+                ("path_lanes", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -73,7 +73,8 @@ class pg_record(C.Structure):
 class pg_stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("records", C.c_uint64),
                 ("trace_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double), ("other_ms", C.c_double),
-                ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64)]
+                ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
+                ("shade_launches", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -98,6 +99,7 @@ def default_config(**overrides):
     c.tile_size = 32
     c.max_paths_in_flight = 0
     c.gpu_depth_cap = 1024
+    c.path_lanes = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")

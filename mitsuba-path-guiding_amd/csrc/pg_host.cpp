@@ -68,9 +68,10 @@ struct EventPair {
 };
 
 // One in-flight chunk of paths: its own stream, path state, queues and counters.  pg_render_pass
-// interleaves PG_LANES lanes, so while the host waits for one lane's per-bounce class counts the
+// interleaves pg_config.path_lanes lanes, so while the host waits for one lane's per-bounce class counts the
 // GPU runs the other lane's kernels (and a lane's sparse late bounces overlap the other's).
-#define PG_LANES 3
+#define PG_MAX_LANES 4
+#define PG_DEFAULT_LANES 3
 struct Lane {
     hipStream_t stream = nullptr;
     uint32_t P = 0;
@@ -108,7 +109,8 @@ struct Ctx {
     std::vector<uint32_t> local_pixels;
     DevBuf d_local_pixels;
     // path state
-    Lane lanes[PG_LANES];
+    Lane lanes[PG_MAX_LANES];
+    int nlanes = PG_DEFAULT_LANES;
     hipEvent_t film_order = nullptr;  // last chunk's film + record commit (keeps them in chunk order)
     hipEvent_t pass_start = nullptr;
     uint64_t rec_bound = 0;           // upper bound of the device-side record count
@@ -315,7 +317,8 @@ EventPair nextEvents(Lane *l) {
 // path-state capacity of every lane for chunks of up to `want` paths
 pg_status ensurePaths(Ctx *c, uint32_t want) {
     int vslots = (c->cfg.guiding ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0);
-    for (Lane &l : c->lanes) {
+    for (int li = 0; li < c->nlanes; ++li) {
+        Lane &l = c->lanes[li];
         if (!l.stream) {
             HIPC(c, hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
             HIPC(c, hipEventCreateWithFlags(&l.ready, hipEventDisableTiming));
@@ -394,6 +397,7 @@ pg_status pg_config_default(pg_config *c) {
     c->tile_size = 32;
     c->max_paths_in_flight = 0;
     c->gpu_depth_cap = 1024;
+    c->path_lanes = 0;
     return PG_OK;
 }
 
@@ -420,6 +424,11 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     c->cfg = *cfg;
     if (c->cfg.tile_size == 0) c->cfg.tile_size = 32;
     if (c->cfg.gpu_depth_cap <= 0) c->cfg.gpu_depth_cap = 1024;
+    if (c->cfg.path_lanes < 0 || c->cfg.path_lanes > PG_MAX_LANES) {
+        delete c;
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: path_lanes must be 0..4");
+    }
+    c->nlanes = c->cfg.path_lanes ? c->cfg.path_lanes : PG_DEFAULT_LANES;
     if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->film_order, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->pass_start, hipEventDisableTiming) != hipSuccess) {
@@ -619,7 +628,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
     uint64_t total = (uint64_t)npix * spp;
     // paths per lane: split small passes so that both lanes get work
-    uint32_t want = (uint32_t)std::min<uint64_t>((total + PG_LANES - 1) / PG_LANES, cap);
+    uint32_t want = (uint32_t)std::min<uint64_t>((total + c->nlanes - 1) / c->nlanes, cap);
     pg_status s;
     if ((s = ensurePaths(c, want))) return s;
     GParams g = c->g;
@@ -739,7 +748,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             // bound could overflow it
             const uint64_t add = (uint64_t)l.n * g.max_vertices;
             if (c->rec_bound + add > c->rec_capacity) {
-                for (Lane &o : c->lanes) HIPC(c, hipStreamSynchronize(o.stream));
+                for (int li = 0; li < c->nlanes; ++li) HIPC(c, hipStreamSynchronize(c->lanes[li].stream));
                 unsigned long long rc = 0;
                 HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
                 c->stats.records += rc - c->rec_host_count;
@@ -801,8 +810,10 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         const Queue shq = lqueue(l, l.qs.as<uint32_t>(), cb + kShadowCounts);
         EventPair es = nextEvents(&l), ew = nextEvents(&l);
         HIPC(c, hipEventRecord(es.a, l.stream));
-        for (int k = 0; k < PG_NUM_CLASSES; ++k)
+        for (int k = 0; k < PG_NUM_CLASSES; ++k) {
             pg_launch_shade_class(l.stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
+            c->stats.shade_launches += clsMax[k] ? 1 : 0;
+        }
         HIPC(c, hipEventRecord(es.b, l.stream));
         l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
         HIPC(c, hipEventRecord(ew.a, l.stream));
@@ -811,20 +822,20 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         return launchTrace(l);
     };
 
-    for (Lane &l : c->lanes)
-        if ((s = startChunk(l))) return s;
+    for (int li = 0; li < c->nlanes; ++li)
+        if ((s = startChunk(c->lanes[li]))) return s;
     // advance whichever lane has its counts first (waiting on a fixed lane order leaves the GPU idle
     // whenever the other lane is already ready)
     for (uint32_t rr = 0;; ++rr) {
         int active = 0, picked = -1;
-        for (int k = 0; k < PG_LANES; ++k) {
-            Lane &l = c->lanes[(rr + k) % PG_LANES];
+        for (int k = 0; k < c->nlanes; ++k) {
+            Lane &l = c->lanes[(rr + k) % c->nlanes];
             if (!l.active) continue;
             ++active;
             if (l.traced) continue;  // waiting for an earlier chunk's film
             const hipError_t q = hipEventQuery(l.ready);
             if (q == hipSuccess) {
-                picked = (int)((rr + k) % PG_LANES);
+                picked = (int)((rr + k) % c->nlanes);
                 break;
             }
             if (q != hipErrorNotReady) HIPC(c, q);
@@ -832,7 +843,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         if (!active) break;
         if (picked >= 0 && (s = advance(c->lanes[picked]))) return s;
     }
-    for (Lane &l : c->lanes) {
+    for (int li = 0; li < c->nlanes; ++li) {
+        Lane &l = c->lanes[li];
         HIPC(c, hipStreamSynchronize(l.stream));
         if ((s = collectStats(l))) return s;
     }
