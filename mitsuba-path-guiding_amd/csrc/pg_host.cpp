@@ -60,7 +60,33 @@ struct DevBuf {
         else p = nullptr;
         return e;
     }
+    // growth with headroom, for buffers re-sized every training iteration (SD-tree): freeing and
+    // re-allocating device memory per refit stalled the next stream operation by up to ~20 ms
+    hipError_t grow(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        return alloc(std::max(n, bytes + bytes / 2));
+    }
     template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+// Pinned host staging buffer (reused): pageable-memory copies are pinned on demand by the runtime.
+struct PinnedBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    hipError_t reserve(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        n = std::max(n, (size_t)1 << 20);
+        n += n / 2;
+        hipError_t e = hipHostMalloc(&p, n, hipHostMallocDefault);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
 };
 
 struct EventPair {
@@ -126,6 +152,7 @@ struct Ctx {
     pgh::SdTree sd;
     DevBuf sd_snodes, sd_meta, sd_qsum, sd_qchild, sd_bchild, sd_bsum, sd_count, sd_jump;
     int sd_jump_bits = 0;
+    PinnedBuf sd_stage;
     bool sd_dirty = true;
     // stats
     pg_stats stats{};
@@ -277,12 +304,27 @@ PathDev pathView(const Lane *c) {
 pg_status uploadSd(Ctx *c) {
     pgh::SdTree::Flat f;
     c->sd.flatten(f);
-    pg_status s;
-    if ((s = upload(c, c->sd_snodes, f.snodes)) || (s = upload(c, c->sd_meta, f.meta)) ||
-        (s = upload(c, c->sd_qsum, f.qsum)) || (s = upload(c, c->sd_qchild, f.qchild)) ||
-        (s = upload(c, c->sd_bchild, f.bchild)) || (s = upload(c, c->sd_bsum, f.bsum)) ||
-        (s = upload(c, c->sd_count, f.count)) || (s = upload(c, c->sd_jump, f.jump)))
-        return s;
+    struct Part {
+        DevBuf *dst;
+        const void *src;
+        size_t bytes;
+    } parts[] = {{&c->sd_snodes, f.snodes.data(), f.snodes.size() * 4}, {&c->sd_meta, f.meta.data(), f.meta.size() * 4},
+                 {&c->sd_qsum, f.qsum.data(), f.qsum.size() * 4},       {&c->sd_qchild, f.qchild.data(), f.qchild.size() * 4},
+                 {&c->sd_bchild, f.bchild.data(), f.bchild.size() * 4}, {&c->sd_bsum, f.bsum.data(), f.bsum.size() * 8},
+                 {&c->sd_count, f.count.data(), f.count.size() * 4},    {&c->sd_jump, f.jump.data(), f.jump.size() * 4}};
+    size_t total = 0;
+    for (const Part &pt : parts) total += (pt.bytes + 255) & ~(size_t)255;
+    HIPC(c, c->sd_stage.reserve(total));
+    size_t off = 0;
+    for (const Part &pt : parts) {
+        HIPC(c, pt.dst->grow(std::max<size_t>(pt.bytes, 16)));
+        if (pt.bytes) {
+            uint8_t *h = (uint8_t *)c->sd_stage.p + off;
+            std::memcpy(h, pt.src, pt.bytes);
+            HIPC(c, hipMemcpyAsync(pt.dst->p, h, pt.bytes, hipMemcpyHostToDevice, c->stream));
+        }
+        off += (pt.bytes + 255) & ~(size_t)255;
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     c->stats.stree_nodes = c->sd.snode.size() / 2;
     c->stats.dtree_nodes = c->sd.samplingNodes();
@@ -294,10 +336,12 @@ pg_status uploadSd(Ctx *c) {
 // pull device-side building sums + counts into the host tree
 pg_status downloadSd(Ctx *c) {
     size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
-    std::vector<uint64_t> bsum(4 * nb);
-    std::vector<uint32_t> cnt(nl);
-    HIPC(c, hipMemcpyAsync(bsum.data(), c->sd_bsum.p, bsum.size() * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(cnt.data(), c->sd_count.p, cnt.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    const size_t sb = (32 * nb + 255) & ~(size_t)255;
+    HIPC(c, c->sd_stage.reserve(sb + 4 * nl));
+    uint64_t *bsum = (uint64_t *)c->sd_stage.p;
+    uint32_t *cnt = (uint32_t *)((uint8_t *)c->sd_stage.p + sb);
+    HIPC(c, hipMemcpyAsync(bsum, c->sd_bsum.p, 32 * nb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(cnt, c->sd_count.p, 4 * nl, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     c->sd.absorb(bsum, cnt);
     return PG_OK;

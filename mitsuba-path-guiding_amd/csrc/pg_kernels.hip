@@ -613,38 +613,65 @@ __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int 
 }
 
 // SD-tree splat: records -> building-tree leaf quadrants (2^-24 fixed point, u64 atomics)
+// Wave-aggregated atomic add: lanes with equal keys are summed in registers and one lane adds the
+// sum.  Early training iterations splat ~1M records into a handful of D-tree nodes, where plain
+// per-record atomics serialize on one address (53 ms for iteration 0).  Integer adds make the
+// result independent of the grouping, so trees stay bit-identical.  Call with the whole wave active.
+template <class T>
+__device__ __forceinline__ void waveKeyedAdd(T *base, uint32_t key, T v, bool valid) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long pending = __ballot(valid);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t k = __shfl(key, leader);
+        const bool mine = valid && key == k;
+        const unsigned long long m = __ballot(mine);
+        T sum = mine ? v : (T)0;
+        for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+        if (lane == leader) atomicAdd(base + k, sum);
+        pending &= ~m;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__restrict__ recs, unsigned long long n) {
-    unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float4 *src = reinterpret_cast<const float4 *>(recs + i);
-    float4 a = src[0], b = src[1];
-    float woPdf = b.y;
-    if (!(woPdf > 0)) return;
-    float val;
-    {
+    const unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    bool valid = i < n, found = false;
+    unsigned long long fx = 0;
+    uint32_t dt = 0, slot = 0;
+    if (valid) {
+        const float4 *src = reinterpret_cast<const float4 *>(recs + i);
+        float4 a = src[0], b = src[1];
+        float woPdf = b.y;
+        float val = 0.0f;
+        {
 #pragma clang fp contract(off)
-        val = b.x / woPdf;
-    }
-    if (!(val >= 0) || !(val < 1e30f)) return;
-    float s = val * 16777216.0f;
-    if (s >= 4.0e18f) s = 4.0e18f;
-    unsigned long long fx = (unsigned long long)s;
-    const SDView sv = sdv(sd);
-    uint32_t dt = sdLookup(sv, mk(a.x, a.y, a.z));
-    atomicAdd(sd.count + dt, 1u);
-    uint32_t dirw = __float_as_uint(a.w);
-    float u = ((float)(dirw & 0xFFFFu) + 0.5f) * (1.0f / 65536.0f);
-    float v = ((float)(dirw >> 16) + 0.5f) * (1.0f / 65536.0f);
-    uint32_t node = sd.meta[dt].y;
-    for (int guard = 0; guard < 64; ++guard) {
-        int q = childIndex(u, v);
-        uint32_t c = c4(sd.bchild[node], q);
-        if (c == 0) {
-            atomicAdd(sd.bsum + 4 * (size_t)node + q, fx);
-            break;
+            if (woPdf > 0) val = b.x / woPdf;
         }
-        node = c;
+        valid = woPdf > 0 && val >= 0 && val < 1e30f;
+        if (valid) {
+            float s = val * 16777216.0f;
+            if (s >= 4.0e18f) s = 4.0e18f;
+            fx = (unsigned long long)s;
+            const SDView sv = sdv(sd);
+            dt = sdLookup(sv, mk(a.x, a.y, a.z));
+            uint32_t dirw = __float_as_uint(a.w);
+            float u = ((float)(dirw & 0xFFFFu) + 0.5f) * (1.0f / 65536.0f);
+            float v = ((float)(dirw >> 16) + 0.5f) * (1.0f / 65536.0f);
+            uint32_t node = sd.meta[dt].y;
+            for (int guard = 0; guard < 64; ++guard) {
+                int q = childIndex(u, v);
+                uint32_t c = c4(sd.bchild[node], q);
+                if (c == 0) {
+                    slot = 4 * node + q;
+                    found = true;
+                    break;
+                }
+                node = c;
+            }
+        }
     }
+    waveKeyedAdd<uint32_t>(sd.count, dt, 1u, valid);
+    waveKeyedAdd<unsigned long long>(sd.bsum, slot, fx, found);
 }
 
 // ---- unit-level kernels used by the parity tests ---------------------------------------------

@@ -194,7 +194,7 @@ void SdTree::flatten(Flat &f) const {
     }
 }
 
-void SdTree::absorb(const std::vector<uint64_t> &bsum, const std::vector<uint32_t> &count) {
+void SdTree::absorb(const uint64_t *bsum, const uint32_t *count) {
     size_t bb = 0;
     for (size_t i = 0; i < leaves.size(); ++i) {
         SdLeaf &L = leaves[i];

@@ -52,7 +52,7 @@ struct SdTree {
     };
     void flatten(Flat &f) const;
     // absorb device-side building sums/counts (same absolute layout as flatten())
-    void absorb(const std::vector<uint64_t> &bsum, const std::vector<uint32_t> &count);
+    void absorb(const uint64_t *bsum, const uint32_t *count);
     size_t samplingNodes() const;
     size_t buildingNodes() const;
 };
