@@ -781,6 +781,112 @@ PGD void sdSampleCanon(const SDView &v, uint4 meta, float px, float py, float &c
     cv = oy + scale * py;
     pdf = 0.0f;
 }
+
+// Two D-tree walks of one lane in lockstep, so their dependent load chains overlap (the shading
+// kernel's two sequential descents were its longest latency chains).  Cursor A is a pdf query at
+// canonical (au, aw) (NEE direction); cursor B is a pdf query at (bu, bw) or, with bSample, a
+// sample draw with random numbers (bu, bw) (one-sample MIS direction).  Per cursor the arithmetic
+// is exactly that of sdPdfCanon / sdSampleCanon, so the results are bit-identical with them.
+PGD void sdDual(const SDView &v, uint4 meta, bool aOn, float au, float aw, float &aPdf, bool bOn, bool bSample,
+                float bu, float bw, float &cu, float &cv, float &bPdf) {
+    const float total0 = __uint_as_float(meta.w);
+    aPdf = kInvFourPi;
+    bPdf = kInvFourPi;
+    cu = bu;
+    cv = bw;
+    if (!(total0 > 0)) return;
+    uint32_t an = meta.x, bn = meta.x;
+    int ad = 1, bd = bSample ? 0 : 1;
+    int aq = 0, bq = 0;
+    bool aAct = aOn, bAct = bOn, aLeaf = false, bLeaf = false;
+    float ox = 0, oy = 0, scale = 1, parentEnergy = total0;
+    float bEnd = 0.0f;  // sample mode: energy the pdf telescopes to (0: guard exhausted)
+    bool bEmpty = false;
+    for (int guard = 0; guard < 64 && (aAct || bAct); ++guard) {
+        // issue every load of this level before using any of them
+        const uint4 ach = v.qchild[an];
+        const uint4 bch = v.qchild[bn];
+        const float4 s = v.qsum[bn];
+        if (aAct) {
+            aq = childIndex(au, aw);
+            const uint32_t c = c4(ach, aq);
+            if (c == 0) {
+                aAct = false;
+                aLeaf = true;
+            } else {
+                an = c;
+                ++ad;
+            }
+        }
+        if (bAct) {
+            if (!bSample) {
+                bq = childIndex(bu, bw);
+                const uint32_t c = c4(bch, bq);
+                if (c == 0) {
+                    bAct = false;
+                    bLeaf = true;
+                } else {
+                    bn = c;
+                    ++bd;
+                }
+            } else {
+                const float total = quadTotal(s);
+                if (!(total > 0)) {
+                    bAct = false;
+                    bEmpty = true;
+                    bEnd = parentEnergy;
+                } else {
+                    float partial = s.x + s.z;
+                    float boundary = partial / total;
+                    int q = 0;
+                    float qx = 0, qy = 0;
+                    if (bu < boundary) {
+                        bu = bu / boundary;
+                        boundary = s.x / partial;
+                    } else {
+                        partial = total - partial;
+                        qx = 0.5f;
+                        bu = (bu - boundary) / (1.0f - boundary);
+                        boundary = s.y / partial;
+                        q |= 1;
+                    }
+                    if (bw < boundary) {
+                        bw = bw / boundary;
+                    } else {
+                        qy = 0.5f;
+                        bw = (bw - boundary) / (1.0f - boundary);
+                        q |= 2;
+                    }
+                    bu = fminf(fmaxf(bu, 0.0f), 0.99999994f);
+                    bw = fminf(fmaxf(bw, 0.0f), 0.99999994f);
+                    ox = ox + scale * qx;
+                    oy = oy + scale * qy;
+                    scale = scale * 0.5f;
+                    ++bd;
+                    const uint32_t c = c4(bch, q);
+                    if (c == 0) {
+                        bAct = false;
+                        bEmpty = true;
+                        bEnd = q4(s, q);
+                    } else {
+                        parentEnergy = q4(s, q);
+                        bn = c;
+                    }
+                }
+            }
+        }
+    }
+    if (aOn) aPdf = aLeaf ? telescopedPdf(q4(v.qsum[an], aq), total0, ad) : 0.0f;
+    if (bOn) {
+        if (!bSample) {
+            bPdf = bLeaf ? telescopedPdf(q4(v.qsum[bn], bq), total0, bd) : 0.0f;
+        } else {
+            cu = ox + scale * bu;
+            cv = oy + scale * bw;
+            bPdf = bEmpty ? telescopedPdf(bEnd, total0, bd) : 0.0f;
+        }
+    }
+}
 #pragma clang fp contract(on)
 
 }  // namespace pgd

@@ -430,9 +430,12 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
             if (guide) meta = sd.meta[sdLookup(sv, h.p)];
             const float alpha = g.bsdf_fraction;
 
-            // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow
-            f3 neeC = mk1(0.f), neeD = mk1(0.f);
-            float neeDist = 0;
+            // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow.  With
+            // guiding, the D-tree pdf of the light direction is resolved below, in one lockstep walk
+            // with the direction-sampling descent (sdDual).
+            f3 neeC = mk1(0.f), neeD = mk1(0.f), neeV = mk1(0.f);
+            float neeDist = 0, neeEmPdf = 0, neeBp = 0;
+            bool neePending = false;
             if (g.use_nee && (M.type & ESmooth)) {
                 float s0, s1;
                 rng2(key, sample, dimOf(depth, SLOT_NEE), s0, s1);
@@ -442,11 +445,12 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                     f3 woL = h.sh.toLocal(neeD);
                     f3 bsdfVal = bsdfEval<MODEL>(M, h.wi, woL);
                     if (!isZero(bsdfVal) && (!g.strict_normals || dot(h.geoN, neeD) * woL.z > 0)) {
-                        float bp = bsdfPdf<MODEL>(M, h.wi, woL);
-                        if (guide) bp = alpha * bp + (1 - alpha) * sdPdf(sv, meta, neeD);
-                        float w = miWeight(emPdf, bp);
-                        neeC = T * value * bsdfVal * w;
+                        neeBp = bsdfPdf<MODEL>(M, h.wi, woL);
+                        neeEmPdf = emPdf;
+                        neeV = T * value * bsdfVal;
                         shadow = true;
+                        if (guide) neePending = true;
+                        else neeC = neeV * miWeight(emPdf, neeBp);
                     }
                 }
             }
@@ -460,6 +464,8 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 float b0, b1;
                 rng2(key, sample, dimOf(depth, SLOT_BSDF), b0, b1);
                 float b2 = rng1(key, sample, dimOf(depth, SLOT_COMP));
+                int mode = 0;  // D-tree walk of the sampled direction: 0 none, 1 pdf (BSDF sample), 2 sample
+                float bu = 0, bw = 0;
                 if (!guide) {
                     weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
                     woPdf = bs.pdf;
@@ -468,29 +474,38 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                     if (isZero(weight)) {
                         ok = false;
                     } else {
-                        float dPdf = sdPdf(sv, meta, h.sh.toWorld(bs.wo));
-                        woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
-                        weight = weight * (bs.pdf / woPdf);
+                        mode = 1;
+                        dirToCanonical(h.sh.toWorld(bs.wo), bu, bw);
                     }
                 } else {
-                    float g0, g1, dPdf, cu, cv;
-                    rng2(key, sample, dimOf(depth, SLOT_GUIDE), g0, g1);
-                    sdSampleCanon(sv, meta, g0, g1, cu, cv, dPdf);
-                    f3 dW = canonicalToDir(cu, cv);
-                    f3 woL = h.sh.toLocal(dW);
-                    f3 f = bsdfEval<MODEL>(M, h.wi, woL);
-                    float bp = bsdfPdf<MODEL>(M, h.wi, woL);
-                    woPdf = alpha * bp + (1 - alpha) * dPdf;
-                    if (!(woPdf > 0) || isZero(f)) {
-                        ok = false;
-                    } else {
-                        weight = f / woPdf;
-                        bs.wo = woL;
-                        bs.pdf = bp;
-                        bool refl = h.wi.z * woL.z > 0;
-                        bs.type = refl ? ((M.type & EDiffuseReflection) ? EDiffuseReflection : EGlossyReflection)
-                                       : EGlossyTransmission;
-                        bs.eta = refl ? 1.0f : (h.wi.z > 0 ? M.eta : M.invEta);
+                    mode = 2;
+                    rng2(key, sample, dimOf(depth, SLOT_GUIDE), bu, bw);
+                }
+                if (guide) {
+                    float au = 0, aw = 0, aPdf, dPdf, cu, cv;
+                    if (neePending) dirToCanonical(neeD, au, aw);
+                    sdDual(sv, meta, neePending, au, aw, aPdf, mode != 0, mode == 2, bu, bw, cu, cv, dPdf);
+                    if (neePending) neeC = neeV * miWeight(neeEmPdf, alpha * neeBp + (1 - alpha) * aPdf);
+                    if (mode == 1) {
+                        woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
+                        weight = weight * (bs.pdf / woPdf);
+                    } else if (mode == 2) {
+                        f3 dW = canonicalToDir(cu, cv);
+                        f3 woL = h.sh.toLocal(dW);
+                        f3 f = bsdfEval<MODEL>(M, h.wi, woL);
+                        float bp = bsdfPdf<MODEL>(M, h.wi, woL);
+                        woPdf = alpha * bp + (1 - alpha) * dPdf;
+                        if (!(woPdf > 0) || isZero(f)) {
+                            ok = false;
+                        } else {
+                            weight = f / woPdf;
+                            bs.wo = woL;
+                            bs.pdf = bp;
+                            bool refl = h.wi.z * woL.z > 0;
+                            bs.type = refl ? ((M.type & EDiffuseReflection) ? EDiffuseReflection : EGlossyReflection)
+                                           : EGlossyTransmission;
+                            bs.eta = refl ? 1.0f : (h.wi.z > 0 ? M.eta : M.invEta);
+                        }
                     }
                 }
             }
