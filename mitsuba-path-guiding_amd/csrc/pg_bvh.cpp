@@ -2,6 +2,7 @@
 #include "pg_bvh.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -47,28 +48,27 @@ constexpr uint32_t kLeafTarget = 4;
 
 }  // namespace
 
-bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
+// Binned-SAH binary build: nodes bn (bn[0] = root), triangle permutation ord, leaves of at most
+// maxLeaf triangles (SAH leaf/split decision, object median past depth 32).
+static void buildBinary(const float *P, const uint32_t *I, uint32_t nt, uint32_t maxLeaf, std::vector<BNode> &bn,
+                 std::vector<uint32_t> &ord, uint32_t &maxDepth, Box &all) {
     std::vector<Box> tb(nt);
     std::vector<float> cen(3 * (size_t)nt);
-    Box all;
+    all = Box();
     for (uint32_t t = 0; t < nt; ++t) {
         for (int j = 0; j < 3; ++j) tb[t].grow(P + 3 * (size_t)I[3 * (size_t)t + j]);
         for (int a = 0; a < 3; ++a) cen[3 * (size_t)t + a] = 0.5f * (tb[t].lo[a] + tb[t].hi[a]);
         all.grow(tb[t]);
     }
-    for (int a = 0; a < 3; ++a) {
-        out.lo[a] = all.lo[a];
-        out.hi[a] = all.hi[a];
-    }
-    std::vector<uint32_t> ord(nt);
+    ord.assign(nt, 0);
     for (uint32_t t = 0; t < nt; ++t) ord[t] = t;
-    std::vector<BNode> bn;
+    bn.clear();
     bn.reserve(nt ? 2 * (size_t)nt / kLeafTarget + 8 : 8);
     struct Job { int32_t node; uint32_t first, count, depth; };
     std::vector<Job> st;
     bn.emplace_back();
     st.push_back({0, 0, nt, 0});
-    uint32_t maxDepth = 0;
+    maxDepth = 0;
     while (!st.empty()) {
         Job j = st.back();
         st.pop_back();
@@ -80,7 +80,7 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         }
         bn[j.node].box = box;
         uint32_t mid = 0;
-        bool leaf = j.count <= kLeafTarget;
+        bool leaf = j.count <= std::min(kLeafTarget, maxLeaf);
         if (!leaf) {
             int bestAxis = -1, bestBin = -1;
             float bestCost = std::numeric_limits<float>::infinity();
@@ -123,7 +123,7 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
                 }
                 float leafCost = box.area() * (float)j.count;
                 float splitCost = box.area() * 1.0f + bestCost;  // traversal cost ~ 1 triangle test
-                if (bestAxis >= 0 && splitCost >= leafCost && j.count <= PG_LEAF_MAX) leaf = true;
+                if (bestAxis >= 0 && splitCost >= leafCost && j.count <= maxLeaf) leaf = true;
             }
             if (!leaf) {
                 if (bestAxis >= 0 && !median) {
@@ -136,7 +136,7 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
                     mid = (uint32_t)(it - ord.begin());
                 }
                 if (bestAxis < 0 || median || mid == j.first || mid == j.first + j.count) {
-                    if (j.count <= 15 && bestAxis < 0 && !median) {
+                    if (j.count <= maxLeaf && bestAxis < 0 && !median) {
                         leaf = true;  // coincident centroids, small enough
                     } else {
                         int ax = 0;
@@ -169,56 +169,288 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
             st.push_back({l, j.first, mid - j.first, j.depth + 1});
         }
     }
+}
+
+// Woop unit-triangle record (3 x float4) of triangle t: rows of the inverse of [e0 e1 n] in double.
+static void woopRecord(const float *P, const uint32_t *I, uint32_t t, float *w) {
+    const float *v0 = P + 3 * (size_t)I[3 * (size_t)t], *v1 = P + 3 * (size_t)I[3 * (size_t)t + 1],
+                *v2 = P + 3 * (size_t)I[3 * (size_t)t + 2];
+    double e0[3], e1[3], n[3];
+    for (int a = 0; a < 3; ++a) {
+        e0[a] = (double)v0[a] - v2[a];
+        e1[a] = (double)v1[a] - v2[a];
+    }
+    n[0] = e0[1] * e1[2] - e0[2] * e1[1];
+    n[1] = e0[2] * e1[0] - e0[0] * e1[2];
+    n[2] = e0[0] * e1[1] - e0[1] * e1[0];
+    // M = [e0 e1 n] (columns); rows of M^-1 map (p - v2) -> (a, b, c)
+    double m[3][3] = {{e0[0], e1[0], n[0]}, {e0[1], e1[1], n[1]}, {e0[2], e1[2], n[2]}};
+    double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
+                 m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
+    for (int k = 0; k < 12; ++k) w[k] = 0.0f;
+    if (!(std::fabs(det) > 0) || !std::isfinite(det)) return;  // degenerate: never hit (NaN t)
+    double inv[3][3];
+    inv[0][0] = (m[1][1] * m[2][2] - m[1][2] * m[2][1]) / det;
+    inv[0][1] = (m[0][2] * m[2][1] - m[0][1] * m[2][2]) / det;
+    inv[0][2] = (m[0][1] * m[1][2] - m[0][2] * m[1][1]) / det;
+    inv[1][0] = (m[1][2] * m[2][0] - m[1][0] * m[2][2]) / det;
+    inv[1][1] = (m[0][0] * m[2][2] - m[0][2] * m[2][0]) / det;
+    inv[1][2] = (m[0][2] * m[1][0] - m[0][0] * m[1][2]) / det;
+    inv[2][0] = (m[1][0] * m[2][1] - m[1][1] * m[2][0]) / det;
+    inv[2][1] = (m[0][1] * m[2][0] - m[0][0] * m[2][1]) / det;
+    inv[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) / det;
+    auto rowdot = [&](int r) { return inv[r][0] * v2[0] + inv[r][1] * v2[1] + inv[r][2] * v2[2]; };
+    // w0: c(p) = r2.p - r2.v2 ; stored as (r2, r2.v2) so that t = (w0.w - r2.o) / r2.d
+    w[0] = (float)inv[2][0];
+    w[1] = (float)inv[2][1];
+    w[2] = (float)inv[2][2];
+    w[3] = (float)rowdot(2);
+    w[4] = (float)inv[0][0];
+    w[5] = (float)inv[0][1];
+    w[6] = (float)inv[0][2];
+    w[7] = (float)(-rowdot(0));
+    w[8] = (float)inv[1][0];
+    w[9] = (float)inv[1][1];
+    w[10] = (float)inv[1][2];
+    w[11] = (float)(-rowdot(1));
+}
+
+namespace {
+
+// Child-slot assignment by ray octant: slot s holds the child a ray of octant s (bit a set =
+// negative direction along axis a) should visit first, i.e. the child minimising
+// dot(centroid - parent centroid, diag(s)).  Greedy over the sorted (cost, child, slot) table.
+void assignSlots(const Box &parent, const std::vector<Box> &cb, int slotOf[8]) {
+    const int k = (int)cb.size();
+    float pc[3];
+    for (int a = 0; a < 3; ++a) pc[a] = 0.5f * (parent.lo[a] + parent.hi[a]);
+    struct C { float cost; int child, slot; };
+    std::vector<C> tab;
+    for (int i = 0; i < k; ++i) {
+        float v[3];
+        for (int a = 0; a < 3; ++a) v[a] = 0.5f * (cb[i].lo[a] + cb[i].hi[a]) - pc[a];
+        for (int sl = 0; sl < 8; ++sl) {
+            float c = 0;
+            for (int a = 0; a < 3; ++a) c += ((sl >> a) & 1) ? -v[a] : v[a];
+            tab.push_back({c, i, sl});
+        }
+    }
+    std::stable_sort(tab.begin(), tab.end(), [](const C &x, const C &y) { return x.cost < y.cost; });
+    bool usedSlot[8] = {false};
+    for (int i = 0; i < k; ++i) slotOf[i] = -1;
+    for (const C &c : tab) {
+        if (slotOf[c.child] >= 0 || usedSlot[c.slot]) continue;
+        slotOf[c.child] = c.slot;
+        usedSlot[c.slot] = true;
+    }
+}
+
+// power-of-two scale exponent with 255 * 2^e >= extent
+int quantExponent(float extent) {
+    if (!(extent > 0)) return -126;
+    int e;
+    std::frexp((double)extent / 255.0, &e);  // extent/255 = m * 2^e, m in [0.5, 1)
+    return std::max(-126, std::min(127, e));
+}
+
+}  // namespace
+
+// 8-wide BVH (for any-hit queries) with its own triangle order: wnodes + wwoop
+static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
+    std::vector<BNode> bn;
+    std::vector<uint32_t> ord;
+    uint32_t maxDepth = 0;
+    Box all;
+    buildBinary(P, I, nt, PG_WIDE_LEAF_MAX, bn, ord, maxDepth, all);
+    // ---- collapse to 8-wide nodes, SAH-optimal over the binary tree (dynamic programming after
+    // Ylitie et al. 2017): dist[n][j] = cheapest way to spread subtree n over at most j slots of
+    // one wide node; a slot is a leaf (subtree of <= PG_WIDE_LEAF_MAX triangles, one contiguous
+    // range of `ord`) or an inner wide node.
+    const size_t nb = bn.size();
+    constexpr float kCostNode = 1.0f, kCostTri = 0.3f;
+    constexpr float kInf = std::numeric_limits<float>::infinity();
+    std::vector<uint32_t> rFirst(nb), rCount(nb);
+    std::vector<std::array<float, 9>> dist(nb);
+    std::vector<float> cWide(nb, kInf), cLeaf(nb, kInf);
+    std::vector<std::array<uint8_t, 9>> splitK(nb);  // best left share for dist[n][j], 0 = n as one slot
+    {
+        std::vector<int32_t> post;
+        std::vector<int32_t> s{0};
+        while (!s.empty()) {
+            int32_t n = s.back();
+            s.pop_back();
+            post.push_back(n);
+            if (!bn[n].leaf) {
+                s.push_back(bn[n].child[0]);
+                s.push_back(bn[n].child[1]);
+            }
+        }
+        for (size_t i = post.size(); i-- > 0;) {
+            const int32_t n = post[i];
+            const float A = bn[n].box.area();
+            splitK[n].fill(0);
+            if (bn[n].leaf) {
+                rFirst[n] = bn[n].first;
+                rCount[n] = bn[n].count;
+                cLeaf[n] = kCostTri * A * (float)bn[n].count;
+                for (int j = 1; j <= 8; ++j) dist[n][j] = cLeaf[n];
+                continue;
+            }
+            const int32_t L = bn[n].child[0], R = bn[n].child[1];
+            rFirst[n] = std::min(rFirst[L], rFirst[R]);
+            rCount[n] = rCount[L] + rCount[R];
+            if (rCount[n] <= PG_WIDE_LEAF_MAX) cLeaf[n] = kCostTri * A * (float)rCount[n];
+            // n opened as a wide node: its children spread over 8 slots
+            float best = kInf;
+            for (int k = 1; k < 8; ++k) best = std::min(best, dist[L][k] + dist[R][8 - k]);
+            cWide[n] = kCostNode * A + best;
+            dist[n][1] = std::min(cLeaf[n], cWide[n]);
+            for (int j = 2; j <= 8; ++j) {
+                dist[n][j] = dist[n][1];
+                for (int k = 1; k < j; ++k) {
+                    const float c = dist[L][k] + dist[R][j - k];
+                    if (c < dist[n][j]) {
+                        dist[n][j] = c;
+                        splitK[n][j] = (uint8_t)k;
+                    }
+                }
+            }
+        }
+    }
+    // slots of wide node n: children of n spread over 8 slots along the DP's choices
+    auto collect = [&](int32_t n, std::vector<int32_t> &out) {
+        std::vector<std::pair<int32_t, int>> s;
+        int bestK = 1;
+        float best = kInf;
+        for (int k = 1; k < 8; ++k) {
+            const float c = dist[bn[n].child[0]][k] + dist[bn[n].child[1]][8 - k];
+            if (c < best) {
+                best = c;
+                bestK = k;
+            }
+        }
+        s.push_back({bn[n].child[1], 8 - bestK});
+        s.push_back({bn[n].child[0], bestK});
+        while (!s.empty()) {
+            auto [m, j] = s.back();
+            s.pop_back();
+            const int k = bn[m].leaf ? 0 : splitK[m][j];
+            if (k == 0) {
+                out.push_back(m);
+            } else {
+                s.push_back({bn[m].child[1], j - k});
+                s.push_back({bn[m].child[0], k});
+            }
+        }
+    };
+    // a slot is a leaf when the subtree fits one and a leaf is not costlier than a wide node
+    auto isLeafSlot = [&](int32_t m) { return bn[m].leaf || cLeaf[m] <= cWide[m]; };
+
+    struct WTask { int32_t bnode; uint32_t wide; uint32_t depth; };
+    std::vector<WTask> work{{0, 0, 1}};
+    std::vector<float> nodes(PG_WIDE_NODE_F4 * 4, 0.0f);
+    std::vector<uint32_t> order;
+    order.reserve(nt);
+    uint32_t wideDepth = 0;
+    for (size_t w = 0; w < work.size(); ++w) {
+        const WTask task = work[w];
+        wideDepth = std::max(wideDepth, task.depth);
+        std::vector<int32_t> ch;
+        if (isLeafSlot(task.bnode)) ch.push_back(task.bnode);  // tiny scene: the root is one leaf
+        else collect(task.bnode, ch);
+        std::vector<Box> cb;
+        Box parent;
+        for (int32_t c : ch) {
+            cb.push_back(bn[c].box);
+            parent.grow(bn[c].box);
+        }
+        int slotOf[8];
+        assignSlots(parent, cb, slotOf);
+        int childAt[8];
+        for (int sl = 0; sl < 8; ++sl) childAt[sl] = -1;
+        for (size_t i = 0; i < ch.size(); ++i) childAt[slotOf[i]] = (int)i;
+        // quantisation frame of this node
+        int ex[3];
+        float scale[3];
+        for (int a = 0; a < 3; ++a) {
+            ex[a] = quantExponent(parent.hi[a] - parent.lo[a]);
+            scale[a] = std::ldexp(1.0f, ex[a]);
+        }
+        uint32_t imask = 0, childBase = (uint32_t)(nodes.size() / (PG_WIDE_NODE_F4 * 4)),
+                 triBase = (uint32_t)order.size(), nInner = 0;
+        uint8_t meta[8] = {0}, q[6][8];
+        for (int a = 0; a < 6; ++a)
+            for (int sl = 0; sl < 8; ++sl) q[a][sl] = 0;
+        for (int sl = 0; sl < 8; ++sl) {
+            const int i = childAt[sl];
+            if (i < 0) continue;
+            const int32_t cn = ch[i];
+            const BNode &c = bn[cn];
+            for (int a = 0; a < 3; ++a) {
+                // conservative: floor / ceil in double, then checked against the float reconstruction
+                double lo = std::floor(((double)c.box.lo[a] - parent.lo[a]) / scale[a]);
+                double hi = std::ceil(((double)c.box.hi[a] - parent.lo[a]) / scale[a]);
+                lo = std::max(0.0, std::min(255.0, lo));
+                hi = std::max(0.0, std::min(255.0, hi));
+                while (lo > 0 && parent.lo[a] + (float)lo * scale[a] > c.box.lo[a]) lo -= 1;
+                while (hi < 255 && parent.lo[a] + (float)hi * scale[a] < c.box.hi[a]) hi += 1;
+                q[a][sl] = (uint8_t)lo;
+                q[3 + a][sl] = (uint8_t)hi;
+            }
+            if (isLeafSlot(cn)) {
+                const uint32_t off = (uint32_t)order.size() - triBase;
+                for (uint32_t k = 0; k < rCount[cn]; ++k) order.push_back(ord[rFirst[cn] + k]);
+                meta[sl] = (uint8_t)(off | (rCount[cn] << 5));  // count 1..3 in bits 5-6 (0 = empty slot)
+            } else {
+                imask |= 1u << sl;
+                work.push_back({cn, childBase + nInner, task.depth + 1});
+                ++nInner;
+            }
+        }
+        nodes.resize(nodes.size() + (size_t)nInner * PG_WIDE_NODE_F4 * 4, 0.0f);
+        float *o = &nodes[(size_t)task.wide * PG_WIDE_NODE_F4 * 4];
+        uint32_t w0 = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16) |
+                      (imask << 24);
+        o[0] = parent.lo[0];
+        o[1] = parent.lo[1];
+        o[2] = parent.lo[2];
+        std::memcpy(&o[3], &w0, 4);
+        uint32_t w1[4] = {childBase, triBase, 0, 0};
+        std::memcpy(&w1[2], meta, 8);
+        std::memcpy(&o[4], w1, 16);
+        // [2] qlo.x qlo.y  [3] qlo.z qhi.x  [4] qhi.y qhi.z   (8 bytes each, slot order)
+        std::memcpy(&o[8], q[0], 8);
+        std::memcpy(&o[10], q[1], 8);
+        std::memcpy(&o[12], q[2], 8);
+        std::memcpy(&o[14], q[3], 8);
+        std::memcpy(&o[16], q[4], 8);
+        std::memcpy(&o[18], q[5], 8);
+    }
+    out.wnodes.swap(nodes);
+    out.wide_depth = wideDepth;
+    if (wideDepth + 1 > stack_limit || order.size() != nt) return false;
+    out.wwoop.assign(12 * (size_t)nt, 0.0f);
+    for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, order[k], &out.wwoop[12 * (size_t)k]);
+    return true;
+}
+
+// binary BVH (for closest-hit queries): nodes + woop in `order`
+static bool buildBinaryBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
+    std::vector<BNode> bn;
+    std::vector<uint32_t> ord;
+    uint32_t maxDepth = 0;
+    Box all;
+    buildBinary(P, I, nt, PG_LEAF_MAX, bn, ord, maxDepth, all);
+    for (int a = 0; a < 3; ++a) {
+        out.lo[a] = all.lo[a];
+        out.hi[a] = all.hi[a];
+    }
     out.max_depth = maxDepth;
     if (maxDepth + 1 > stack_limit) return false;
-
-    // ---- pack: inner nodes get GPU indices in DFS order; a leaf root gets a synthetic parent
     out.order = ord;
     out.woop.assign(12 * (size_t)nt, 0.0f);
-    for (uint32_t k = 0; k < nt; ++k) {
-        uint32_t t = ord[k];
-        const float *v0 = P + 3 * (size_t)I[3 * (size_t)t], *v1 = P + 3 * (size_t)I[3 * (size_t)t + 1],
-                    *v2 = P + 3 * (size_t)I[3 * (size_t)t + 2];
-        double e0[3], e1[3], n[3];
-        for (int a = 0; a < 3; ++a) {
-            e0[a] = (double)v0[a] - v2[a];
-            e1[a] = (double)v1[a] - v2[a];
-        }
-        n[0] = e0[1] * e1[2] - e0[2] * e1[1];
-        n[1] = e0[2] * e1[0] - e0[0] * e1[2];
-        n[2] = e0[0] * e1[1] - e0[1] * e1[0];
-        // M = [e0 e1 n] (columns); rows of M^-1 map (p - v2) -> (a, b, c)
-        double m[3][3] = {{e0[0], e1[0], n[0]}, {e0[1], e1[1], n[1]}, {e0[2], e1[2], n[2]}};
-        double det = m[0][0] * (m[1][1] * m[2][2] - m[1][2] * m[2][1]) - m[0][1] * (m[1][0] * m[2][2] - m[1][2] * m[2][0]) +
-                     m[0][2] * (m[1][0] * m[2][1] - m[1][1] * m[2][0]);
-        float *w = &out.woop[12 * (size_t)k];
-        if (!(std::fabs(det) > 0) || !std::isfinite(det)) continue;  // degenerate: never hit (NaN t)
-        double inv[3][3];
-        inv[0][0] = (m[1][1] * m[2][2] - m[1][2] * m[2][1]) / det;
-        inv[0][1] = (m[0][2] * m[2][1] - m[0][1] * m[2][2]) / det;
-        inv[0][2] = (m[0][1] * m[1][2] - m[0][2] * m[1][1]) / det;
-        inv[1][0] = (m[1][2] * m[2][0] - m[1][0] * m[2][2]) / det;
-        inv[1][1] = (m[0][0] * m[2][2] - m[0][2] * m[2][0]) / det;
-        inv[1][2] = (m[0][2] * m[1][0] - m[0][0] * m[1][2]) / det;
-        inv[2][0] = (m[1][0] * m[2][1] - m[1][1] * m[2][0]) / det;
-        inv[2][1] = (m[0][1] * m[2][0] - m[0][0] * m[2][1]) / det;
-        inv[2][2] = (m[0][0] * m[1][1] - m[0][1] * m[1][0]) / det;
-        auto rowdot = [&](int r) { return inv[r][0] * v2[0] + inv[r][1] * v2[1] + inv[r][2] * v2[2]; };
-        // w0: c(p) = r2.p - r2.v2 ; stored as (r2, r2.v2) so that t = (w0.w - r2.o) / r2.d
-        w[0] = (float)inv[2][0];
-        w[1] = (float)inv[2][1];
-        w[2] = (float)inv[2][2];
-        w[3] = (float)rowdot(2);
-        w[4] = (float)inv[0][0];
-        w[5] = (float)inv[0][1];
-        w[6] = (float)inv[0][2];
-        w[7] = (float)(-rowdot(0));
-        w[8] = (float)inv[1][0];
-        w[9] = (float)inv[1][1];
-        w[10] = (float)inv[1][2];
-        w[11] = (float)(-rowdot(1));
-    }
-
+    for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, ord[k], &out.woop[12 * (size_t)k]);
+    // ---- pack: inner nodes get GPU indices in DFS order; a leaf root gets a synthetic parent
     std::vector<int32_t> gpuIndex(bn.size(), -1);
     std::vector<int32_t> innerOrder;
     {
@@ -261,6 +493,25 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         putNode(&out.nodes[16 * i], bn[n.child[0]].box, ref(n.child[0]), bn[n.child[1]].box, ref(n.child[1]));
     }
     return true;
+}
+
+bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
+    if (nt == 0) {  // every ray misses: an inner root with two empty far-away leaves; a childless wide node
+        out.nodes.assign(16, 0.0f);
+        for (int k = 0; k < 4; ++k) out.nodes[k] = out.nodes[4 + k] = 1e30f;
+        out.nodes[8] = out.nodes[9] = out.nodes[10] = out.nodes[11] = 1e30f;
+        int32_t empty = ~(int32_t)0;
+        std::memcpy(&out.nodes[12], &empty, 4);
+        std::memcpy(&out.nodes[13], &empty, 4);
+        out.wnodes.assign(PG_WIDE_NODE_F4 * 4, 0.0f);
+        out.order.clear();
+        out.woop.clear();
+        out.wwoop.clear();
+        out.max_depth = out.wide_depth = 1;
+        for (int a = 0; a < 3; ++a) out.lo[a] = out.hi[a] = 0.0f;
+        return true;
+    }
+    return buildBinaryBvh(P, I, nt, stack_limit, out) && buildWide(P, I, nt, stack_limit, out);
 }
 
 }  // namespace pgh

@@ -127,7 +127,7 @@ struct Ctx {
     // scene
     bool has_scene = false;
     GParams g{};
-    DevBuf nodes, woop, tshade, tclass, mats, ems, emtri, emcdf;
+    DevBuf nodes, woop, wnodes, wwoop, tshade, tclass, mats, ems, emtri, emcdf;
     uint32_t num_tris = 0, num_mats = 0;
     std::vector<GMat> host_mats;
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
@@ -274,7 +274,8 @@ pg_status upload(Ctx *c, DevBuf &b, const std::vector<T> &v) {
 }
 
 SceneDev sceneView(const Ctx *c) {
-    return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->tshade.as<float4>(), c->tclass.as<uint8_t>(),
+    return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->wnodes.as<float4>(), c->wwoop.as<float4>(),
+                    c->tshade.as<float4>(), c->tclass.as<uint8_t>(),
                     c->mats.as<GMat>(),
                     c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>()};
 }
@@ -589,7 +590,8 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     for (uint32_t m = 0; m < d->num_materials; ++m) c->host_mats.push_back(makeGMat(d->materials[m]));
 
     pg_status s;
-    if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) || (s = upload(c, c->tshade, shade)) ||
+    if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) ||
+        (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->wwoop, bvh.wwoop)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||
         (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||
         (s = upload(c, c->emcdf, emcdf)))

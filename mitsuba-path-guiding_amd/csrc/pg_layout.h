@@ -39,12 +39,24 @@ static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 // The same layout is used for the compact emitter-triangle array.
 #define PG_TRI_SHADE_F4 5
 
-// BVH2 node (4 x float4 = 64 B):
+// Binary BVH node for closest-hit rays (4 x float4 = 64 B):
 //   [0] c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y   [1] c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y
 //   [2] c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z   [3] bits(child0), bits(child1), 0, 0
 // child >= 0: inner node index; child < 0: leaf, ~child = (first_tri << 4) | count (count <= 15).
 #define PG_BVH_NODE_F4 4
 #define PG_LEAF_MAX 8
+
+// 8-wide BVH node for shadow rays, with quantised child boxes (5 x float4 = 80 B; after Ylitie et al. 2017):
+//   [0] p.xyz (quantisation origin = node box min), bits(ex | ey << 8 | ez << 16 | imask << 24)
+//       child box coordinate = p + q * 2^(e - 127) per axis; imask bit s: slot s is an inner node
+//   [1] child_base (inner children are consecutive nodes, in slot order), tri_base (leaf triangles
+//       are consecutive BVH-order triangles, in slot order), meta[8] (bytes): leaf slot s =
+//       offset from tri_base | count << 5 (count 1..3), 0 = empty slot
+//   [2] qlo.x[8] qlo.y[8]   [3] qlo.z[8] qhi.x[8]   [4] qhi.y[8] qhi.z[8]   (uint8, slot order)
+// Slot s holds the child that rays of direction octant s (bit a = negative along axis a) should
+// visit first, so traversal orders hits by slot ^ (7 - octant) without sorting.
+#define PG_WIDE_NODE_F4 5
+#define PG_WIDE_LEAF_MAX 3
 
 // Material classes of the per-bounce shading queues (k_classify -> k_shade<MODEL>)
 #define PG_CLASS_DIFFUSE 0
