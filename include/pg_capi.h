@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 2
+#define PG_ABI_VERSION 3
 
 typedef int32_t pg_status;
 enum {
@@ -57,7 +57,8 @@ enum {
     PG_BSDF_DIELECTRIC = 3,       /* src/bsdfs/dielectric.cpp       */
     PG_BSDF_ROUGHDIELECTRIC = 4,  /* src/bsdfs/roughdielectric.cpp  */
     PG_BSDF_PLASTIC = 5,          /* src/bsdfs/plastic.cpp          */
-    PG_BSDF_COUNT = 6
+    PG_BSDF_ROUGHPLASTIC = 6,     /* src/bsdfs/roughplastic.cpp     */
+    PG_BSDF_COUNT = 7
 };
 /* Microfacet distributions (src/bsdfs/microfacet.h:48-58). */
 enum { PG_DIST_BECKMANN = 0, PG_DIST_GGX = 1 };
@@ -233,6 +234,13 @@ pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hi
  * wo_given: n x 3 local directions for the eval/pdf part (may be NULL). */
 pg_status pg_bsdf_query(void *ctx, uint32_t material, const float *wi, const float *u,
                         const float *wo_given, uint64_t n, float *out);
+
+/* Rough dielectric transmittance slice of a roughplastic material, as RoughPlastic::configure
+ * reduces it (roughplastic.cpp:283-299, src/bsdfs/rtrans.h setEta/setAlpha/evalDiffuse):
+ * table[100] = transmittance at cos(theta) = (j/99)^4 (interpolated with Catmull-Rom in
+ * cos^(1/4)), fdr_int = 1 - internal diffuse transmittance.  Computed on the host at scene upload
+ * by quadrature instead of read from data/microfacet/ *.dat.  Needs no device or context. */
+pg_status pg_rough_transmittance(uint32_t distribution, float alpha, float eta, float *table, float *fdr_int);
 
 #ifdef __cplusplus
 }

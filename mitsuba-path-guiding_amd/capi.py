@@ -11,7 +11,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "build", "libpgamd.so")
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, PG_ERR_NO_DEVICE = range(7)
-PG_BSDF_DIFFUSE, PG_BSDF_CONDUCTOR, PG_BSDF_ROUGHCONDUCTOR, PG_BSDF_DIELECTRIC, PG_BSDF_ROUGHDIELECTRIC, PG_BSDF_PLASTIC = range(6)
+(PG_BSDF_DIFFUSE, PG_BSDF_CONDUCTOR, PG_BSDF_ROUGHCONDUCTOR, PG_BSDF_DIELECTRIC, PG_BSDF_ROUGHDIELECTRIC,
+ PG_BSDF_PLASTIC, PG_BSDF_ROUGHPLASTIC) = range(7)
 PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
 PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
 
@@ -133,6 +134,7 @@ SIGNATURES = [
     ("pg_local_pixel_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
     ("pg_trace_rays", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_bsdf_query", C.c_int32, [VP, C.c_uint32, VP, VP, VP, C.c_uint64, VP]),
+    ("pg_rough_transmittance", C.c_int32, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
 ]
 
 

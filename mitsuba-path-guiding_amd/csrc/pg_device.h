@@ -367,6 +367,30 @@ PGD f3 plasticDiff(const GMat &M) {
 PGD float plasticProbSpec(const GMat &M, float Fi) {
     return (Fi * M.specWeight) / (Fi * M.specWeight + (1 - Fi) * (1 - M.specWeight));
 }
+// Rough transmittance of a roughplastic material at cos(theta) (RoughTransmittance::eval with eta
+// and alpha fixed, rtrans.h): Catmull-Rom in cos^(1/4) over the 100-entry table
+// (spline.cpp:23-60), clamped to [0, 1].  cos^(1/4) is sqrt(sqrt(.)) so that the oracle agrees
+// bit for bit (the reference uses std::pow).
+PGD float rtransEval(const float *tab, float cosTheta) {
+    if (!(cosTheta >= 0)) return 0.0f;
+    const float x = sqrtf(sqrtf(fabsf(cosTheta)));
+    if (!(x >= 0.0f && x <= 1.0f)) return 0.0f;
+    const int n = 100;
+    float t = x * (float)(n - 1);
+    const int k = max(0, min((int)t, n - 2));
+    const float f0 = tab[k], f1 = tab[k + 1];
+    const float d0 = k > 0 ? 0.5f * (tab[k + 1] - tab[k - 1]) : tab[k + 1] - tab[k];
+    const float d1 = k + 2 < n ? 0.5f * (tab[k + 2] - tab[k]) : tab[k + 1] - tab[k];
+    t = t - (float)k;
+    const float t2 = t * t, t3 = t2 * t;
+    const float r = (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+    return fminf(1.0f, fmaxf(0.0f, r));
+}
+// probability of sampling the glossy lobe (roughplastic.cpp:405-414)
+PGD float roughPlasticProbSpec(const GMat &M, float cosThetaI) {
+    const float p = 1 - rtransEval(M.rtrans, cosThetaI);
+    return (p * M.specWeight) / (p * M.specWeight + (1 - p) * (1 - M.specWeight));
+}
 
 // f * cos(theta_o), solid-angle measure (BSDF::eval with ESolidAngle)
 template <int MODEL = -1>
@@ -407,6 +431,17 @@ PGD f3 bsdfEval1(const GMat &M, f3 wi, f3 wo) {
             if (wo.z <= 0 || wi.z <= 0) return mk1(0.f);
             float Fi = fresnelDielectricExt(wi.z, M.eta), Fo = fresnelDielectricExt(wo.z, M.eta);
             return plasticDiff(M) * (cosineHemispherePdf(wo) * M.invEta2 * (1 - Fi) * (1 - Fo));
+        }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:344-397
+            if (wi.z <= 0 || wo.z <= 0) return mk1(0.f);
+            Mf d = mfOf(M);
+            const f3 H = normalize(wo + wi);
+            const float D = d.eval(H);
+            const float F = fresnelDielectricExt(dot(wi, H), M.eta);
+            const float G = d.G(wi, wo, H);
+            const float value = F * D * G / (4.0f * wi.z);
+            const float T12 = rtransEval(M.rtrans, wi.z), T21 = rtransEval(M.rtrans, wo.z);
+            return specOf(M) * value + plasticDiff(M) * (kInvPi * wo.z * T12 * T21 * M.invEta2);
         }
         default: return mk1(0.f);
     }
@@ -454,6 +489,15 @@ PGD float bsdfPdf1(const GMat &M, f3 wi, f3 wo) {
             if (wo.z <= 0 || wi.z <= 0) return 0.0f;
             float Fi = fresnelDielectricExt(wi.z, M.eta);
             return cosineHemispherePdf(wo) * (1 - plasticProbSpec(M, Fi));
+        }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:398-447
+            if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+            Mf d = mfOf(M);
+            const f3 H = normalize(wo + wi);
+            const float probSpecular = roughPlasticProbSpec(M, wi.z), probDiffuse = 1 - probSpecular;
+            const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+            const float prob = d.pdf(wi, H);
+            return prob * dwh_dwo * probSpecular + probDiffuse * cosineHemispherePdf(wo);
         }
         default: return 0.0f;
     }
@@ -574,6 +618,33 @@ PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
             float Fo = fresnelDielectricExt(bs.wo.z, M.eta);
             bs.pdf = (1 - ps) * cosineHemispherePdf(bs.wo);
             return plasticDiff(M) * (M.invEta2 * (1 - Fi) * (1 - Fo) / (1 - ps));
+        }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:449-510
+            if (wi.z <= 0) return mk1(0.f);
+            const float ps = roughPlasticProbSpec(M, wi.z);
+            float sy = u1;
+            bool spec = true;
+            if (sy < ps) {
+                sy /= ps;
+            } else {
+                sy = (sy - ps) / (1 - ps);
+                spec = false;
+            }
+            if (spec) {
+                Mf d = mfOf(M);
+                float mpdf;
+                const f3 m = d.sample(wi, u0, sy, mpdf);
+                bs.wo = reflectV(wi, m);
+                bs.type = EGlossyReflection;
+                if (bs.wo.z <= 0) return mk1(0.f);
+            } else {
+                bs.type = EDiffuseReflection;
+                bs.wo = squareToCosineHemisphere(u0, sy);
+            }
+            bs.eta = 1.0f;
+            bs.pdf = bsdfPdf1<PG_BSDF_ROUGHPLASTIC>(M, wi, bs.wo);
+            if (bs.pdf == 0) return mk1(0.f);
+            return bsdfEval1<PG_BSDF_ROUGHPLASTIC>(M, wi, bs.wo) / bs.pdf;
         }
         default: return mk1(0.f);
     }

@@ -17,6 +17,7 @@
 #include "pg_bvh.h"
 #include "pg_kernels.h"
 #include "pg_layout.h"
+#include "pg_rtrans.h"
 #include "pg_sdtree.h"
 
 namespace {
@@ -26,7 +27,7 @@ constexpr uint32_t kMaxBounces = 1100;     // > gpu_depth_cap default (1024) + 2
 // per-bounce device counters (words): [0, 64) shard counts of the live queue entering the bounce,
 // [64, 128) shadow-queue shard counts, [128, 512) shard counts of the PG_NUM_CLASSES material-class
 // queues followed by the escaped-path counts
-constexpr uint32_t kBounceWords = 512;
+constexpr uint32_t kBounceWords = 640;
 constexpr uint32_t kShadowCounts = PG_QSHARDS, kClassCounts = 2 * PG_QSHARDS;
 static_assert(kClassCounts + (PG_NUM_CLASSES + 1) * PG_QSHARDS <= kBounceWords, "counter layout");
 constexpr uint32_t kCounterWords = kBounceWords * (kMaxBounces + 1);
@@ -38,6 +39,7 @@ int materialClass(uint32_t model) {
         case PG_BSDF_ROUGHCONDUCTOR: return PG_CLASS_ROUGHCONDUCTOR;
         case PG_BSDF_ROUGHDIELECTRIC: return PG_CLASS_ROUGHDIELECTRIC;
         case PG_BSDF_PLASTIC: return PG_CLASS_PLASTIC;
+        case PG_BSDF_ROUGHPLASTIC: return PG_CLASS_ROUGHPLASTIC;
         default: return PG_CLASS_DELTA;
     }
 }
@@ -127,7 +129,7 @@ struct Ctx {
     // scene
     bool has_scene = false;
     GParams g{};
-    DevBuf nodes, woop, wnodes, wwoop, tshade, tclass, mats, ems, emtri, emcdf;
+    DevBuf nodes, woop, wnodes, wwoop, tshade, tclass, mats, rtab, ems, emtri, emcdf;
     uint32_t num_tris = 0, num_mats = 0;
     std::vector<GMat> host_mats;
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
@@ -228,6 +230,12 @@ GMat makeGMat(const pg_material &m) {
         case PG_BSDF_PLASTIC: {
             g.type = 0x20 | 0x2;
             g.fdrInt = fresnelDiffuseReflectanceH(1 / g.eta);
+            float dAvg = luminance(m.diffuse_reflectance), sAvg = luminance(m.specular_reflectance);
+            g.specWeight = sAvg / (dAvg + sAvg);
+            break;
+        }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:258-307; table + fdrInt set by the caller
+            g.type = 0x8 | 0x2;         // EGlossyReflection | EDiffuseReflection
             float dAvg = luminance(m.diffuse_reflectance), sAvg = luminance(m.specular_reflectance);
             g.specWeight = sAvg / (dAvg + sAvg);
             break;
@@ -588,8 +596,28 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     }
     c->host_mats.clear();
     for (uint32_t m = 0; m < d->num_materials; ++m) c->host_mats.push_back(makeGMat(d->materials[m]));
+    // roughplastic: rough-transmittance slice + internal diffuse Fresnel per material
+    // (RoughPlastic::configure, roughplastic.cpp:283-299; ranges of rtrans.h checkEta/checkAlpha)
+    std::vector<float> rtab;
+    std::vector<std::pair<uint32_t, size_t>> rtabOf;
+    for (uint32_t m = 0; m < d->num_materials; ++m) {
+        const pg_material &pm = d->materials[m];
+        if (pm.type != PG_BSDF_ROUGHPLASTIC) continue;
+        GMat &gm = c->host_mats[m];
+        if (pm.alpha_u != pm.alpha_v)
+            return fail(c, PG_ERR_INVALID, "pg_upload_scene: roughplastic does not support anisotropic roughness");
+        const float e = gm.eta < 1 ? 1 / gm.eta : gm.eta;
+        if (!(e >= 1.0001f && e <= 4.0f) || !(gm.alpha_u <= 4.0f))
+            return fail(c, PG_ERR_INVALID, "pg_upload_scene: roughplastic IOR or roughness outside the tabulated range");
+        const size_t off = rtab.size();
+        rtab.resize(off + pgh::kRoughTransSamples);
+        pgh::roughTransmittance((int)pm.distribution, gm.alpha_u, gm.eta, &rtab[off], &gm.fdrInt);
+        rtabOf.push_back({m, off});
+    }
 
     pg_status s;
+    if ((s = upload(c, c->rtab, rtab))) return s;
+    for (auto &mo : rtabOf) c->host_mats[mo.first].rtrans = c->rtab.as<float>() + mo.second;
     if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) ||
         (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->wwoop, bvh.wwoop)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||
@@ -901,6 +929,14 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         c->rec_host_count = c->rec_bound = rc;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_rough_transmittance(uint32_t distribution, float alpha, float eta, float *table, float *fdr_int) {
+    if (!table || !fdr_int) return fail(nullptr, PG_ERR_INVALID, "pg_rough_transmittance: null argument");
+    if (distribution > PG_DIST_GGX || !(alpha >= 0) || !(eta > 0) || eta == 1.0f)
+        return fail(nullptr, PG_ERR_INVALID, "pg_rough_transmittance: bad distribution, alpha or eta");
+    pgh::roughTransmittance((int)distribution, std::max(alpha, 1e-4f), eta, table, fdr_int);
     return PG_OK;
 }
 

@@ -974,6 +974,9 @@ void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const Scene
         case PG_CLASS_PLASTIC:
             hipLaunchKernelGGL((k_shade<PG_BSDF_PLASTIC, false>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
             break;
+        case PG_CLASS_ROUGHPLASTIC:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHPLASTIC, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
         default:  // delta lobes: conductor, dielectric (runtime switch, never guided)
             hipLaunchKernelGGL((k_shade<-1, false>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
     }

@@ -13,7 +13,13 @@ struct GMat {
     float diff[4];
     float spec[4];
     float trans[4];
-    float ceta[4];
+    union {
+        float ceta[4];
+        struct {
+            const float *rtrans;  // roughplastic: external rough-transmittance table (device)
+            float pad1[2];
+        };
+    };
     float ck[4];
 };
 static_assert(sizeof(GMat) == 128, "GMat layout");
@@ -63,8 +69,9 @@ static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 #define PG_CLASS_ROUGHCONDUCTOR 1
 #define PG_CLASS_ROUGHDIELECTRIC 2
 #define PG_CLASS_PLASTIC 3
-#define PG_CLASS_DELTA 4
-#define PG_NUM_CLASSES 5
+#define PG_CLASS_ROUGHPLASTIC 4
+#define PG_CLASS_DELTA 5
+#define PG_NUM_CLASSES 6
 
 // Path-state flags (pinfo.z high bits)
 #define PF_SCATTERED 0x1u

@@ -46,6 +46,18 @@ class PGError(RuntimeError):
         self.status = status
 
 
+def rough_transmittance(distribution, alpha, eta):
+    """roughplastic's rough-transmittance slice (pg_rough_transmittance): the 100-entry table over
+    cos^(1/4) and the internal diffuse Fresnel reflectance.  Host-only, no device needed."""
+    lib = library()
+    table = np.zeros(100, np.float32)
+    fdr = C.c_float()
+    st = lib.pg_rough_transmittance(int(distribution), float(alpha), float(eta), _p(table), C.byref(fdr))
+    if st != capi.PG_OK:
+        raise PGError(st, lib.pg_last_error(None).decode())
+    return table, fdr.value
+
+
 class Device:
     """One pg_ctx: a render context bound to one HIP device and one image-tile shard."""
 

@@ -30,11 +30,13 @@ def _f4(v):
 
 
 def material(kind, **kw):
-    """Build a pg_material.  kind in diffuse|conductor|roughconductor|dielectric|roughdielectric|plastic."""
+    """Build a pg_material.  kind in diffuse|conductor|roughconductor|dielectric|roughdielectric|plastic|
+    roughplastic."""
     m = capi.pg_material()
     types = {"diffuse": capi.PG_BSDF_DIFFUSE, "conductor": capi.PG_BSDF_CONDUCTOR,
              "roughconductor": capi.PG_BSDF_ROUGHCONDUCTOR, "dielectric": capi.PG_BSDF_DIELECTRIC,
-             "roughdielectric": capi.PG_BSDF_ROUGHDIELECTRIC, "plastic": capi.PG_BSDF_PLASTIC}
+             "roughdielectric": capi.PG_BSDF_ROUGHDIELECTRIC, "plastic": capi.PG_BSDF_PLASTIC,
+             "roughplastic": capi.PG_BSDF_ROUGHPLASTIC}
     m.type = types[kind]
     dist = kw.get("distribution", "beckmann")
     m.distribution = capi.PG_DIST_GGX if dist == "ggx" else capi.PG_DIST_BECKMANN
@@ -50,7 +52,7 @@ def material(kind, **kw):
     m.alpha_u = kw.get("alpha_u", a)
     m.alpha_v = kw.get("alpha_v", a)
     # dielectric defaults: intIOR bk7 1.5046, extIOR air 1.000277 (dielectric.cpp); plastic polypropylene 1.49
-    if kind == "plastic":
+    if kind in ("plastic", "roughplastic"):
         m.int_ior = kw.get("int_ior", 1.49)
     else:
         m.int_ior = kw.get("int_ior", 1.5046)
@@ -278,7 +280,9 @@ def cylinder(center, radius, height, n=64):
 
 # ---------------------------------------------------------------------------------------------
 # C1/C2: the Cornell box (measured geometry of the Cornell data set, in metres)
-def cornell(width=512, height=512):
+def cornell(width=512, height=512, short_material=None, tall_material=None):
+    """Cornell box (C1/C2).  short_material / tall_material: optional pg_material for the blocks
+    (default: the white diffuse)."""
     s = Scene()
     s.name = "cornell"
     white = s.add_material(material("diffuse", reflectance=(0.725, 0.71, 0.68)))
@@ -329,8 +333,8 @@ def cornell(width=512, height=512):
         [P(314.0, 0.0, 456.0), P(314.0, 330.0, 456.0), P(265.0, 330.0, 296.0), P(265.0, 0.0, 296.0)],
         [P(265.0, 0.0, 296.0), P(265.0, 330.0, 296.0), P(423.0, 330.0, 247.0), P(423.0, 0.0, 247.0)],
     ]
-    block(short, white)
-    block(tall, white)
+    block(short, white if short_material is None else s.add_material(short_material))
+    block(tall, white if tall_material is None else s.add_material(tall_material))
     s.set_camera(P(278, 273, -800), P(278, 273, -799), (0, 1, 0), 39.3077, width, height)
     return s.finalize()
 

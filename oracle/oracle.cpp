@@ -409,6 +409,13 @@ void oracle_intersect(void *sp, const float *rays, uint64_t n, float *out) {
 }
 
 // Per query: out[12] = wo.xyz, pdf, weight.rgb, sampledType, eval(wi, wo_given).rgb, pdf(wi, wo_given)
+// roughplastic slices (orc_rtrans.h): table[100], fdr_int
+void oracle_rough_transmittance(uint32_t dist, float alpha, float eta, float *table, float *fdr) {
+    std::vector<float> t;
+    roughPlasticTables((int)dist, std::max(alpha, 1e-4f), eta, t, *fdr);
+    for (int i = 0; i < kRtransSamples; ++i) table[i] = t[i];
+}
+
 void oracle_bsdf_query(const pg_material *pm, const float *wi, const float *u, const float *wog, uint64_t n, float *out) {
     Material M = makeMaterial(*pm);
     for (uint64_t i = 0; i < n; ++i) {

@@ -47,6 +47,7 @@ def lib(capi):
             "oracle_trace_rays": (None, [VP, VP, C.c_uint64, C.c_int32, VP]),
             "oracle_bsdf_query": (None, [C.POINTER(capi.pg_material), VP, VP, VP, C.c_uint64, VP]),
             "oracle_material_type": (C.c_uint32, [C.POINTER(capi.pg_material)]),
+            "oracle_rough_transmittance": (None, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
             "oracle_intersect": (None, [VP, VP, C.c_uint64, VP]),
         }
         for k, (r, a) in sig.items():
@@ -172,3 +173,11 @@ def bsdf_query(capi, mat, wi, u, wo_given=None):
 
 def material_type(capi, mat):
     return lib(capi).oracle_material_type(C.byref(mat))
+
+
+def rough_transmittance(capi, distribution, alpha, eta):
+    """Oracle roughplastic slices (orc_rtrans.h): (table[100], fdr_int)."""
+    table = np.zeros(100, np.float32)
+    fdr = np.zeros(1, np.float32)
+    lib(capi).oracle_rough_transmittance(int(distribution), float(alpha), float(eta), _p(table), _p(fdr))
+    return table, float(fdr[0])

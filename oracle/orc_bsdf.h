@@ -6,11 +6,15 @@
 //   dielectric     src/bsdfs/dielectric.cpp:235-340
 //   roughdielectric src/bsdfs/roughdielectric.cpp:277-620
 //   plastic        src/bsdfs/plastic.cpp:271-460
+//   roughplastic   src/bsdfs/roughplastic.cpp:258-510 (rough transmittance: orc_rtrans.h)
 //   twosided       src/bsdfs/twosided.cpp:116-190 (flag PG_MAT_TWOSIDED)
 // Type bits are EBSDFType (include/mitsuba/render/bsdf.h:224-262).
 #pragma once
 #include "../include/pg_capi.h"
 #include "orc_math.h"
+#include "orc_rtrans.h"
+
+#include <memory>
 
 namespace orc {
 
@@ -30,8 +34,9 @@ struct Material {
     // derived constants (configure())
     float eta = 1, invEta = 1;        // dielectric / plastic: int/ext
     float fdrInt = 0, fdrExt = 0;     // plastic
-    float specSamplingWeight = 0;     // plastic
+    float specSamplingWeight = 0;     // plastic, roughplastic
     float invEta2 = 1;
+    std::shared_ptr<std::vector<float>> rtrans;  // roughplastic: external rough transmittance
     uint32_t type = 0;                // combined EBSDFType
     V3 diff() const { return {m.diffuse_reflectance[0], m.diffuse_reflectance[1], m.diffuse_reflectance[2]}; }
     V3 spec() const { return {m.specular_reflectance[0], m.specular_reflectance[1], m.specular_reflectance[2]}; }
@@ -67,6 +72,14 @@ inline Material makeMaterial(const pg_material &pm) {
             M.specSamplingWeight = sAvg / (dAvg + sAvg);
             break;
         }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:258-307
+            M.type = EGlossyReflection | EDiffuseReflection;
+            float dAvg = luminance(M.diff()), sAvg = luminance(M.spec());
+            M.specSamplingWeight = sAvg / (dAvg + sAvg);
+            M.rtrans = std::make_shared<std::vector<float>>();
+            roughPlasticTables((int)pm.distribution, std::max(pm.alpha_u, 1e-4f), M.eta, *M.rtrans, M.fdrInt);
+            break;
+        }
         default: M.type = 0;
     }
     if (M.twosided()) sides |= EBackSide;
@@ -88,6 +101,11 @@ inline V3 plasticDiff(const Material &M) {
     V3 d = M.diff();
     if (M.m.flags & PG_MAT_NONLINEAR) return d / (V3(1.0f) - d * M.fdrInt);
     return d / (1 - M.fdrInt);
+}
+
+inline float roughPlasticProbSpec(const Material &M, float cosThetaI) {  // roughplastic.cpp:405-414
+    float p = 1 - rtransEval(M.rtrans->data(), cosThetaI);
+    return (p * M.specSamplingWeight) / (p * M.specSamplingWeight + (1 - p) * (1 - M.specSamplingWeight));
 }
 
 inline V3 eval1(const Material &M, V3 wi, V3 wo) {
@@ -139,6 +157,17 @@ inline V3 eval1(const Material &M, V3 wi, V3 wo) {
             float Fo = fresnelDielectricExt(wo.z, M.eta);
             return plasticDiff(M) * (cosineHemispherePdf(wo) * M.invEta2 * (1 - Fi) * (1 - Fo));
         }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:344-397
+            if (wi.z <= 0 || wo.z <= 0) return V3(0.f);
+            Microfacet d = M.distr();
+            V3 H = normalize(wo + wi);
+            float D = d.eval(H);
+            float F = fresnelDielectricExt(dot(wi, H), M.eta);
+            float G = d.G(wi, wo, H);
+            float value = F * D * G / (4.0f * wi.z);
+            float T12 = rtransEval(M.rtrans->data(), wi.z), T21 = rtransEval(M.rtrans->data(), wo.z);
+            return M.spec() * value + plasticDiff(M) * (kInvPi * wo.z * T12 * T21 * M.invEta2);
+        }
         default: return V3(0.f);  // delta-only models have no solid-angle density
     }
 }
@@ -182,6 +211,15 @@ inline float pdf1(const Material &M, V3 wi, V3 wo) {
             float ps = (Fi * M.specSamplingWeight) /
                        (Fi * M.specSamplingWeight + (1 - Fi) * (1 - M.specSamplingWeight));
             return cosineHemispherePdf(wo) * (1 - ps);
+        }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:398-447
+            if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+            Microfacet d = M.distr();
+            V3 H = normalize(wo + wi);
+            float probSpecular = roughPlasticProbSpec(M, wi.z), probDiffuse = 1 - probSpecular;
+            float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+            float prob = d.pdf(wi, H);
+            return prob * dwh_dwo * probSpecular + probDiffuse * cosineHemispherePdf(wo);
         }
         default: return 0.0f;
     }
@@ -302,6 +340,33 @@ inline V3 sample1(const Material &M, V3 wi, float u0, float u1, float u2, BSampl
                 bs.pdf = (1 - ps) * cosineHemispherePdf(bs.wo);
                 return plasticDiff(M) * (M.invEta2 * (1 - Fi) * (1 - Fo) / (1 - ps));
             }
+        }
+        case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:449-510
+            if (wi.z <= 0) return V3(0.f);
+            float ps = roughPlasticProbSpec(M, wi.z);
+            float sy = u1;
+            bool spec = true;
+            if (sy < ps) {
+                sy /= ps;
+            } else {
+                sy = (sy - ps) / (1 - ps);
+                spec = false;
+            }
+            if (spec) {
+                Microfacet d = M.distr();
+                float mpdf;
+                V3 m = d.sample(wi, u0, sy, mpdf);
+                bs.wo = reflectV(wi, m);
+                bs.sampledType = EGlossyReflection;
+                if (bs.wo.z <= 0) return V3(0.f);
+            } else {
+                bs.sampledType = EDiffuseReflection;
+                bs.wo = squareToCosineHemisphere(u0, sy);
+            }
+            bs.eta = 1.0f;
+            bs.pdf = pdf1(M, wi, bs.wo);
+            if (bs.pdf == 0) return V3(0.f);
+            return eval1(M, wi, bs.wo) / bs.pdf;
         }
         default: return V3(0.f);
     }

@@ -7,7 +7,8 @@ compare against the pdf integrated over each bin with a chi-square test at signi
 
 The test_bsdf.xml entries covered are those of the configs' BSDF set (diffuse, twosided, conductor,
 dielectric water/air, roughdielectric beckmann/ggx alpha .3, roughconductor beckmann alpha .3, an
-anisotropic rough conductor (GGX 0.1/0.3 in place of the unsupported Ashikhmin-Shirley), plastic).
+anisotropic rough conductor (GGX 0.1/0.3 in place of the unsupported Ashikhmin-Shirley), plastic,
+roughplastic beckmann alpha .7 plus a GGX one).
 """
 import numpy as np
 import pytest
@@ -32,11 +33,15 @@ def materials(S):
         ("roughdielectric_beckmann", S.material("roughdielectric", int_ior=1.5, ext_ior=1.0, alpha=0.3), True),
         ("roughdielectric_ggx", S.material("roughdielectric", int_ior=1.5, ext_ior=1.0, alpha=0.3,
                                            distribution="ggx"), True),
+        ("roughplastic_beckmann", S.material("roughplastic", alpha=0.7), False),  # test_bsdf.xml:133-136
+        ("roughplastic_ggx", S.material("roughplastic", alpha=0.2, distribution="ggx",
+                                        diffuse_reflectance=(0.5, 0.3, 0.2)), False),
     ]
 
 
-def _bins_pdf(O, capi, mat, wi, sub=10):
-    """pdf integrated over each (theta, phi) bin by a sub x sub midpoint rule (solid angle)."""
+def _bins_pdf(O, capi, mat, wi, sub=30):
+    """pdf integrated over each (theta, phi) bin by a sub x sub midpoint rule (solid angle); sub=10
+    under-resolves glossy lobes of alpha ~0.2 (false rejections), 30 does not."""
     th_edges = np.linspace(0, np.pi, THETA_BINS + 1)
     ph_edges = np.linspace(0, 2 * np.pi, PHI_BINS + 1)
     dth = np.pi / THETA_BINS / sub
@@ -81,7 +86,7 @@ def _chi2(obs, exp):
     return float(stats.chi2.sf(chi, len(po) - 1))
 
 
-@pytest.mark.parametrize("idx", range(8))
+@pytest.mark.parametrize("idx", range(10))
 def test_chisquare(pg, O, idx):
     name, mat, both_sides = materials(pg.scenes)[idx]
     rng = np.random.default_rng(100 + idx)
@@ -160,3 +165,5 @@ def test_material_types(pg, O):
     assert O.material_type(c, S.material("dielectric")) == c.EDelta | c.EFrontSide | c.EBackSide
     assert O.material_type(c, S.material("roughconductor")) == c.EGlossyReflection | c.EFrontSide
     assert O.material_type(c, S.material("plastic")) == c.EDeltaReflection | c.EDiffuseReflection | c.EFrontSide
+    assert O.material_type(c, S.material("roughplastic", alpha=0.3)) == (c.EGlossyReflection | c.EDiffuseReflection
+                                                                           | c.EFrontSide)

@@ -1,0 +1,60 @@
+"""roughplastic's rough-transmittance slices against the reference's precomputed tables.
+
+The reference ships data/microfacet/{beckmann,ggx}.dat (src/utils/rdielprec.cpp) and reduces them
+per material in RoughPlastic::configure (roughplastic.cpp:283-299, rtrans.h setEta/setAlpha/
+evalDiffuse).  tests/golden/rtrans_slices.npz holds those reductions for four (distribution, eta,
+alpha) cases (made by tests/golden/make_rtrans_fixture.py from the .dat files).  The library
+(pg_rough_transmittance, host-only) and the oracle integrate the same quantity directly at the
+material's (eta, alpha) with different estimators; both must agree with the shipped tables.
+"""
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "rtrans_slices.npz")
+TABLE_TOL = 5e-4   # absolute, transmittance in [0, 1]
+FDR_TOL = 2e-3     # the reference's internal diffuse value is itself cubic-interpolated in (alpha, eta)
+
+
+def _cases():
+    z = np.load(GOLDEN)
+    n = len([k for k in z.files if k.endswith("_params")])
+    return [(z[f"case{i}_params"], z[f"case{i}_table"], float(z[f"case{i}_fdr_int"][0])) for i in range(n)]
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_library_tables_match_reference(pg, i):
+    from mitsuba_path_guiding_amd.integrator import rough_transmittance
+    (dist, eta, alpha), table, fdr = _cases()[i]
+    t, f = rough_transmittance(int(dist), alpha, eta)
+    assert np.abs(t - table).max() < TABLE_TOL
+    assert abs(f - fdr) < FDR_TOL
+
+
+@pytest.mark.parametrize("i", range(4))
+def test_oracle_tables_match_reference(pg, O, i):
+    (dist, eta, alpha), table, fdr = _cases()[i]
+    t, f = O.rough_transmittance(pg.capi, int(dist), alpha, eta)
+    assert np.abs(t - table).max() < TABLE_TOL
+    assert abs(f - fdr) < FDR_TOL
+
+
+def test_library_vs_oracle_and_limits(pg, O):
+    from mitsuba_path_guiding_amd.integrator import rough_transmittance
+    for dist, eta, alpha in [(0, 1.3, 0.05), (1, 2.0, 0.5), (0, 1.6, 1.5)]:
+        t, f = rough_transmittance(dist, alpha, eta)
+        to, fo = O.rough_transmittance(pg.capi, dist, alpha, eta)
+        assert np.abs(t - to).max() < 1e-3 and abs(f - fo) < 1e-3
+        # normal incidence of a nearly smooth interface: 1 - Fresnel reflectance
+        if alpha <= 0.05:
+            assert abs(t[-1] - (1 - ((eta - 1) / (eta + 1)) ** 2)) < 2e-3
+        assert np.all((t >= 0) & (t <= 1)) and 0 < f < 1
+
+
+def test_rejects_bad_arguments(pg):
+    from mitsuba_path_guiding_amd.integrator import PGError, rough_transmittance
+    with pytest.raises(PGError):
+        rough_transmittance(7, 0.1, 1.5)
+    with pytest.raises(PGError):
+        rough_transmittance(0, 0.1, 1.0)
