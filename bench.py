@@ -45,6 +45,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--train", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
     return ap.parse_args()
@@ -61,15 +62,20 @@ def main():
 
     rank, world, local = D.env_rank()
     world = max(world, 1)
+    # RCCL ("nccl") over xGMI; PG_DIST_BACKEND=gloo rehearses the multi-rank path with ranks
+    # sharing the visible GPUs (collectives through host memory)
+    backend = os.environ.get("PG_DIST_BACKEND", "nccl")
     if world > 1:
-        D.init("nccl")
+        D.init(backend)
     import torch
 
-    on_dev = torch.cuda.is_available()
+    on_dev = torch.cuda.is_available() and backend == "nccl"
+    device = local % max(1, torch.cuda.device_count())
     scene = pg.scenes.SCENES[a.scene](a.width, a.height)
-    exchange = D.make_exchange(on_dev) if world > 1 else None
+    # postprogression exchange: all-reduce of the SD-tree building statistics
+    exchange = D.make_exchange(on_dev, mode=a.exchange) if world > 1 else None
     # one progression for the final render (the device chunks it into waves of <= 4M paths)
-    integ = GuidedPathTracer({"trainingIterations": a.train, "samplesPerProgression": a.spp}, device=local,
+    integ = GuidedPathTracer({"trainingIterations": a.train, "samplesPerProgression": a.spp}, device=device,
                              rank=rank, world_size=world, exchange=exchange)
     integ.preprocess(scene)
     dev = integ.dev
@@ -77,7 +83,7 @@ def main():
     def barrier():
         if world > 1:
             torch.distributed.barrier()
-        if on_dev:
+        if torch.cuda.is_available():
             torch.cuda.synchronize()
 
     def job():
@@ -107,7 +113,7 @@ def main():
                 "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
                 "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
                 "note": "all path kernels over the timed wall clock (3 path lanes run concurrently)"}
-    roofline = kernel_roofline(pg, scene, integ, local, a)
+    roofline = kernel_roofline(pg, scene, integ, device, a)
 
     # ---- CPU baseline (oracle, rank 0, N = 1, bounded sample) + equal-spp RMSE on the sample
     cpu = None
@@ -125,7 +131,7 @@ def main():
                                    f"iterations (1..{2 ** (a.train - 1)} spp) + {a.spp} spp render",
                        "scene": a.scene, "triangles": scene.num_triangles, "width": a.width, "height": a.height,
                        "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
-                       "parallelism": f"tile-shard x{world}, RCCL all-gather of records"},
+                       "parallelism": f"tile-shard x{world}, RCCL {a.exchange} per training iteration"},
             "roofline": roofline,
             "pipeline": pipeline,
             "cpu_baseline": cpu,

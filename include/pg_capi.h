@@ -240,6 +240,15 @@ pg_status pg_bsdf_query(void *ctx, uint32_t material, const float *wi, const flo
  * table[100] = transmittance at cos(theta) = (j/99)^4 (interpolated with Catmull-Rom in
  * cos^(1/4)), fdr_int = 1 - internal diffuse transmittance.  Computed on the host at scene upload
  * by quadrature instead of read from data/microfacet/ *.dat.  Needs no device or context. */
+/* Building-tree statistics of the SD-tree, i.e. the additive state that splats produce: the u64
+ * quadrant sums of every building node (4 per node, 2^-24 fixed point) followed by the record count
+ * of every D-tree (u64), in the order of the serialized tree.  Summing these vectors over ranks
+ * (an all-reduce) and putting the sum back equals splatting every rank's records into one tree,
+ * bit for bit (replaces the record all-gather of postprogression).
+ * dst == NULL: only *words is returned.  Between pg_refit calls the layout is fixed. */
+pg_status pg_get_tree_stats(void *ctx, void *dst, uint64_t capacity_words, int32_t dst_is_device, uint64_t *words);
+pg_status pg_put_tree_stats(void *ctx, const void *src, uint64_t words, int32_t src_is_device);
+
 pg_status pg_rough_transmittance(uint32_t distribution, float alpha, float eta, float *table, float *fdr_int);
 
 #ifdef __cplusplus

@@ -135,6 +135,8 @@ SIGNATURES = [
     ("pg_trace_rays", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_bsdf_query", C.c_int32, [VP, C.c_uint32, VP, VP, VP, C.c_uint64, VP]),
     ("pg_rough_transmittance", C.c_int32, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
+    ("pg_get_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
+    ("pg_put_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32]),
 ]
 
 

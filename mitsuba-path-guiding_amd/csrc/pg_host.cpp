@@ -295,7 +295,7 @@ SDDev sdView(const Ctx *c) {
     s.qchild = c->sd_qchild.as<uint4>();
     s.bchild = c->sd_bchild.as<uint4>();
     s.bsum = c->sd_bsum.as<unsigned long long>();
-    s.count = c->sd_count.as<uint32_t>();
+    s.count = c->sd_count.as<unsigned long long>();
     s.jump = c->sd_jump.as<uint32_t>();
     s.jump_bits = c->sd_jump_bits;
     for (int a = 0; a < 3; ++a) s.lo[a] = c->sd.lo[a];
@@ -313,6 +313,7 @@ PathDev pathView(const Lane *c) {
 pg_status uploadSd(Ctx *c) {
     pgh::SdTree::Flat f;
     c->sd.flatten(f);
+    const std::vector<uint64_t> count64(f.count.begin(), f.count.end());
     struct Part {
         DevBuf *dst;
         const void *src;
@@ -320,7 +321,7 @@ pg_status uploadSd(Ctx *c) {
     } parts[] = {{&c->sd_snodes, f.snodes.data(), f.snodes.size() * 4}, {&c->sd_meta, f.meta.data(), f.meta.size() * 4},
                  {&c->sd_qsum, f.qsum.data(), f.qsum.size() * 4},       {&c->sd_qchild, f.qchild.data(), f.qchild.size() * 4},
                  {&c->sd_bchild, f.bchild.data(), f.bchild.size() * 4}, {&c->sd_bsum, f.bsum.data(), f.bsum.size() * 8},
-                 {&c->sd_count, f.count.data(), f.count.size() * 4},    {&c->sd_jump, f.jump.data(), f.jump.size() * 4}};
+                 {&c->sd_count, count64.data(), count64.size() * 8},    {&c->sd_jump, f.jump.data(), f.jump.size() * 4}};
     size_t total = 0;
     for (const Part &pt : parts) total += (pt.bytes + 255) & ~(size_t)255;
     HIPC(c, c->sd_stage.reserve(total));
@@ -346,13 +347,15 @@ pg_status uploadSd(Ctx *c) {
 pg_status downloadSd(Ctx *c) {
     size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
     const size_t sb = (32 * nb + 255) & ~(size_t)255;
-    HIPC(c, c->sd_stage.reserve(sb + 4 * nl));
+    HIPC(c, c->sd_stage.reserve(sb + 8 * nl));
     uint64_t *bsum = (uint64_t *)c->sd_stage.p;
-    uint32_t *cnt = (uint32_t *)((uint8_t *)c->sd_stage.p + sb);
+    uint64_t *cnt = (uint64_t *)((uint8_t *)c->sd_stage.p + sb);
     HIPC(c, hipMemcpyAsync(bsum, c->sd_bsum.p, 32 * nb, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(cnt, c->sd_count.p, 4 * nl, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(cnt, c->sd_count.p, 8 * nl, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
-    c->sd.absorb(bsum, cnt);
+    std::vector<uint32_t> cnt32(nl);
+    for (size_t i = 0; i < nl; ++i) cnt32[i] = (uint32_t)std::min<uint64_t>(cnt[i], 0xFFFFFFFFu);
+    c->sd.absorb(bsum, cnt32.data());
     return PG_OK;
 }
 
@@ -1007,6 +1010,36 @@ pg_status pg_refit(void *ctx, uint32_t iteration) {
     HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 8, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     c->rec_host_count = 0;
+    return PG_OK;
+}
+
+pg_status pg_get_tree_stats(void *ctx, void *dst, uint64_t capacity_words, int32_t dst_is_device, uint64_t *words) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !words) return fail(c, PG_ERR_INVALID, "pg_get_tree_stats: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_get_tree_stats: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
+    *words = 4 * nb + nl;
+    if (!dst) return PG_OK;
+    if (capacity_words < *words) return fail(c, PG_ERR_INVALID, "pg_get_tree_stats: buffer too small");
+    const hipMemcpyKind k = dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIPC(c, hipMemcpyAsync(dst, c->sd_bsum.p, 32 * nb, k, c->stream));
+    HIPC(c, hipMemcpyAsync((uint64_t *)dst + 4 * nb, c->sd_count.p, 8 * nl, k, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_put_tree_stats(void *ctx, const void *src, uint64_t words, int32_t src_is_device) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !src) return fail(c, PG_ERR_INVALID, "pg_put_tree_stats: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_put_tree_stats: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
+    if (words != 4 * nb + nl) return fail(c, PG_ERR_INVALID, "pg_put_tree_stats: size does not match the tree");
+    const hipMemcpyKind k = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    HIPC(c, hipMemcpyAsync(c->sd_bsum.p, src, 32 * nb, k, c->stream));
+    HIPC(c, hipMemcpyAsync(c->sd_count.p, (const uint64_t *)src + 4 * nb, 8 * nl, k, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }
 

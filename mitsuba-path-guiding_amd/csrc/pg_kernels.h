@@ -34,7 +34,7 @@ struct SDDev {
     const uint4 *qchild;
     const uint4 *bchild;
     unsigned long long *bsum;  // 4 per building node
-    uint32_t *count;           // per D-tree
+    unsigned long long *count;  // records per D-tree (u64, so the building statistics are one u64 vector)
     const uint32_t *jump;      // S-tree jump grid, (2^jump_bits)^3 node ids
     float lo[3];
     float extent;

@@ -843,7 +843,7 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
             }
         }
     }
-    waveKeyedAdd<uint32_t>(sd.count, dt, 1u, valid);
+    waveKeyedAdd<unsigned long long>(sd.count, dt, 1ull, valid);
     waveKeyedAdd<unsigned long long>(sd.bsum, slot, fx, found);
 }
 

@@ -5,13 +5,17 @@ gloo on CPU for tests.  Replaces the reference's master/worker TCP/SSH scheduler
   * image tiles are sharded statically across ranks inside the C-ABI context (pg_config.rank /
     world_size, 32x32 tiles dealt round-robin; the RNG is keyed by the global pixel, so results do
     not depend on the number of ranks);
-  * before each SD-tree refit (postprogression) every rank all-gathers the training records of all
-    ranks (counts first, then one all_gather of the padded record buffers) and splats them in rank
-    order.  The splat is exact integer arithmetic, so every rank refits a bit-identical tree;
+  * before each SD-tree refit (postprogression) every rank splats its own training records into
+    its building tree, then the building-tree statistics (u64 fixed-point quadrant sums + record
+    counts, pg_get_tree_stats) are all-reduced (SUM) and put back.  Integer sums are exact, so
+    every rank refits a bit-identical tree, equal to splatting all records on one GPU
+    (a few MB per iteration instead of all-gathering ~1 GB of records, and the
+    splat work is split across ranks).  The record all-gather is kept as mode="allgather";
   * at the end the film tiles are sum-reduced to rank 0 (tiles are disjoint, so the sum is a gather).
 
-The exchange takes any object with the Device record interface (record_count / get_records /
-splat_records), which lets the gloo tests run it against a CPU stand-in.
+The exchange takes any object with the Device interface it uses (splat_local / tree_stats_words /
+get_tree_stats / put_tree_stats / record_count, or get_records / splat_records for "allgather"),
+which lets the gloo tests run it against a CPU stand-in.
 """
 import os
 
@@ -41,13 +45,36 @@ def init(backend=None):
     return rank, world, local
 
 
-def make_exchange(on_device):
-    """Returns exchange(dev): all-gather every rank's records and splat them into dev.
+def make_exchange(on_device, mode="allreduce"):
+    """Returns exchange(dev) for the postprogression slot; it returns every rank's record count.
 
-    on_device=True: records move device->device (RCCL over xGMI); False: through host memory (gloo).
+    mode="allreduce": splat local records, all-reduce the building-tree statistics.
+    mode="allgather": all-gather every rank's records and splat all of them into dev.
+    on_device=True: buffers move device->device (RCCL over xGMI); False: through host memory (gloo).
     """
     import torch
     import torch.distributed as dist
+    if mode not in ("allreduce", "allgather"):
+        raise ValueError(f"unknown exchange mode {mode!r}")
+
+    def exchange_allreduce(dev):
+        world = dist.get_world_size()
+        tdev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+        counts = torch.zeros(world, dtype=torch.int64, device=tdev)
+        dist.all_gather_into_tensor(counts, torch.tensor([int(dev.record_count())], dtype=torch.int64, device=tdev))
+        dev.splat_local()
+        words = int(dev.tree_stats_words())
+        if on_device:
+            t = torch.empty(words, dtype=torch.int64, device=tdev)
+            dev.get_tree_stats(dst_ptr=t.data_ptr(), words=words)  # synchronous on the library's stream
+            dist.all_reduce(t)
+            torch.cuda.synchronize()
+            dev.put_tree_stats(device_ptr=t.data_ptr(), words=words)
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(dev.get_tree_stats()).view(np.int64).copy())
+            dist.all_reduce(t)
+            dev.put_tree_stats(t.numpy().view(np.uint64))
+        return counts.cpu().tolist()
 
     def exchange(dev):
         world = dist.get_world_size()
@@ -85,7 +112,7 @@ def make_exchange(on_device):
                     dev.splat_records(g[off: off + counts[r] * RECORD_BYTES])
         return counts
 
-    return exchange
+    return exchange_allreduce if mode == "allreduce" else exchange
 
 
 def reduce_film(rgbw, sumsq, on_device):

@@ -124,6 +124,28 @@ class Device:
     def splat_local(self):
         self._chk(self.lib.pg_splat_local_records(self.h))
 
+    def tree_stats_words(self):
+        n = C.c_uint64()
+        self._chk(self.lib.pg_get_tree_stats(self.h, None, 0, 0, C.byref(n)))
+        return n.value
+
+    def get_tree_stats(self, dst_ptr=None, words=None):
+        """Building-tree statistics (pg_get_tree_stats): numpy uint64 array, or into device memory."""
+        n = C.c_uint64()
+        if dst_ptr is not None:
+            self._chk(self.lib.pg_get_tree_stats(self.h, C.c_void_p(dst_ptr), int(words), 1, C.byref(n)))
+            return n.value
+        out = np.zeros(self.tree_stats_words(), np.uint64)
+        self._chk(self.lib.pg_get_tree_stats(self.h, _p(out), len(out), 0, C.byref(n)))
+        return out
+
+    def put_tree_stats(self, stats=None, device_ptr=None, words=None):
+        if device_ptr is not None:
+            self._chk(self.lib.pg_put_tree_stats(self.h, C.c_void_p(device_ptr), int(words), 1))
+        else:
+            stats = np.ascontiguousarray(stats, np.uint64)
+            self._chk(self.lib.pg_put_tree_stats(self.h, _p(stats), len(stats), 0))
+
     def refit(self, iteration):
         self._chk(self.lib.pg_refit(self.h, iteration))
 

@@ -1,10 +1,14 @@
-"""World-size-2 gloo test of the multi-rank training path (CPU): tile sharding + the record
-all-gather of mitsuba_path_guiding_amd.distributed + splat + refit must leave every rank with the
-same SD-tree, bit for bit, and that tree must equal a single-rank training on the whole image
-(the splat is exact fixed-point arithmetic, so the order of gathered records cannot matter).
+"""World-size-2 gloo test of the multi-rank training path (CPU): tile sharding + the exchange of
+mitsuba_path_guiding_amd.distributed (both the building-statistics all-reduce and the record
+all-gather) + refit must leave every rank with the same SD-tree, bit for bit, and that tree must
+equal a single-rank training on the whole image (splats are exact fixed-point arithmetic, so
+neither record order nor where the sums were formed can matter).
 
 The per-rank "device" here is a CPU stand-in built on the oracle (test double): the exchange code
-under test only needs the Device record interface (record_count / get_records / splat_records).
+under test only needs the Device interface it calls (record_count / get_records / splat_records /
+splat_local / tree_stats_words / get_tree_stats / put_tree_stats).  The stand-in reads and writes
+the building statistics through the tree's wire format (pg_sdtree.cpp serialize), in the same
+order as pg_get_tree_stats.
 """
 import os
 import socket
@@ -58,8 +62,40 @@ class OracleShardDevice:
         self.tree.refit(it, self.cfg)
         self.pending = np.zeros(0, np.uint8)
 
+    def splat_local(self):
+        self.tree.splat_bytes(self.pending)
 
-def _worker(rank, world, port, outdir):
+    # building statistics through the wire format: header 16 B, box 32 B, counts (snodes, dtrees,
+    # sampling nodes, building nodes), snodes 8 B, D-tree meta 32 B (record count at word 5),
+    # sampling nodes 32 B, building nodes 48 B (u64 sum[4] + u32 child[4])
+    def _layout(self, blob):
+        ns, nd, nsamp, nb = np.frombuffer(blob[48:64].tobytes(), np.uint32)
+        meta = 64 + 8 * int(ns)
+        build = meta + 32 * int(nd) + 32 * int(nsamp)
+        return int(nd), int(nb), meta, build
+
+    def tree_stats_words(self):
+        nd, nb, _, _ = self._layout(self.tree.serialize())
+        return 4 * nb + nd
+
+    def get_tree_stats(self):
+        blob = self.tree.serialize()
+        nd, nb, meta, build = self._layout(blob)
+        sums = np.frombuffer(blob[build:build + 48 * nb].tobytes(), np.uint8).reshape(nb, 48)[:, :32]
+        cnt = np.frombuffer(blob[meta:meta + 32 * nd].tobytes(), np.uint32).reshape(nd, 8)[:, 5]
+        return np.concatenate([sums.copy().view(np.uint64).reshape(-1), cnt.astype(np.uint64)])
+
+    def put_tree_stats(self, stats):
+        blob = np.array(self.tree.serialize(), np.uint8)
+        nd, nb, meta, build = self._layout(blob)
+        b = blob[build:build + 48 * nb].reshape(nb, 48)
+        b[:, :32] = np.asarray(stats[:4 * nb], np.uint64).reshape(nb, 4).view(np.uint8)
+        m = blob[meta:meta + 32 * nd].reshape(nd, 32)
+        m[:, 20:24] = np.asarray(stats[4 * nb:], np.uint64).astype(np.uint32).reshape(nd, 1).view(np.uint8)
+        self.tree.deserialize(blob)
+
+
+def _worker(rank, world, port, outdir, mode):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
@@ -72,7 +108,7 @@ def _worker(rank, world, port, outdir):
     sc = pg.scenes.cornell(RES, RES)
     cfg = pg.capi.default_config(guiding=1, s_tree_threshold=THR, rank=rank, world_size=world)
     dev = OracleShardDevice(pg, O, sc, cfg, rank, world)
-    exchange = D.make_exchange(on_device=False)
+    exchange = D.make_exchange(on_device=False, mode=mode)
     off = 0
     for it in range(ITERS):
         dev.render_pass(2 ** it, off, True)
@@ -94,10 +130,11 @@ def _free_port():
     return p
 
 
-def test_two_rank_exchange_gives_identical_trees(pg, O, tmp_path):
+@pytest.mark.parametrize("mode", ["allreduce", "allgather"])
+def test_two_rank_exchange_gives_identical_trees(pg, O, tmp_path, mode):
     import torch.multiprocessing as mp
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     t0 = np.load(tmp_path / "tree0.npy")
     t1 = np.load(tmp_path / "tree1.npy")
     assert np.array_equal(t0, t1)

@@ -282,6 +282,34 @@ def test_image_parity_roughplastic(pg, O):
     assert abs(m1.mean() - m2.mean()) / m2.mean() < 0.01
 
 
+def test_tree_stats_allreduce_equals_single_rank(pg, scenes):
+    """The all-reduce exchange through the C-ABI (pg_get/put_tree_stats), emulated with two shard
+    contexts on one GPU: summed building statistics give the single-rank tree bit for bit."""
+    sc = scenes["cornell"]
+    cfg = dict(guiding=1, s_tree_threshold=300.0)
+    full = make_dev(pg, sc, **cfg)
+    parts = [make_dev(pg, sc, rank=r, world_size=2, **cfg) for r in range(2)]
+    off = 0
+    for it in range(3):
+        full.render_pass(2 ** it, off, True)
+        full.splat_local()
+        full.refit(it)
+        for d in parts:
+            d.render_pass(2 ** it, off, True)
+            d.splat_local()
+        stats = [d.get_tree_stats() for d in parts]
+        assert len(stats[0]) == parts[0].tree_stats_words()
+        total = stats[0] + stats[1]
+        for d in parts:
+            d.put_tree_stats(total)
+            d.refit(it)
+        off += 2 ** it
+    t = full.get_sdtree()
+    assert all(np.array_equal(d.get_sdtree(), t) for d in parts)
+    for d in parts + [full]:
+        d.close()
+
+
 def test_cancel_and_errors(pg, scenes):
     from mitsuba_path_guiding_amd.integrator import Device, PGError
     d = Device(pg.capi.default_config())
