@@ -75,7 +75,10 @@ struct AABB {
         lo = V3(std::min(lo.x, p.x), std::min(lo.y, p.y), std::min(lo.z, p.z));
         hi = V3(std::max(hi.x, p.x), std::max(hi.y, p.y), std::max(hi.z, p.z));
     }
-    void expand(const AABB &b) { expand(b.lo); expand(b.hi); }
+    void expand(const AABB &b) {  // component-wise, so an empty b (lo = +inf, hi = -inf) is a no-op
+        lo = V3(std::min(lo.x, b.lo.x), std::min(lo.y, b.lo.y), std::min(lo.z, b.lo.z));
+        hi = V3(std::max(hi.x, b.hi.x), std::max(hi.y, b.hi.y), std::max(hi.z, b.hi.z));
+    }
     float area() const {
         V3 e = hi - lo;
         if (e.x < 0) return 0;
@@ -276,10 +279,11 @@ inline void Scene::build(const pg_scene_desc &d) {
                     }
                 }
             }
-            if (bestAxis < 0 || best >= box.area() * j.count) {
-                if (j.count <= 16 || bestAxis < 0) {
+            // SAH with a traversal cost of one triangle test per node visit; leaves hold <= 8
+            if (bestAxis < 0 || box.area() + best >= box.area() * j.count) {
+                if (j.count <= 8 || bestAxis < 0) {
                     leaf = true;
-                    if (bestAxis < 0 && j.count > 16) {  // all centroids equal: split in the middle
+                    if (bestAxis < 0 && j.count > 8) {  // all centroids equal: split in the middle
                         leaf = false;
                         mid = j.first + j.count / 2;
                     }
@@ -321,25 +325,30 @@ inline bool Scene::traverse(const Ray &r, float mint, float maxt, bool any, floa
                             uint32_t &prim) const {
     if (nodes.empty()) return false;
     V3 inv(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
-    uint32_t stack[128];
-    int sp = 0;
-    stack[sp++] = 0;
     bool hit = false;
     float far = maxt;
-    while (sp > 0) {
-        const BvhNode &n = nodes[stack[--sp]];
-        // slab test against [mint, far]
+    // slab test of node n against [mint, far]; returns the entry distance or +inf on a miss
+    auto enter = [&](const BvhNode &n) {
         float t0 = mint, t1 = far;
-        bool ok = true;
-        for (int a = 0; a < 3 && ok; ++a) {
+        for (int a = 0; a < 3; ++a) {
             float ta = (n.box.lo[a] - r.o[a]) * inv[a], tb = (n.box.hi[a] - r.o[a]) * inv[a];
             if (ta > tb) std::swap(ta, tb);
             if (std::isnan(ta) || std::isnan(tb)) continue;  // degenerate slab with d == 0 and o on the plane
             t0 = std::max(t0, ta);
             t1 = std::min(t1, tb);
-            if (t0 > t1) ok = false;
+            if (t0 > t1) return kInf;
         }
-        if (!ok) continue;
+        return t0;
+    };
+    // near-first traversal: stack entries carry their entry distance, culled against `far`
+    std::vector<std::pair<uint32_t, float>> stack;
+    stack.reserve(64);
+    if (enter(nodes[0]) < kInf) stack.push_back({0u, 0.0f});
+    while (!stack.empty()) {
+        auto [ni, tin] = stack.back();
+        stack.pop_back();
+        if (tin > far) continue;
+        const BvhNode &n = nodes[ni];
         if (n.count > 0) {
             for (uint32_t i = n.left_or_first; i < n.left_or_first + n.count; ++i) {
                 float u, v, t;
@@ -354,8 +363,15 @@ inline bool Scene::traverse(const Ray &r, float mint, float maxt, bool any, floa
                 }
             }
         } else {
-            stack[sp++] = n.left_or_first + 1;
-            stack[sp++] = n.left_or_first;
+            const uint32_t c0 = n.left_or_first, c1 = n.left_or_first + 1;
+            const float t0 = enter(nodes[c0]), t1 = enter(nodes[c1]);
+            if (t0 <= t1) {
+                if (t1 < kInf) stack.push_back({c1, t1});
+                if (t0 < kInf) stack.push_back({c0, t0});
+            } else {
+                if (t0 < kInf) stack.push_back({c0, t0});
+                if (t1 < kInf) stack.push_back({c1, t1});
+            }
         }
     }
     return hit;
