@@ -254,6 +254,21 @@ def test_guided_training_parity(pg, O, scenes):
     assert abs(m1.mean() - m2.mean()) / m2.mean() < 0.01
 
 
+def test_image_parity_kitchen_unguided(pg, O):
+    """C4 kitchen class (~1 M triangles, 5 area emitters, plastic / rough conductor / glass
+    clutter) at a small resolution: per-pixel z-test and image mean against the oracle."""
+    sc = pg.scenes.kitchen(96, 54)
+    spp = 64
+    dev = make_dev(pg, sc)
+    dev.render_pass(spp, 0)
+    g = dev.read_film()
+    dev.close()
+    c = O.render(O.OracleScene(pg.capi, sc), pg.capi.default_config(), spp)[:2]
+    m1, m2, z = _zstats(g, c)
+    assert (np.abs(z) < 5).mean() > 0.999
+    assert abs(m1.mean() - m2.mean()) / m2.mean() < 5e-3
+
+
 def test_image_parity_roughplastic(pg, O):
     """roughplastic blocks (GGX and Beckmann) in the Cornell box: unguided GPU vs oracle per-pixel
     z-test, then the guided GPU image against the same unguided oracle (guiding is unbiased).  The
