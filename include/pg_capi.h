@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 3
+#define PG_ABI_VERSION 4
 
 typedef int32_t pg_status;
 enum {
@@ -58,7 +58,8 @@ enum {
     PG_BSDF_ROUGHDIELECTRIC = 4,  /* src/bsdfs/roughdielectric.cpp  */
     PG_BSDF_PLASTIC = 5,          /* src/bsdfs/plastic.cpp          */
     PG_BSDF_ROUGHPLASTIC = 6,     /* src/bsdfs/roughplastic.cpp     */
-    PG_BSDF_COUNT = 7
+    PG_BSDF_NULL = 7,             /* src/bsdfs/null.cpp: index-matched medium boundary */
+    PG_BSDF_COUNT = 8
 };
 /* Microfacet distributions (src/bsdfs/microfacet.h:48-58). */
 enum { PG_DIST_BECKMANN = 0, PG_DIST_GGX = 1 };
@@ -89,8 +90,28 @@ typedef struct pg_shape {
     uint32_t tri_begin;
     uint32_t tri_count;
     uint32_t material;
-    int32_t emitter; /* index into emitters, or -1 */
+    int32_t emitter;          /* index into emitters, or -1 */
+    int32_t interior_medium;  /* Shape::getInteriorMedium (shape.h), index into media or -1 */
+    int32_t exterior_medium;  /* Shape::getExteriorMedium; the side is the geometric normal's */
 } pg_shape;
+
+/* Participating medium (volpath integrator only).  PG_MEDIUM_HETEROGENEOUS is
+ * src/medium/heterogeneous.cpp with Woodcock tracking (the default 'method'): a float32 density
+ * grid (src/volume/gridvolume.cpp, trilinear, the data AABB mapped onto [0, res-1]^3, zero outside),
+ * density multiplier 'scale', constant albedo (constvolume) and a Henyey-Greenstein phase function
+ * (src/phase/hg.cpp).  Densities must lie in [0, 1] (heterogeneous.cpp:236-239). */
+enum { PG_MEDIUM_HETEROGENEOUS = 0 };
+typedef struct pg_medium {
+    uint32_t type;
+    uint32_t res[3];
+    const float *density;  /* res[0] * res[1] * res[2], x fastest; copied at upload */
+    float aabb_min[3];
+    float aabb_max[3];
+    float scale;
+    float albedo[3];
+    float g;               /* HG mean cosine */
+    uint32_t pad0;
+} pg_medium;
 
 /* Area emitter attached to a shape (src/emitters/area.cpp:158-183).  Sampling weight 1, so the
  * scene picks emitters uniformly (Scene::sampleEmitterDirect, src/librender/scene.cpp:871-895). */
@@ -120,7 +141,7 @@ typedef struct pg_scene_desc {
     uint32_t num_shapes;
     uint32_t num_materials;
     uint32_t num_emitters;
-    uint32_t pad0;
+    uint32_t num_media;
     const float *positions;     /* 3 * num_vertices */
     const float *normals;       /* 3 * num_vertices, or NULL (face normals) */
     const uint32_t *indices;    /* 3 * num_triangles */
@@ -128,6 +149,9 @@ typedef struct pg_scene_desc {
     const pg_material *materials;
     const pg_emitter *emitters;
     pg_camera camera;
+    const pg_medium *media;     /* num_media entries (may be NULL when 0) */
+    int32_t camera_medium;      /* Sensor::getMedium, index into media or -1 */
+    int32_t pad1;
 } pg_scene_desc;
 
 /* Integrator parameters (MonteCarloIntegrator props: src/librender/integrator.cpp:195-230;
@@ -154,7 +178,10 @@ typedef struct pg_config {
     uint32_t max_paths_in_flight; /* 0 = auto */
     int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024) */
     int32_t path_lanes;           /* path chunks in flight on separate streams, 1..4 (0 = auto: 3) */
+    int32_t integrator;           /* PG_INTEGRATOR_PATH (progressive_path) or _VOLPATH (progressive_volpath) */
+    int32_t pad1;
 } pg_config;
+enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
 
 /* Training record written per non-delta path vertex (SoA-free 32-byte AoS). */
 typedef struct pg_record {
@@ -179,6 +206,8 @@ typedef struct pg_stats {
     uint64_t stree_nodes;
     uint64_t dtree_nodes;
     uint64_t shade_launches;  /* material-class shading launches */
+    double volume_ms;         /* device time of the volumetric path kernel (integrator = volpath) */
+    uint64_t volume_launches;
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */
@@ -234,6 +263,17 @@ pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hi
  * wo_given: n x 3 local directions for the eval/pdf part (may be NULL). */
 pg_status pg_bsdf_query(void *ctx, uint32_t material, const float *wi, const float *u,
                         const float *wo_given, uint64_t n, float *out);
+/* HG phase function of medium `medium` on the device (HGPhaseFunction::sample / eval, hg.cpp:74-106).
+ * in: n x 5 (wi.xyz pointing back along the incident ray, 2D sample); out: n x 5 floats
+ * wo.xyz, pdf, eval(wi, wo_given) (0 when wo_given is NULL). */
+pg_status pg_phase_query(void *ctx, uint32_t medium, const float *in, const float *wo_given, uint64_t n, float *out);
+/* Medium queries on the device for medium `medium` (heterogeneous.cpp:546-660, gridvolume.cpp:337-380).
+ * op 0 (density): in n x 3 world points; out n floats = lookupFloat(p) (unscaled).
+ * op 1 (free flight) / op 2 (transmittance): in n x 8 rays (o.xyz, mint, d.xyz, maxt) and keys n x 2
+ * (rng key, sample): the draws are dimensions 1, 2, ... of that counter stream.  out n x 4:
+ * op 1: (interaction 1/0, t, draws used, 0), op 2: (transmittance estimate, draws used, 0, 0). */
+pg_status pg_medium_query(void *ctx, uint32_t medium, int32_t op, const float *in, const uint32_t *keys, uint64_t n,
+                          float *out);
 
 /* Rough dielectric transmittance slice of a roughplastic material, as RoughPlastic::configure
  * reduces it (roughplastic.cpp:283-299, src/bsdfs/rtrans.h setEta/setAlpha/evalDiffuse):

@@ -12,7 +12,9 @@ LIB_PATH = os.path.join(_HERE, "build", "libpgamd.so")
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, PG_ERR_NO_DEVICE = range(7)
 (PG_BSDF_DIFFUSE, PG_BSDF_CONDUCTOR, PG_BSDF_ROUGHCONDUCTOR, PG_BSDF_DIELECTRIC, PG_BSDF_ROUGHDIELECTRIC,
- PG_BSDF_PLASTIC, PG_BSDF_ROUGHPLASTIC) = range(7)
+ PG_BSDF_PLASTIC, PG_BSDF_ROUGHPLASTIC, PG_BSDF_NULL) = range(8)
+PG_MEDIUM_HETEROGENEOUS = 0
+PG_INTEGRATOR_PATH, PG_INTEGRATOR_VOLPATH = 0, 1
 PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
 PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
 
@@ -34,7 +36,17 @@ class pg_material(C.Structure):
 
 
 class pg_shape(C.Structure):
-    _fields_ = [("tri_begin", C.c_uint32), ("tri_count", C.c_uint32), ("material", C.c_uint32), ("emitter", C.c_int32)]
+    _fields_ = [("tri_begin", C.c_uint32), ("tri_count", C.c_uint32), ("material", C.c_uint32), ("emitter", C.c_int32),
+                ("interior_medium", C.c_int32), ("exterior_medium", C.c_int32)]
+
+    def __init__(self, tri_begin=0, tri_count=0, material=0, emitter=-1, interior_medium=-1, exterior_medium=-1):
+        super().__init__(tri_begin, tri_count, material, emitter, interior_medium, exterior_medium)
+
+
+class pg_medium(C.Structure):
+    _fields_ = [("type", C.c_uint32), ("res", C.c_uint32 * 3), ("density", C.POINTER(C.c_float)),
+                ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("scale", C.c_float),
+                ("albedo", C.c_float * 3), ("g", C.c_float), ("pad0", C.c_uint32)]
 
 
 class pg_emitter(C.Structure):
@@ -49,11 +61,12 @@ class pg_camera(C.Structure):
 
 class pg_scene_desc(C.Structure):
     _fields_ = [("num_vertices", C.c_uint32), ("num_triangles", C.c_uint32), ("num_shapes", C.c_uint32),
-                ("num_materials", C.c_uint32), ("num_emitters", C.c_uint32), ("pad0", C.c_uint32),
+                ("num_materials", C.c_uint32), ("num_emitters", C.c_uint32), ("num_media", C.c_uint32),
                 ("positions", C.POINTER(C.c_float)), ("normals", C.POINTER(C.c_float)),
                 ("indices", C.POINTER(C.c_uint32)), ("shapes", C.POINTER(pg_shape)),
                 ("materials", C.POINTER(pg_material)), ("emitters", C.POINTER(pg_emitter)),
-                ("camera", pg_camera)]
+                ("camera", pg_camera), ("media", C.POINTER(pg_medium)), ("camera_medium", C.c_int32),
+                ("pad1", C.c_int32)]
 
 
 class pg_config(C.Structure):
@@ -63,7 +76,7 @@ class pg_config(C.Structure):
                 ("s_tree_threshold", C.c_float), ("d_tree_threshold", C.c_float), ("d_tree_max_depth", C.c_int32),
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
-                ("path_lanes", C.c_int32)]
+                ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("pad1", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -75,7 +88,7 @@ class pg_stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("records", C.c_uint64),
                 ("trace_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double), ("other_ms", C.c_double),
                 ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
-                ("shade_launches", C.c_uint64)]
+                ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -101,6 +114,7 @@ def default_config(**overrides):
     c.max_paths_in_flight = 0
     c.gpu_depth_cap = 1024
     c.path_lanes = 0
+    c.integrator = PG_INTEGRATOR_PATH
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")
@@ -134,14 +148,20 @@ SIGNATURES = [
     ("pg_local_pixel_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
     ("pg_trace_rays", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_bsdf_query", C.c_int32, [VP, C.c_uint32, VP, VP, VP, C.c_uint64, VP]),
+    ("pg_phase_query", C.c_int32, [VP, C.c_uint32, VP, VP, C.c_uint64, VP]),
+    ("pg_medium_query", C.c_int32, [VP, C.c_uint32, C.c_int32, VP, VP, C.c_uint64, VP]),
     ("pg_rough_transmittance", C.c_int32, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
     ("pg_get_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_put_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32]),
 ]
 
 
+PG_ABI_VERSION = 4  # include/pg_capi.h
+
+
 def load_library(path=None):
-    """Load libpgamd.so and attach prototypes.  Raises if it is missing (no fallback path)."""
+    """Load libpgamd.so and attach prototypes.  Raises if it is missing or built against another
+    ABI version (no fallback path)."""
     path = path or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"HIP extension {path} is missing: run __graft_entry__.build() (no CPU fallback exists)")
@@ -150,4 +170,6 @@ def load_library(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.pg_abi_version() != PG_ABI_VERSION:
+        raise RuntimeError(f"{path} has ABI {lib.pg_abi_version()}, this package needs {PG_ABI_VERSION}: rebuild it")
     return lib

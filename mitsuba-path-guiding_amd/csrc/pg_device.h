@@ -341,8 +341,8 @@ enum : uint32_t {
     EGlossyTransmission = 0x10, EDeltaReflection = 0x20, EDeltaTransmission = 0x40,
     EFrontSide = 0x8000, EBackSide = 0x10000,
     ESmooth = EDiffuseReflection | EDiffuseTransmission | EGlossyReflection | EGlossyTransmission,
-    EDelta = EDeltaReflection | EDeltaTransmission,
-    ETransmission = EDiffuseTransmission | EGlossyTransmission | EDeltaTransmission,
+    EDelta = ENull | EDeltaReflection | EDeltaTransmission,                            // bsdf.h:280
+    ETransmission = EDiffuseTransmission | EGlossyTransmission | EDeltaTransmission | ENull,  // bsdf.h:270-272
 };
 
 struct BS {
@@ -507,6 +507,13 @@ PGD float bsdfPdf1(const GMat &M, f3 wi, f3 wo) {
 template <int MODEL = -1>
 PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
     switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
+        case PG_BSDF_NULL: {  // null.cpp:64-75 (eval/pdf of the continuous measures are 0)
+            bs.wo = -wi;
+            bs.eta = 1.0f;
+            bs.type = ENull;
+            bs.pdf = 1.0f;
+            return mk1(1.0f);
+        }
         case PG_BSDF_DIFFUSE: {  // diffuse.cpp:139-153
             if (wi.z <= 0) return mk1(0.f);
             bs.wo = squareToCosineHemisphere(u0, u1);

@@ -130,6 +130,12 @@ struct Ctx {
     bool has_scene = false;
     GParams g{};
     DevBuf nodes, woop, wnodes, wwoop, tshade, tclass, mats, rtab, ems, emtri, emcdf;
+    // media (volpath)
+    DevBuf media, density, tmed;
+    int32_t cam_medium = -1;
+    uint32_t num_media = 0;
+    DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
+    uint32_t vol_cap = 0;
     uint32_t num_tris = 0, num_mats = 0;
     std::vector<GMat> host_mats;
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
@@ -234,6 +240,7 @@ GMat makeGMat(const pg_material &m) {
             g.specWeight = sAvg / (dAvg + sAvg);
             break;
         }
+        case PG_BSDF_NULL: g.type = 0x1; sides |= 0x10000u; break;  // ENull, both sides (null.cpp:40)
         case PG_BSDF_ROUGHPLASTIC: {  // roughplastic.cpp:258-307; table + fdrInt set by the caller
             g.type = 0x8 | 0x2;         // EGlossyReflection | EDiffuseReflection
             float dAvg = luminance(m.diffuse_reflectance), sAvg = luminance(m.specular_reflectance);
@@ -431,6 +438,31 @@ extern "C" {
 
 int32_t pg_abi_version(void) { return PG_ABI_VERSION; }
 
+// HeterogeneousMedium / GridDataSource preconditions (heterogeneous.cpp:227-242: densities in
+// [0, 1]; hg.cpp:47-50: |g| < 1).  The optical-depth bound keeps one Woodcock walk across the
+// grid box below ~1e7 steps (the reference has no bound; a thicker medium is rejected).
+pg_status validateMedium(Ctx *c, const pg_medium &pm, uint32_t m) {
+    const std::string id = "pg_upload_scene: medium " + std::to_string(m) + ": ";
+    if (pm.type != PG_MEDIUM_HETEROGENEOUS) return fail(c, PG_ERR_INVALID, id + "unknown type");
+    if (!pm.density || pm.res[0] < 1 || pm.res[1] < 1 || pm.res[2] < 1 ||
+        (uint64_t)pm.res[0] * pm.res[1] * pm.res[2] > (1ull << 32))
+        return fail(c, PG_ERR_INVALID, id + "bad density grid");
+    double diag2 = 0;
+    for (int a = 0; a < 3; ++a) {
+        if (!(pm.aabb_max[a] > pm.aabb_min[a]) || !std::isfinite(pm.aabb_min[a]) || !std::isfinite(pm.aabb_max[a]))
+            return fail(c, PG_ERR_INVALID, id + "empty or non-finite AABB");
+        diag2 += (double)(pm.aabb_max[a] - pm.aabb_min[a]) * (pm.aabb_max[a] - pm.aabb_min[a]);
+        if (!(pm.albedo[a] >= 0) || !std::isfinite(pm.albedo[a])) return fail(c, PG_ERR_INVALID, id + "bad albedo");
+    }
+    if (!(pm.scale > 0) || !std::isfinite(pm.scale)) return fail(c, PG_ERR_INVALID, id + "scale must be finite and > 0");
+    if (pm.scale * std::sqrt(diag2) > 1e7) return fail(c, PG_ERR_INVALID, id + "optical depth too large");
+    if (!(pm.g > -1 && pm.g < 1)) return fail(c, PG_ERR_INVALID, id + "HG g must lie in (-1, 1)");
+    const size_t n = (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+    for (size_t i = 0; i < n; ++i)
+        if (!(pm.density[i] >= 0.0f && pm.density[i] <= 1.0f)) return fail(c, PG_ERR_INVALID, id + "density outside [0, 1]");
+    return PG_OK;
+}
+
 pg_status pg_config_default(pg_config *c) {
     if (!c) return PG_ERR_INVALID;
     std::memset(c, 0, sizeof *c);
@@ -454,6 +486,7 @@ pg_status pg_config_default(pg_config *c) {
     c->max_paths_in_flight = 0;
     c->gpu_depth_cap = 1024;
     c->path_lanes = 0;
+    c->integrator = PG_INTEGRATOR_PATH;
     return PG_OK;
 }
 
@@ -485,6 +518,14 @@ pg_status pg_create(const pg_config *cfg, void **out) {
         return fail(nullptr, PG_ERR_INVALID, "pg_create: path_lanes must be 0..4");
     }
     c->nlanes = c->cfg.path_lanes ? c->cfg.path_lanes : PG_DEFAULT_LANES;
+    if (c->cfg.integrator != PG_INTEGRATOR_PATH && c->cfg.integrator != PG_INTEGRATOR_VOLPATH) {
+        delete c;
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown integrator");
+    }
+    if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH && c->cfg.guiding) {
+        delete c;
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: guiding is not available with the volpath integrator");
+    }
     if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->film_order, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->pass_start, hipEventDisableTiming) != hipSuccess) {
@@ -538,14 +579,46 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     const uint32_t nt = d->num_triangles;
     for (uint64_t i = 0; i < 3ull * nt; ++i)
         if (d->indices[i] >= d->num_vertices) return fail(c, PG_ERR_INVALID, "pg_upload_scene: index out of range");
-    if (d->num_materials > 65535 || d->num_emitters > 65534)
-        return fail(c, PG_ERR_INVALID, "pg_upload_scene: too many materials/emitters");
+    if (d->num_materials > 65535 || d->num_emitters > 65534 || d->num_media > 65534)
+        return fail(c, PG_ERR_INVALID, "pg_upload_scene: too many materials/emitters/media");
+    for (uint32_t m = 0; m < d->num_materials; ++m)
+        if (d->materials[m].type >= PG_BSDF_COUNT || d->materials[m].distribution > PG_DIST_GGX)
+            return fail(c, PG_ERR_INVALID, "pg_upload_scene: bad material type");
+    if (d->num_media && !d->media) return fail(c, PG_ERR_INVALID, "pg_upload_scene: media missing");
+    if (d->camera_medium < -1 || d->camera_medium >= (int32_t)d->num_media)
+        return fail(c, PG_ERR_INVALID, "pg_upload_scene: bad camera medium");
+    std::vector<GMedium> gmed;
+    std::vector<size_t> denOff;
+    size_t denTotal = 0;
+    for (uint32_t m = 0; m < d->num_media; ++m) {
+        const pg_medium &pm = d->media[m];
+        if (pg_status vs = validateMedium(c, pm, m)) return vs;
+        GMedium gm{};
+        gm.resx = pm.res[0];
+        gm.resy = pm.res[1];
+        gm.resz = pm.res[2];
+        gm.scale = pm.scale;
+        gm.invMax = 1.0f / (pm.scale * 1.0f);  // maxDensity = scale * getMaximumFloatValue() = scale
+        gm.g = pm.g;
+        for (int a = 0; a < 3; ++a) {
+            gm.lo[a] = pm.aabb_min[a];
+            gm.hi[a] = pm.aabb_max[a];
+            gm.gs[a] = (float)(pm.res[a] - 1) / (pm.aabb_max[a] - pm.aabb_min[a]);
+            gm.go[a] = gm.gs[a] * -pm.aabb_min[a];
+            gm.albedo[a] = pm.albedo[a];
+        }
+        denOff.push_back(denTotal);
+        denTotal += (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+        gmed.push_back(gm);
+    }
     // per-triangle (material | emitter+1 << 16) from the shape partition
     std::vector<uint32_t> triBits(nt, 0xFFFFFFFFu);
     for (uint32_t s = 0; s < d->num_shapes; ++s) {
         const pg_shape &sh = d->shapes[s];
         if ((uint64_t)sh.tri_begin + sh.tri_count > nt || sh.material >= d->num_materials ||
-            (sh.emitter >= 0 && (uint32_t)sh.emitter >= d->num_emitters))
+            (sh.emitter >= 0 && (uint32_t)sh.emitter >= d->num_emitters) || sh.interior_medium < -1 ||
+            sh.interior_medium >= (int32_t)d->num_media || sh.exterior_medium < -1 ||
+            sh.exterior_medium >= (int32_t)d->num_media)
             return fail(c, PG_ERR_INVALID, "pg_upload_scene: bad shape");
         uint32_t bits = sh.material | ((uint32_t)(sh.emitter + 1) << 16);
         for (uint32_t t = 0; t < sh.tri_count; ++t) triBits[sh.tri_begin + t] = bits;
@@ -562,6 +635,17 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         uint32_t t = bvh.order[k];
         packShade(&shade[20 * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
         tclass[k] = (uint8_t)materialClass(d->materials[triBits[t] & 0xFFFFu].type);
+    }
+    // per BVH-order triangle: the shape's medium transition, (interior + 1) | (exterior + 1) << 16
+    std::vector<uint32_t> tmed(nt, 0);
+    {
+        std::vector<uint32_t> shapeMed(nt, 0);
+        for (uint32_t sidx = 0; sidx < d->num_shapes; ++sidx) {
+            const pg_shape &sh = d->shapes[sidx];
+            const uint32_t bits = (uint32_t)(sh.interior_medium + 1) | ((uint32_t)(sh.exterior_medium + 1) << 16);
+            for (uint32_t t = 0; t < sh.tri_count; ++t) shapeMed[sh.tri_begin + t] = bits;
+        }
+        for (uint32_t k = 0; k < nt; ++k) tmed[k] = shapeMed[bvh.order[k]];
     }
     // emitters: compact triangle array + area CDF (double accumulation of fp32 areas)
     std::vector<GEmitter> ems;
@@ -625,8 +709,28 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->wwoop, bvh.wwoop)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||
         (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||
-        (s = upload(c, c->emcdf, emcdf)))
+        (s = upload(c, c->emcdf, emcdf)) || (s = upload(c, c->tmed, tmed)))
         return s;
+    // densities: one buffer, each grid 256-B aligned
+    {
+        size_t words = 0;
+        std::vector<size_t> at;
+        for (uint32_t m = 0; m < d->num_media; ++m) {
+            at.push_back(words);
+            words += ((size_t)d->media[m].res[0] * d->media[m].res[1] * d->media[m].res[2] + 63) & ~(size_t)63;
+        }
+        HIPC(c, c->density.grow(std::max<size_t>(words * 4, 256)));
+        for (uint32_t m = 0; m < d->num_media; ++m) {
+            const size_t n = (size_t)d->media[m].res[0] * d->media[m].res[1] * d->media[m].res[2];
+            HIPC(c, hipMemcpyAsync(c->density.as<float>() + at[m], d->media[m].density, n * 4, hipMemcpyHostToDevice,
+                                   c->stream));
+            gmed[m].density = c->density.as<float>() + at[m];
+        }
+        HIPC(c, hipStreamSynchronize(c->stream));  // the host density arrays are caller-owned
+        if ((s = upload(c, c->media, gmed))) return s;
+        c->num_media = d->num_media;
+        c->cam_medium = d->camera_medium;
+    }
 
     // camera (Transform::lookAt, transform.cpp:191-214) and integrator constants
     GParams &g = c->g;
@@ -693,6 +797,76 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     return PG_OK;
 }
 
+// progressive_volpath: chunks of (pixel, sample) items through k_volpath, films in chunk order
+pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
+    const uint32_t npix = (uint32_t)c->local_pixels.size();
+    const uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
+    const uint32_t want = (uint32_t)std::min<uint64_t>((uint64_t)npix * spp, cap);
+    if (c->vol_cap < want) {
+        HIPC(c, c->vol_rad.alloc((size_t)want * 16));
+        c->vol_cap = want;
+    }
+    if (!c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
+    if (!c->vol_work.p) HIPC(c, c->vol_work.alloc(64));
+    HIPC(c, hipMemsetAsync(c->vol_work.p, 0, 64, c->stream));
+    GParams g = c->g;
+    g.max_depth = c->cfg.max_depth;
+    g.rr_depth = c->cfg.rr_depth;
+    g.use_nee = c->cfg.use_nee;
+    g.hide_emitters = c->cfg.hide_emitters;
+    g.strict_normals = c->cfg.strict_normals;
+    g.max_component_value = c->cfg.max_component_value;
+    g.seed = c->cfg.seed;
+    g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
+    const SceneDev sc = sceneView(c);
+    VolDev v{};
+    v.media = c->media.as<GMedium>();
+    v.tmed = c->tmed.as<uint32_t>();
+    v.cam_medium = c->cam_medium;
+    v.num_media = c->num_media;
+    v.rad = c->vol_rad.as<float4>();
+    v.next = c->vol_work.as<uint32_t>();
+    v.stats = (unsigned long long *)(c->vol_work.as<uint8_t>() + 16);
+    v.stack_ovf = c->vol_ovf.as<uint32_t>();
+    PathDev pv{};
+    pv.rad = v.rad;
+    const uint32_t layersPer = std::max<uint32_t>(1, want / npix), pixPer = std::min(npix, want);
+    std::vector<EventPair> evs;
+    for (uint32_t layer = 0; layer < spp;) {
+        const uint32_t nl = npix > want ? 1 : std::min(layersPer, spp - layer);
+        for (uint32_t pb = 0; pb < npix; pb += pixPer) {
+            if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+            const uint32_t np = std::min(pixPer, npix - pb);
+            EventPair e;
+            HIPC(c, hipEventCreate(&e.a));
+            HIPC(c, hipEventCreate(&e.b));
+            evs.push_back(e);
+            HIPC(c, hipEventRecord(e.a, c->stream));
+            pg_launch_volpath(c->stream, g, sc, v, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + layer);
+            HIPC(c, hipEventRecord(e.b, c->stream));
+            pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
+                           c->film_sq.as<float4>());
+            HIPC(c, hipGetLastError());
+            c->stats.paths += (uint64_t)np * nl;
+        }
+        layer += nl;
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    unsigned long long st[2];
+    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 16, hipMemcpyDeviceToHost));
+    c->stats.segments += st[0];
+    c->stats.shadow_rays += st[1];
+    for (EventPair &e : evs) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e.a, e.b);
+        c->stats.volume_ms += ms;
+        c->stats.volume_launches++;
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    return PG_OK;
+}
+
 pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_t record) {
     Ctx *c = (Ctx *)ctx;
     if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_render_pass: null context");
@@ -701,6 +875,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     HIPC(c, hipSetDevice(c->cfg.device));
     const uint32_t npix = (uint32_t)c->local_pixels.size();
     if (npix == 0 || spp == 0) return PG_OK;
+    if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH) return renderVolpath(c, spp, sample_offset);
     const bool rec = record && c->cfg.guiding;
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
     uint64_t total = (uint64_t)npix * spp;
@@ -1186,6 +1361,56 @@ pg_status pg_bsdf_query(void *ctx, uint32_t material, const float *wi, const flo
                          wo_given ? g.as<float>() : nullptr, (uint32_t)n, o.as<float>());
     HIPC(c, hipGetLastError());
     HIPC(c, hipMemcpyAsync(out, o.p, n * 48, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_phase_query(void *ctx, uint32_t medium, const float *in, const float *wo_given, uint64_t n, float *out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!in && n) || (!out && n)) return fail(c, PG_ERR_INVALID, "pg_phase_query: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_phase_query: no scene");
+    if (medium >= c->num_media) return fail(c, PG_ERR_INVALID, "pg_phase_query: bad medium");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!n) return PG_OK;
+    DevBuf a, g, o;
+    HIPC(c, a.alloc(n * 20));
+    HIPC(c, o.alloc(n * 20));
+    HIPC(c, hipMemcpyAsync(a.p, in, n * 20, hipMemcpyHostToDevice, c->stream));
+    if (wo_given) {
+        HIPC(c, g.alloc(n * 12));
+        HIPC(c, hipMemcpyAsync(g.p, wo_given, n * 12, hipMemcpyHostToDevice, c->stream));
+    }
+    pg_launch_phase_query(c->stream, c->media.as<GMedium>() + medium, a.as<float>(), wo_given ? g.as<float>() : nullptr,
+                          (uint32_t)n, o.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(out, o.p, n * 20, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_medium_query(void *ctx, uint32_t medium, int32_t op, const float *in, const uint32_t *keys, uint64_t n,
+                          float *out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!in && n) || (!out && n) || (op != 0 && !keys && n))
+        return fail(c, PG_ERR_INVALID, "pg_medium_query: null argument");
+    if (op < 0 || op > 2) return fail(c, PG_ERR_INVALID, "pg_medium_query: bad op");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_medium_query: no scene");
+    if (medium >= c->num_media) return fail(c, PG_ERR_INVALID, "pg_medium_query: bad medium");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!n) return PG_OK;
+    const size_t inBytes = n * (op == 0 ? 12 : 32), outBytes = n * (op == 0 ? 4 : 16);
+    DevBuf a, k, o;
+    HIPC(c, a.alloc(inBytes));
+    HIPC(c, o.alloc(outBytes));
+    HIPC(c, hipMemcpyAsync(a.p, in, inBytes, hipMemcpyHostToDevice, c->stream));
+    if (op != 0) {
+        HIPC(c, k.alloc(n * 8));
+        HIPC(c, hipMemcpyAsync(k.p, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    pg_launch_medium_query(c->stream, c->media.as<GMedium>() + medium, op, a.as<float>(),
+                           op != 0 ? k.as<uint32_t>() : nullptr, (uint32_t)n, o.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(out, o.p, outBytes, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }

@@ -42,6 +42,18 @@ struct SDDev {
     int built;
 };
 
+// Volumetric path tracing (pg_config.integrator == PG_INTEGRATOR_VOLPATH)
+struct VolDev {
+    const GMedium *media;
+    const uint32_t *tmed;      // per BVH-order triangle: (interior + 1) | (exterior + 1) << 16, 0 = no transition
+    int32_t cam_medium;        // -1: none
+    uint32_t num_media;
+    float4 *rad;               // per work item (layer-major: item = layer * npix + lp), radiance
+    uint32_t *next;            // work counter (zeroed by the launcher)
+    unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries
+    uint32_t *stack_ovf;       // pg_stack_overflow_words(0) words
+};
+
 // Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).
 // Appends are wave-aggregated atomics on the shard's own counter: one counter per queue serialized
 // every append of the chip (58k returning atomics on one address: 658 us; on 64 addresses: 18 us,
@@ -76,6 +88,14 @@ void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uin
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
                       unsigned long long *rec_count, unsigned long long rec_capacity);
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n);
+// one volpath sample per (pixel, layer) item of the chunk, written to v.rad[item]
+void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v,
+                       const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
+                       uint32_t sample_base);
+void pg_launch_phase_query(hipStream_t s, const GMedium *medium, const float *in, const float *wog, uint32_t n,
+                           float *out);
+void pg_launch_medium_query(hipStream_t s, const GMedium *medium, int op, const float *in, const uint32_t *keys,
+                            uint32_t n, float *out);
 void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits,
                           uint32_t *ovf);
 // words of traversal-stack overflow storage for a launch of max_threads (0 = persistent grid)

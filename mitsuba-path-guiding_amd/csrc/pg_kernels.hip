@@ -6,387 +6,9 @@
 // training-vertex write, queue compaction by wave ballot) -> shadow (any hit; adds the NEE
 // contribution).  Camera rays, film accumulation, record commit and SD-tree splat are separate
 // kernels.  Path state is SoA float4/uint4 arrays indexed by path slot.
-#include "pg_device.h"
-#include "pg_kernels.h"
-
 #include <algorithm>
 
-using namespace pgd;
-
-#define TRACE_BLOCK 128
-#define STACK_DEPTH 48  // total traversal stack entries (the BVH builder bounds the depth below this)
-#define LDS_STACK 16    // binary BVH: top entries in LDS (4 B each: 8 KiB per block), deeper ones spill
-#define WIDE_LDS_STACK 8  // wide BVH: top group entries in LDS (8 B each: 8 KiB per block)
-#define SHADE_BLOCK 256
-// persistent grid-stride launches: enough blocks to fill 256 CUs at full occupancy
-#define TRACE_MAX_BLOCKS (256 * 16)
-
-namespace {
-
-// ---------------------------------------------------------------------------------------------
-// BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,
-// sahkdtree3.h:178-308) with the same contract: closest t in [tmin, tmax] (any hit for shadow
-// rays).  Closest-hit rays walk the binary BVH (64-B nodes), shadow rays the 8-wide BVH with
-// quantised boxes (80-B nodes); both test 48-B Woop unit triangles.
-// Stacks: entries [0, LDS) in LDS (columns per thread, stride TRACE_BLOCK: conflict-free), deeper
-// entries in a per-thread column of a global overflow ring (stride = launched threads).
-struct TStack {
-    uint32_t *lds;
-    uint32_t *ovf;
-    uint32_t ostride;
-    __device__ __forceinline__ void put(int i, uint32_t v) const {
-        if (i < LDS_STACK) lds[i * TRACE_BLOCK] = v;
-        else ovf[(size_t)(i - LDS_STACK) * ostride] = v;
-    }
-    __device__ __forceinline__ uint32_t get(int i) const {
-        return i < LDS_STACK ? lds[i * TRACE_BLOCK] : ovf[(size_t)(i - LDS_STACK) * ostride];
-    }
-};
-// group entries (base index, hit mask) of the wide traversal
-struct WStack {
-    uint32_t *lds;
-    uint32_t *ovf;
-    uint32_t ostride;
-    __device__ __forceinline__ void put(int i, uint2 v) const {
-        if (i < WIDE_LDS_STACK) {
-            lds[(2 * i) * TRACE_BLOCK] = v.x;
-            lds[(2 * i + 1) * TRACE_BLOCK] = v.y;
-        } else {
-            ovf[(size_t)(2 * (i - WIDE_LDS_STACK)) * ostride] = v.x;
-            ovf[(size_t)(2 * (i - WIDE_LDS_STACK) + 1) * ostride] = v.y;
-        }
-    }
-    __device__ __forceinline__ uint2 get(int i) const {
-        if (i < WIDE_LDS_STACK) return make_uint2(lds[(2 * i) * TRACE_BLOCK], lds[(2 * i + 1) * TRACE_BLOCK]);
-        return make_uint2(ovf[(size_t)(2 * (i - WIDE_LDS_STACK)) * ostride],
-                          ovf[(size_t)(2 * (i - WIDE_LDS_STACK) + 1) * ostride]);
-    }
-};
-
-// Woop unit-triangle test (closest hit: a hit at t <= tmax replaces the current one)
-__device__ __forceinline__ bool woopHit(const float4 *__restrict__ woop, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
-                                        float &tt, float &bu, float &bv) {
-    const float4 w0 = woop[3 * tr + 0];
-    float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
-    float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-    tt = oz / dz;
-    if (!(tt >= tmin && tt <= tmax)) return false;
-    const float4 w1 = woop[3 * tr + 1];
-    float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
-    if (!(a >= 0.0f && a <= 1.0f)) return false;
-    const float4 w2 = woop[3 * tr + 2];
-    float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
-    if (!(b >= 0.0f && a + b <= 1.0f)) return false;
-    bu = b;             // weight of p1
-    bv = 1.0f - a - b;  // weight of p2
-    return true;
-}
-
-__device__ __forceinline__ float qbyte(uint32_t lo, uint32_t hi, int s) {
-    return (float)(((s < 4 ? lo : hi) >> (8 * (s & 3))) & 0xFFu);
-}
-__device__ __forceinline__ float max3f(float a, float b, float c) {
-    float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ __forceinline__ float min3f(float a, float b, float c) {
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-// bit s of m moves to bit s ^ x (x < 8): three conditional swaps of bit groups
-__device__ __forceinline__ uint32_t permuteXor8(uint32_t m, uint32_t x) {
-    if (x & 1u) m = ((m & 0x55u) << 1) | ((m >> 1) & 0x55u);
-    if (x & 2u) m = ((m & 0x33u) << 2) | ((m >> 2) & 0x33u);
-    if (x & 4u) m = ((m & 0x0Fu) << 4) | ((m >> 4) & 0x0Fu);
-    return m;
-}
-
-// Traversal of the 8-wide BVH (after Ylitie, Karras & Laine 2017): the current node group
-// G = (child_base, hit bits 24..31 in octant order | imask bits 0..7) and triangle group
-// T = (tri_base, hit bits 0..23); one node is opened per step, its remaining siblings stay on the
-// stack as one group entry.  (Postponing triangle groups while few lanes have triangle work, as
-// in the paper, measured slower here: 20.0 vs 17.4 ms per pass.)
-template <bool ANY>
-__device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o,
-                                             f3 d, float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                             const WStack &stk) {
-    const float eps = 1e-30f;
-    const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
-                       1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-                       1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
-    // 7 - octant: bit a set where the direction is non-negative along axis a
-    const uint32_t octinv = (d.x < 0 ? 0u : 1u) | (d.y < 0 ? 0u : 2u) | (d.z < 0 ? 0u : 4u);
-    uint2 G = make_uint2(0u, 0x80000000u);  // the root, as a one-node group
-    uint2 T = make_uint2(0u, 0u);
-    int sp = 0;
-    bool found = false;
-    for (;;) {
-        if (G.y > 0x00FFFFFFu) {
-            const int bit = 31 - __clz(G.y);
-            const uint32_t slot = (uint32_t)(bit - 24) ^ octinv;
-            const uint32_t ni = G.x + __popc(G.y & 0xFFu & ((1u << slot) - 1u));
-            G.y &= ~(1u << bit);
-            if (G.y > 0x00FFFFFFu) stk.put(sp++, G);
-            const float4 n0 = nodes[PG_WIDE_NODE_F4 * ni + 0];
-            const float4 n1 = nodes[PG_WIDE_NODE_F4 * ni + 1];
-            const float4 n2 = nodes[PG_WIDE_NODE_F4 * ni + 2];
-            const float4 n3 = nodes[PG_WIDE_NODE_F4 * ni + 3];
-            const float4 n4 = nodes[PG_WIDE_NODE_F4 * ni + 4];
-            const uint32_t e = __float_as_uint(n0.w);
-            // t = q * (2^e * idir) + (p - o) * idir per axis; the near plane of each axis is the lo
-            // byte for a non-negative direction and the hi byte otherwise (chosen once per node)
-            const float ax = __uint_as_float((e & 0xFFu) << 23) * idir.x, bx = (n0.x - o.x) * idir.x;
-            const float ay = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y, by = (n0.y - o.y) * idir.y;
-            const float az = __uint_as_float(((e >> 16) & 0xFFu) << 23) * idir.z, bz = (n0.z - o.z) * idir.z;
-            const uint32_t imask = e >> 24;
-            const bool px = octinv & 1u, py = octinv & 2u, pz = octinv & 4u;
-            const uint32_t loX0 = __float_as_uint(n2.x), loX1 = __float_as_uint(n2.y);
-            const uint32_t loY0 = __float_as_uint(n2.z), loY1 = __float_as_uint(n2.w);
-            const uint32_t loZ0 = __float_as_uint(n3.x), loZ1 = __float_as_uint(n3.y);
-            const uint32_t hiX0 = __float_as_uint(n3.z), hiX1 = __float_as_uint(n3.w);
-            const uint32_t hiY0 = __float_as_uint(n4.x), hiY1 = __float_as_uint(n4.y);
-            const uint32_t hiZ0 = __float_as_uint(n4.z), hiZ1 = __float_as_uint(n4.w);
-            const uint32_t nX0 = px ? loX0 : hiX0, nX1 = px ? loX1 : hiX1, fX0 = px ? hiX0 : loX0, fX1 = px ? hiX1 : loX1;
-            const uint32_t nY0 = py ? loY0 : hiY0, nY1 = py ? loY1 : hiY1, fY0 = py ? hiY0 : loY0, fY1 = py ? hiY1 : loY1;
-            const uint32_t nZ0 = pz ? loZ0 : hiZ0, nZ1 = pz ? loZ1 : hiZ1, fZ0 = pz ? hiZ0 : loZ0, fZ1 = pz ? hiZ1 : loZ1;
-            uint32_t hitSlots = 0;
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const float tnx = fmaf(qbyte(nX0, nX1, s), ax, bx), tfx = fmaf(qbyte(fX0, fX1, s), ax, bx);
-                const float tny = fmaf(qbyte(nY0, nY1, s), ay, by), tfy = fmaf(qbyte(fY0, fY1, s), ay, by);
-                const float tnz = fmaf(qbyte(nZ0, nZ1, s), az, bz), tfz = fmaf(qbyte(fZ0, fZ1, s), az, bz);
-                const float cmin = max3f(tnx, tny, fmaxf(tnz, tmin));
-                const float cmax = min3f(tfx, tfy, fminf(tfz, tmax));
-                hitSlots |= (cmin <= cmax ? 1u : 0u) << s;
-            }
-            const uint32_t nodeHits = permuteXor8(hitSlots & imask, octinv) << 24;
-            uint32_t triHits = 0;
-            const uint32_t meta0 = __float_as_uint(n1.z), meta1 = __float_as_uint(n1.w);
-            for (uint32_t leaves = hitSlots & ~imask; leaves; leaves &= leaves - 1u) {
-                const int s = __ffs(leaves) - 1;
-                const uint32_t meta = ((s < 4 ? meta0 : meta1) >> (8 * (s & 3))) & 0xFFu;
-                triHits |= ((1u << (meta >> 5)) - 1u) << (meta & 31u);
-            }
-            G = make_uint2(__float_as_uint(n1.x), nodeHits | imask);
-            T = make_uint2(__float_as_uint(n1.y), triHits);
-        }
-        while (T.y != 0) {
-            const uint32_t tr = T.x + (uint32_t)(__ffs(T.y) - 1);
-            T.y &= T.y - 1u;
-            float tt, bu, bv;
-            if (woopHit(woop, tr, o, d, tmin, tmax, tt, bu, bv)) {
-                found = true;
-                if (ANY) return true;
-                tmax = tt;
-                hitTri = tr;
-                hu = bu;
-                hv = bv;
-            }
-        }
-        if (G.y <= 0x00FFFFFFu) {
-            if (sp == 0) break;
-            G = stk.get(--sp);
-        }
-    }
-    return found;
-}
-
-// While-while traversal with postponed leaves (Aila & Laine 2009): lanes keep descending inner
-// nodes until every lane of the wave holds a leaf, then all lanes test triangles together.  This
-// keeps the 64-wide wave in one code path most of the time (if-if traversal measured 23 % lane
-// utilisation on gfx950).
-template <bool ANY>
-__device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
-                                         float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                         const TStack &stk) {
-    const int DONE = 0x7fffffff;
-    const float eps = 1e-30f;
-    const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
-                       1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-                       1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
-    const f3 ood = o * idir;
-    int sp = 0;
-    int node = 0;   // >= 0 inner node, < 0 leaf ref, DONE
-    int leaf = 0;   // postponed leaf ref (< 0) or none (>= 0)
-    bool found = false;
-    while (node != DONE) {
-        while (node >= 0 && node != DONE) {
-            const float4 n0 = nodes[4 * node + 0];
-            const float4 n1 = nodes[4 * node + 1];
-            const float4 n2 = nodes[4 * node + 2];
-            const float4 n3 = nodes[4 * node + 3];
-            float a0 = fmaf(n0.x, idir.x, -ood.x), a1 = fmaf(n0.y, idir.x, -ood.x);
-            float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
-            float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
-            float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), tmin));
-            float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), tmax));
-            float b0 = fmaf(n1.x, idir.x, -ood.x), b1 = fmaf(n1.y, idir.x, -ood.x);
-            float b2 = fmaf(n1.z, idir.y, -ood.y), b3 = fmaf(n1.w, idir.y, -ood.y);
-            float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
-            float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), tmin));
-            float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tmax));
-            const bool h0 = c0min <= c0max, h1 = c1min <= c1max;
-            const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
-            if (!h0 && !h1) {
-                node = sp > 0 ? (int)stk.get(--sp) : DONE;
-            } else {
-                node = h0 ? ch0 : ch1;
-                if (h0 && h1) {
-                    int farC = ch1;
-                    if (c1min < c0min) {
-                        node = ch1;
-                        farC = ch0;
-                    }
-                    if (sp < STACK_DEPTH) stk.put(sp++, (uint32_t)farC);
-                }
-            }
-            // first leaf found: postpone it and keep descending
-            if (node < 0 && leaf >= 0) {
-                leaf = node;
-                node = sp > 0 ? (int)stk.get(--sp) : DONE;
-            }
-            if (!__any(leaf >= 0)) break;  // every lane still here holds a leaf
-        }
-        while (leaf < 0) {
-            const uint32_t lr = ~(uint32_t)leaf;
-            const uint32_t first = lr >> 4, cnt = lr & 15u;
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const uint32_t tr = first + k;
-                const float4 w0 = woop[3 * tr + 0];
-                float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
-                float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-                float tt = oz / dz;
-                if (tt >= tmin && tt <= tmax) {
-                    const float4 w1 = woop[3 * tr + 1];
-                    float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
-                    if (a >= 0.0f && a <= 1.0f) {
-                        const float4 w2 = woop[3 * tr + 2];
-                        float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
-                        if (b >= 0.0f && a + b <= 1.0f) {
-                            found = true;
-                            if (ANY) return true;
-                            tmax = tt;
-                            hitTri = tr;
-                            hu = b;             // weight of p1
-                            hv = 1.0f - a - b;  // weight of p2
-                        }
-                    }
-                }
-            }
-            // another postponed leaf (in node)?  process it too
-            leaf = node;
-            if (node < 0) node = sp > 0 ? (int)stk.get(--sp) : DONE;
-        }
-    }
-    return found;
-}
-
-__device__ __forceinline__ float miWeight(float a, float b) {
-    a *= a;
-    b *= b;
-    return a / (a + b);
-}
-
-// wave-aggregated append of `pred` lanes' values into q (one atomic per wave)
-__device__ __forceinline__ void waveAppend(bool pred, uint32_t value, uint32_t *q, uint32_t *count) {
-    unsigned long long m = __ballot(pred);
-    if (m == 0) return;
-    int lane = threadIdx.x & 63;
-    int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (pred) {
-        unsigned long long below = m & ((1ull << lane) - 1ull);
-        q[base + __popcll(below)] = value;
-    }
-}
-
-__device__ __forceinline__ SDView sdv(const SDDev &sd) {
-    return SDView{sd.snodes, sd.meta, sd.qsum, sd.qchild, sd.jump, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]),
-                  sd.extent, sd.jump_bits, sd.built};
-}
-
-struct Hit {
-    f3 p, geoN, shN;
-    Frame sh;
-    f3 wi;
-    uint32_t mat;
-    int emitter;
-};
-
-__device__ __forceinline__ void fetchHit(const SceneDev &sc, uint32_t tri, float u, float v, f3 rd, Hit &h) {
-    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
-    float4 s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3], s4 = r[4];
-    uint32_t bits = __float_as_uint(s0.w);
-    h.mat = bits & 0xFFFFu;
-    h.emitter = (int)(bits >> 16) - 1;
-    float b0 = 1 - u - v;
-    f3 p0 = xyz(s0), p1 = xyz(s1), p2 = xyz(s2);
-    f3 n0 = xyz(s3), n1 = mk(s3.w, s4.x, s4.y), n2 = mk(s4.z, s4.w, s1.w);
-    // fillIntersectionRecord<true> (skdtree.h:343-430)
-    h.p = p0 * b0 + p1 * u + p2 * v;
-    f3 side1 = p1 - p0, side2 = p2 - p0;
-    f3 fn = cross(side1, side2);
-    float l = len(fn);
-    if (!isZero(fn)) fn = fn / l;
-    f3 shn = normalize(n0 * b0 + n1 * u + n2 * v);
-    if (dot(fn, shn) < 0) fn = -fn;
-    h.geoN = fn;
-    h.shN = shn;
-    h.sh = shadingFrame(shn, side1);
-    h.wi = h.sh.toLocal(-rd);
-}
-
-// Scene::sampleEmitterDirect without the visibility test (scene.cpp:871-895 + area.cpp:158-171 +
-// shape.cpp:102-115 + trimesh.cpp:412-423 + triangle.cpp:24-45); returns radiance/pdf.
-__device__ __forceinline__ f3 sampleEmitter(const GParams &g, const SceneDev &sc, f3 ref, f3 refN, float sx, float sy,
-                                            f3 &dOut, float &dist, float &pdfOut) {
-    uint32_t ne = g.num_emitters;
-    pdfOut = 0;
-    if (ne == 0) return mk1(0.f);
-    uint32_t ei = min((uint32_t)(sx * (float)ne), ne - 1);
-    sx = sx * (float)ne - (float)ei;
-    const GEmitter em = sc.ems[ei];
-    // DiscreteDistribution::sampleReuse over the area CDF (lower_bound)
-    const float *cdf = sc.emcdf + em.cdf_begin;
-    uint32_t lo = 0, hi = em.tri_count + 1;  // first index with cdf[i] >= sy
-    while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (cdf[mid] < sy) lo = mid + 1; else hi = mid;
-    }
-    int e = (int)lo - 1;
-    uint32_t idx = (uint32_t)min((int)em.tri_count - 1, max(0, e));
-    while (cdf[idx + 1] - cdf[idx] == 0 && idx < em.tri_count - 1) ++idx;
-    sy = (sy - cdf[idx]) / (cdf[idx + 1] - cdf[idx]);
-    const float4 *r = sc.emtri + (size_t)PG_TRI_SHADE_F4 * (em.tri_begin + idx);
-    float4 s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3], s4 = r[4];
-    f3 p0 = xyz(s0), p1 = xyz(s1), p2 = xyz(s2);
-    float a = safe_sqrt(1.0f - sx);
-    float bx = 1 - a, by = a * sy;
-    f3 sideA = p1 - p0, sideB = p2 - p0;
-    f3 p = p0 + (sideA * bx) + (sideB * by);
-    f3 n0 = xyz(s3), n1 = mk(s3.w, s4.x, s4.y), n2 = mk(s4.z, s4.w, s1.w);
-    f3 n = normalize(n0 * (1.0f - bx - by) + n1 * bx + n2 * by);
-    float pdf = em.inv_area;
-    f3 d = p - ref;
-    float distSq = dot(d, d);
-    dist = sqrtf(distSq);
-    d = d / dist;
-    float dp = absDot(d, n);
-    pdf *= dp != 0 ? (distSq / dp) : 0.0f;
-    dOut = d;
-    if (dot(d, refN) >= 0 && dot(d, n) < 0 && pdf != 0) {
-        float emPdf = 1.0f / (float)ne;
-        pdfOut = pdf * emPdf;
-        return mk(em.radiance[0], em.radiance[1], em.radiance[2]) / pdf / emPdf;
-    }
-    return mk1(0.f);
-}
-
-}  // namespace
+#include "pg_trace.h"
 
 // =============================================================================================
 // camera rays: PerspectiveCamera::sampleRay (perspective.cpp:271-298) for (pixel, sample) slots
@@ -421,14 +43,6 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
 }
 
-__device__ __forceinline__ TStack threadStack(uint32_t *lds, uint32_t *ovf) {
-    const uint32_t gtid = blockIdx.x * TRACE_BLOCK + threadIdx.x;
-    return TStack{lds + threadIdx.x, ovf + gtid, gridDim.x * TRACE_BLOCK};
-}
-__device__ __forceinline__ WStack threadWideStack(uint32_t *lds, uint32_t *ovf) {
-    const uint32_t gtid = blockIdx.x * TRACE_BLOCK + threadIdx.x;
-    return WStack{lds + threadIdx.x, ovf + gtid, gridDim.x * TRACE_BLOCK};
-}
 
 // closest hit for every queued path: hit[slot] = (t, BVH-order triangle | ~0, u, v).
 // Grid-stride over the queue shard blockIdx % PG_QSHARDS.  (A persistent variant with dynamic

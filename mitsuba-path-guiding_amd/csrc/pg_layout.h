@@ -36,6 +36,23 @@ struct GEmitter {
 };
 static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 
+// Heterogeneous medium record: 128 B (volpath).  World -> grid is g = p * gs + go
+// (gridvolume.cpp:186-198); invMax = 1 / (scale * maxFloatValue), maxFloatValue = 1
+// (gridvolume.cpp:583-585, heterogeneous.cpp:236-242).  density: res x*y*z floats, x fastest.
+struct GMedium {
+    const float *density;
+    uint32_t resx, resy;
+    uint32_t resz;
+    float scale, invMax, g;
+    float lo[3], pad0;
+    float hi[3], pad1;
+    float gs[3], pad2;
+    float go[3], pad3;
+    float albedo[3], pad4;
+    uint32_t pad5[4];
+};
+static_assert(sizeof(GMedium) == 128, "GMedium layout");
+
 // Per-triangle shading record (5 x float4 = 80 B), indexed by BVH-order triangle id:
 //   [0] p0.xyz, bits(material | (emitter + 1) << 16)
 //   [1] p1.xyz, n2.z

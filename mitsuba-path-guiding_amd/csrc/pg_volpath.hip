@@ -1,0 +1,607 @@
+// gfx950 volumetric path tracer: ProgressiveVolumetricPathTracer::Li
+// (src/integrators/path/progressive_volpath.cpp:98-374) with heterogeneous media
+// (src/medium/heterogeneous.cpp, Woodcock tracking), grid densities (src/volume/gridvolume.cpp)
+// and the HG phase function (src/phase/hg.cpp).  DESIGN.md §"Volumes".
+//
+// One persistent megakernel: every lane owns one camera path at a time and runs the reference's
+// loop one iteration per step; a lane whose path ended takes the next (pixel, sample) item from a
+// wave-aggregated work counter, so long paths (dense media) do not idle the rest of the wave.
+// Each item's radiance goes to rad[item]; k_film then accumulates items in sample order, so the
+// image is independent of which lane ran which item.  Random numbers: one sequential counter
+// stream per path (dimension 0 = pixel jitter, then one dimension per next1D / next2D), the same
+// stream the CPU oracle (oracle/orc_volpath.h) draws from.
+#include "pg_trace.h"
+
+namespace {
+
+#define VOL_BLOCK TRACE_BLOCK  // the traversal stack columns assume TRACE_BLOCK threads per block
+
+// Sampler::next1D / next2D over the counter RNG
+struct VRng {
+    uint32_t key, sample, dim;
+    __device__ __forceinline__ float next1() { return rng1(key, sample, dim++); }
+    __device__ __forceinline__ void next2(float &a, float &b) { rng2(key, sample, dim++, a, b); }
+};
+
+// ---- HG phase function (hg.cpp:74-106) --------------------------------------------------------
+__device__ __forceinline__ float hgEval(float g, f3 wi, f3 wo) {
+    float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
+    return kInvFourPi * (1 - g * g) / (temp * sqrtf(temp));
+}
+// Frame(n) by coordinateSystem (util.cpp:594-603): s = cross(c, n), t = c
+__device__ __forceinline__ f3 frameToWorld(f3 a, f3 v) {
+    f3 c;
+    if (fabsf(a.x) > fabsf(a.y)) {
+        float invLen = 1.0f / sqrtf(a.x * a.x + a.z * a.z);
+        c = mk(a.z * invLen, 0.0f, -a.x * invLen);
+    } else {
+        float invLen = 1.0f / sqrtf(a.y * a.y + a.z * a.z);
+        c = mk(0.0f, a.z * invLen, -a.y * invLen);
+    }
+    return cross(c, a) * v.x + c * v.y + a * v.z;
+}
+__device__ __forceinline__ f3 hgSample(float g, f3 wi, float sx, float sy, float &pdf) {
+    float cosTheta;
+    if (fabsf(g) < kEpsilon) {
+        cosTheta = 1 - 2 * sx;
+    } else {
+        float sqrTerm = (1 - g * g) / (1 - g + 2 * g * sx);
+        cosTheta = (1 + g * g - sqrTerm * sqrTerm) / (2 * g);
+    }
+    float sinTheta = safe_sqrt(1.0f - cosTheta * cosTheta);
+    float sinPhi, cosPhi;
+    sincosf(2 * kPi * sy, &sinPhi, &cosPhi);
+    f3 wo = frameToWorld(-wi, mk(sinTheta * cosPhi, sinTheta * sinPhi, cosTheta));
+    pdf = hgEval(g, wi, wo);
+    return wo;
+}
+
+// ---- heterogeneous medium (heterogeneous.cpp:546-660, gridvolume.cpp:337-380) -----------------
+struct MedView {
+    const float *density;
+    int rx, ry, rz;
+    f3 gs, go, lo, hi;
+    float scale, invMax;
+};
+__device__ __forceinline__ MedView medView(const GMedium *media, int m) {
+    const GMedium &G = media[m];
+    MedView v;
+    v.density = G.density;
+    v.rx = (int)G.resx;
+    v.ry = (int)G.resy;
+    v.rz = (int)G.resz;
+    v.gs = mk(G.gs[0], G.gs[1], G.gs[2]);
+    v.go = mk(G.go[0], G.go[1], G.go[2]);
+    v.lo = mk(G.lo[0], G.lo[1], G.lo[2]);
+    v.hi = mk(G.hi[0], G.hi[1], G.hi[2]);
+    v.scale = G.scale;
+    v.invMax = G.invMax;
+    return v;
+}
+// lookupFloat: trilinear, zero unless all 8 corners are inside the grid
+__device__ __forceinline__ float lookupDensity(const MedView &M, f3 p) {
+    const float px = p.x * M.gs.x + M.go.x, py = p.y * M.gs.y + M.go.y, pz = p.z * M.gs.z + M.go.z;
+    const int x1 = (int)floorf(px), y1 = (int)floorf(py), z1 = (int)floorf(pz);
+    if (x1 < 0 || y1 < 0 || z1 < 0 || x1 + 1 >= M.rx || y1 + 1 >= M.ry || z1 + 1 >= M.rz) return 0.0f;
+    const float fx = px - x1, fy = py - y1, fz = pz - z1, _fx = 1.0f - fx, _fy = 1.0f - fy, _fz = 1.0f - fz;
+    const size_t sy = (size_t)M.rx, sz = (size_t)M.rx * M.ry;
+    const float *b = M.density + (size_t)z1 * sz + (size_t)y1 * sy + x1;
+    const float d000 = b[0], d001 = b[1], d010 = b[sy], d011 = b[sy + 1];
+    const float d100 = b[sz], d101 = b[sz + 1], d110 = b[sz + sy], d111 = b[sz + sy + 1];
+    return ((d000 * _fx + d001 * fx) * _fy + (d010 * _fx + d011 * fx) * fy) * _fz +
+           ((d100 * _fx + d101 * fx) * _fy + (d110 * _fx + d111 * fx) * fy) * fz;
+}
+// AABB::rayIntersect of the density box, clipped to [mint, maxt]
+__device__ __forceinline__ bool medClip(const MedView &M, f3 o, f3 d, float mint, float maxt, float &t0, float &t1) {
+    float nearT = -__int_as_float(0x7f800000), farT = __int_as_float(0x7f800000);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const float oi = i == 0 ? o.x : (i == 1 ? o.y : o.z), di = i == 0 ? d.x : (i == 1 ? d.y : d.z);
+        const float mn = i == 0 ? M.lo.x : (i == 1 ? M.lo.y : M.lo.z), mx = i == 0 ? M.hi.x : (i == 1 ? M.hi.y : M.hi.z);
+        if (di == 0) {
+            if (oi < mn || oi > mx) return false;
+        } else {
+            float a = (mn - oi) / di, b = (mx - oi) / di;
+            if (a > b) {
+                const float tmp = a;
+                a = b;
+                b = tmp;
+            }
+            nearT = fmaxf(a, nearT);
+            farT = fminf(b, farT);
+            if (!(nearT <= farT)) return false;
+        }
+    }
+    t0 = fmaxf(nearT, mint);
+    t1 = fminf(farT, maxt);
+    return true;
+}
+// Woodcock tracking: true with the collision point (sampleDistance, 'woodcock' branch)
+__device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, float maxt, VRng &rng, f3 &pOut) {
+    float t0, t1;
+    if (!medClip(M, o, d, 0.0f, maxt, t0, t1)) return false;
+    float t = t0;
+    for (;;) {
+        t -= logf(1 - rng.next1()) * M.invMax;
+        if (!(t < t1)) return false;
+        const f3 p = o + d * t;
+        const float density = lookupDensity(M, p) * M.scale;
+        if (density * M.invMax > rng.next1()) {
+            pOut = p;
+            return true;
+        }
+    }
+}
+// evalTransmittance with a sampler: mean of 2 delta-tracking survival indicators
+__device__ __forceinline__ float evalTransmittance(const MedView &M, f3 o, f3 d, float maxt, VRng &rng) {
+    float t0, t1;
+    if (!medClip(M, o, d, 0.0f, maxt, t0, t1)) return 1.0f;
+    float result = 0;
+    for (int i = 0; i < 2; ++i) {
+        float t = t0;
+        for (;;) {
+            t -= logf(1 - rng.next1()) * M.invMax;
+            if (!(t < t1)) {
+                result += 1;
+                break;
+            }
+            const f3 p = o + d * t;
+            const float density = lookupDensity(M, p) * M.scale;
+            if (density * M.invMax > rng.next1()) break;
+        }
+    }
+    return result * 0.5f;
+}
+
+// ---- scene queries ----------------------------------------------------------------------------
+__device__ __forceinline__ float max3abs(f3 o) { return fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)); }
+// ShapeKDTree::rayIntersect(ray, its) epsilon rule for mint == Epsilon (skdtree.cpp:125-128)
+__device__ __forceinline__ float itsMinT(f3 o) { return kEpsilon * fmaxf(max3abs(o), kEpsilon); }
+
+__device__ __forceinline__ bool closestHit(const SceneDev &sc, f3 o, f3 d, float tmin, float tmax, float &t,
+                                           uint32_t &tri, float &u, float &v, const TStack &stk) {
+    t = tmax;
+    tri = 0xFFFFFFFFu;
+    u = v = 0;
+    if (!(tmax > tmin)) return false;
+    return traverse<false>(sc.nodes, sc.woop, o, d, tmin, t, tri, u, v, stk);
+}
+__device__ __forceinline__ uint32_t triBits(const SceneDev &sc, uint32_t tri) {
+    return __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri].w);
+}
+__device__ __forceinline__ bool isNullMat(const SceneDev &sc, uint32_t bits) {
+    return (sc.mats[bits & 0xFFFFu].type & ENull) != 0;
+}
+// Intersection::getTargetMedium(d) from the packed (interior + 1) | (exterior + 1) << 16
+__device__ __forceinline__ int targetMedium(uint32_t tm, f3 d, f3 n) {
+    return dot(d, n) > 0 ? (int)(tm >> 16) - 1 : (int)(tm & 0xFFFFu) - 1;
+}
+__device__ __forceinline__ f3 rawFaceNormal(const SceneDev &sc, uint32_t tri) {
+    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
+    const f3 p0 = xyz(r[0]), p1 = xyz(r[1]), p2 = xyz(r[2]);
+    return normalize(cross(p1 - p0, p2 - p0));
+}
+
+// Scene::evalTransmittance (scene.cpp:662-720) from p1 to a point p2 on an emitter
+__device__ __forceinline__ float sceneTransmittance(const SceneDev &sc, const VolDev &v, f3 p1, bool p1OnSurface, f3 p2, int medium,
+                                    int maxInteractions, VRng &rng, const TStack &stk, uint32_t &segs) {
+    f3 d = p2 - p1;
+    float remaining = len(d);
+    d = d / remaining;
+    const float lengthFactor = 1 - kShadowEpsilon;
+    f3 o = p1;
+    float mint = p1OnSurface ? kEpsilon * max3abs(o) : 0.0f;  // rayIntersect(ray, t, shape, n, uv) rule
+    float maxt = remaining * lengthFactor;
+    float T = 1.0f;
+    int interactions = 0;
+    while (remaining > 0) {
+        float t, u, w;
+        uint32_t tri;
+        const bool surface = closestHit(sc, o, d, mint, maxt, t, tri, u, w, stk);
+        segs++;
+        if (!surface) t = __int_as_float(0x7f800000);
+        if (surface && (interactions == maxInteractions || !isNullMat(sc, triBits(sc, tri)))) return 0.0f;
+        if (medium >= 0) T *= evalTransmittance(medView(v.media, medium), o, d, fminf(t, remaining), rng);
+        if (!surface || T == 0) break;
+        const uint32_t tm = v.tmed[tri];
+        if (tm) {
+            const f3 n = rawFaceNormal(sc, tri);
+            if (medium != targetMedium(tm, -d, n)) return 0.0f;
+            medium = targetMedium(tm, d, n);
+        }
+        if (++interactions > 100) break;
+        o = o + d * t;
+        remaining -= t;
+        maxt = remaining * lengthFactor;
+        mint = kEpsilon * max3abs(o);
+    }
+    return T;
+}
+
+struct ItsRef {  // the caller's intersection record: closest hit of the current ray
+    bool valid;
+    float t, u, v;
+    uint32_t tri;
+};
+
+// rayIntersectAndLookForEmitter (progressive_volpath.cpp:401-460).  `its` gets the FIRST hit.  The
+// walk through null surfaces is done once without the medium; only when it ends on a lit emitter
+// is it walked again to estimate the transmittance of its segments (the reference estimates it
+// on every walk and discards it otherwise: same estimator, oracle/orc_volpath.h "lazy").
+__device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev &v, int medium, int maxInteractions, f3 o0, f3 d,
+                               float mint0, ItsRef &its, f3 &value, f3 &qn, float &qdist, int &qem, VRng &rng,
+                               const TStack &stk, uint32_t &segs) {
+    value = mk1(0.f);
+    qem = -1;
+    f3 o = o0;
+    float mint = mint0;
+    int m = medium, interactions = 0;
+    bool anyMedium = false;
+    float t = 0, u = 0, w = 0;
+    uint32_t tri = 0;
+    uint32_t bits = 0;
+    for (;;) {
+        const bool surface = closestHit(sc, o, d, mint, __int_as_float(0x7f800000), t, tri, u, w, stk);
+        segs++;
+        if (interactions == 0) its = ItsRef{surface, surface ? t : __int_as_float(0x7f800000), u, w, tri};
+        anyMedium |= m >= 0;
+        if (!surface) return;  // no environment emitter
+        bits = triBits(sc, tri);
+        if (interactions == maxInteractions || !isNullMat(sc, bits) || (bits >> 16) != 0) break;
+        const uint32_t tm = v.tmed[tri];
+        if (tm) {
+            Hit h;
+            fetchHit(sc, tri, u, w, d, h);
+            m = targetMedium(tm, d, h.geoN);
+        }
+        o = o + d * t;
+        mint = itsMinT(o);
+        if (++interactions > 100) return;
+    }
+    const int em = (int)(bits >> 16) - 1;
+    if (em < 0) return;
+    Hit h;
+    fetchHit(sc, tri, u, w, d, h);
+    if (!(dot(h.shN, -d) > 0)) return;  // AreaLight::eval: back side emits nothing
+    const GEmitter &E = sc.ems[em];
+    float T = 1.0f;
+    if (anyMedium) {  // second walk: the transmittance estimate of every segment in a medium
+        f3 oo = o0;
+        float mt = mint0;
+        int mm = medium;
+        for (int k = 0; k <= interactions; ++k) {
+            float tt, uu, ww;
+            uint32_t tr;
+            closestHit(sc, oo, d, mt, __int_as_float(0x7f800000), tt, tr, uu, ww, stk);
+            segs++;
+            if (mm >= 0) {
+                T *= evalTransmittance(medView(v.media, mm), oo, d, tt, rng);
+                if (T == 0) break;
+            }
+            const uint32_t tm = v.tmed[tr];
+            if (tm) {
+                Hit hh;
+                fetchHit(sc, tr, uu, ww, d, hh);
+                mm = targetMedium(tm, d, hh.geoN);
+            }
+            oo = oo + d * tt;
+            mt = itsMinT(oo);
+        }
+    }
+    value = mk(E.radiance[0], E.radiance[1], E.radiance[2]) * T;
+    qn = h.shN;
+    qdist = t;  // setQuery: the LAST segment's length (records.inl:170-178)
+    qem = em;
+}
+
+// Scene::pdfEmitterDirect for a found emitter (area.cpp pdfDirect + shape.cpp:117-126)
+__device__ __forceinline__ float pdfEmitter(const GParams &g, const SceneDev &sc, int em, f3 refN, f3 d, f3 n,
+                                            float dist) {
+    if (!(dot(d, refN) >= 0 && dot(d, n) < 0)) return 0.0f;
+    return sc.ems[em].inv_area * (dist * dist) / absDot(d, n) * (1.0f / (float)g.num_emitters);
+}
+
+struct VPath {
+    f3 o, d;
+    ItsRef its;
+    f3 T, L;
+    float eta;
+    int medium, depth;
+    bool scattered, emission;
+};
+
+// one iteration of the Li loop; false when the path ends
+__device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, VPath &P, VRng &rng,
+                        const TStack &stk, uint32_t &segs, uint32_t &shadows) {
+    const int maxDepth = g.max_depth;
+    if (!(P.depth <= maxDepth || maxDepth < 0) || P.depth > g.depth_cap) return false;
+    const int maxInter = maxDepth - P.depth - 1;
+    bool inMedium = false;
+    f3 mp = mk1(0.f);
+    if (P.medium >= 0)
+        inMedium = sampleDistance(medView(v.media, P.medium), P.o, P.d, P.its.valid ? P.its.t : __int_as_float(0x7f800000),
+                                  rng, mp);
+    if (inMedium) {
+        // ---- medium interaction (progressive_volpath.cpp:117-196)
+        if (P.depth >= maxDepth && maxDepth != -1) return false;
+        const GMedium &GM = v.media[P.medium];
+        P.T = P.T * mk(GM.albedo[0], GM.albedo[1], GM.albedo[2]);
+        const float hg = GM.g;
+        const f3 wi = -P.d;
+        if (g.use_nee) {
+            float s0, s1;
+            rng.next2(s0, s1);
+            f3 dD, ep;
+            float dist, pdf;
+            f3 value = sampleEmitter(g, sc, mp, mk1(0.f), s0, s1, dD, dist, pdf, &ep);
+            if (pdf != 0) {
+                shadows++;
+                value = value * sceneTransmittance(sc, v, mp, false, ep, P.medium, maxInter, rng, stk, segs);
+                if (!isZero(value)) {
+                    const float phaseVal = hgEval(hg, wi, dD);
+                    if (phaseVal != 0) P.L = P.L + P.T * value * (phaseVal * miWeight(pdf, phaseVal));
+                }
+            }
+        }
+        float u0, u1, phasePdf;
+        rng.next2(u0, u1);
+        const f3 wo = hgSample(hg, wi, u0, u1, phasePdf);
+        P.o = mp;
+        P.d = wo;
+        f3 value, qn;
+        float qdist;
+        int qem;
+        lookForEmitter(sc, v, P.medium, maxInter, mp, wo, 0.0f, P.its, value, qn, qdist, qem, rng, stk, segs);
+        if (!isZero(value) && fminf(value.x, fminf(value.y, value.z)) > 0.f) {
+            const float emitterPdf = g.use_nee ? pdfEmitter(g, sc, qem, mk1(0.f), wo, qn, qdist) : 0.0f;
+            P.L = P.L + P.T * value * (g.use_nee ? miWeight(phasePdf, emitterPdf) : 1.0f);
+        }
+        P.emission = false;
+    } else {
+        // ---- surface interaction (progressive_volpath.cpp:197-352)
+        if (!P.its.valid) return false;  // no environment emitter
+        Hit h;
+        fetchHit(sc, P.its.tri, P.its.u, P.its.v, P.d, h);
+        if (h.emitter >= 0 && P.emission && (!g.hide_emitters || P.scattered) && dot(h.shN, -P.d) > 0) {
+            const GEmitter &E = sc.ems[h.emitter];
+            P.L = P.L + P.T * mk(E.radiance[0], E.radiance[1], E.radiance[2]);
+        }
+        if (P.depth >= maxDepth && maxDepth != -1) return false;
+        if (g.strict_normals && -dot(h.geoN, P.d) * h.wi.z < 0) return false;
+        const GMat M = sc.mats[h.mat];
+        const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
+        const uint32_t tm = v.tmed[P.its.tri];
+        if (g.use_nee && (M.type & ESmooth)) {
+            float s0, s1;
+            rng.next2(s0, s1);
+            f3 dD, ep;
+            float dist, pdf;
+            f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, dD, dist, pdf, &ep);
+            if (pdf != 0) {
+                const int m2 = tm ? targetMedium(tm, dD, h.geoN) : P.medium;
+                shadows++;
+                value = value * sceneTransmittance(sc, v, h.p, true, ep, m2, maxInter, rng, stk, segs);
+                if (!isZero(value)) {
+                    const f3 woL = h.sh.toLocal(dD);
+                    const f3 f = bsdfEval(M, h.wi, woL);
+                    if (!isZero(f) && (!g.strict_normals || dot(h.geoN, dD) * woL.z > 0))
+                        P.L = P.L + P.T * value * f * miWeight(pdf, bsdfPdf(M, h.wi, woL));
+                }
+            }
+        }
+        float b0, b1;
+        rng.next2(b0, b1);
+        const float b2 = rng.next1();
+        BS bs;
+        const f3 weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+        if (isZero(weight)) return false;
+        const f3 wo = h.sh.toWorld(bs.wo);
+        if (g.strict_normals && dot(h.geoN, wo) * bs.wo.z <= 0) return false;
+        P.o = h.p;
+        P.d = wo;
+        P.T = P.T * weight;
+        P.eta *= bs.eta;
+        if (tm) P.medium = targetMedium(tm, wo, h.geoN);
+        if (bs.type == ENull) {  // index-matched boundary: straight through, counted as a bounce
+            P.emission = !P.scattered;
+            float t, u, w;
+            uint32_t tri;
+            const bool hit = closestHit(sc, h.p, wo, itsMinT(h.p), __int_as_float(0x7f800000), t, tri, u, w, stk);
+            segs++;
+            P.its = ItsRef{hit, hit ? t : __int_as_float(0x7f800000), u, w, tri};
+            P.depth++;
+            return true;
+        }
+        f3 value, qn;
+        float qdist;
+        int qem;
+        lookForEmitter(sc, v, P.medium, maxInter, h.p, wo, itsMinT(h.p), P.its, value, qn, qdist, qem, rng, stk, segs);
+        if (!isZero(value)) {
+            const float emitterPdf =
+                (g.use_nee && !(bs.type & EDelta)) ? pdfEmitter(g, sc, qem, refN, wo, qn, qdist) : 0.0f;
+            P.L = P.L + P.T * value * (g.use_nee ? miWeight(bs.pdf, emitterPdf) : 1.0f);
+        }
+        P.emission = false;
+    }
+    if (P.depth++ >= g.rr_depth) {
+        const float q = fminf(maxc(P.T) * P.eta * P.eta, 0.95f);
+        if (rng.next1() >= q) return false;
+        P.T = P.T / q;
+    }
+    P.scattered = true;
+    return true;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(VOL_BLOCK) void k_volpath(GParams g, SceneDev sc, VolDev v,
+                                                       const uint32_t *__restrict__ local_pixels, uint32_t pix_begin,
+                                                       uint32_t npix, uint32_t nlayers, uint32_t sample_base) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, v.stack_ovf);
+    const uint32_t nitems = npix * nlayers;
+    const int lane = threadIdx.x & 63;
+    uint32_t segs = 0, shadows = 0;
+    bool alive = false, done = false;
+    uint32_t item = 0;
+    VPath P;
+    VRng rng{0, 0, 0};
+    for (;;) {
+        // refill finished lanes from the work counter (one atomic per wave)
+        const unsigned long long need = __ballot(!alive && !done);
+        if (need) {
+            const int leader = __ffsll((long long)need) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(v.next, (uint32_t)__popcll(need));
+            base = __shfl(base, leader);
+            if (!alive && !done) {
+                item = base + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                if (item >= nitems) {
+                    done = true;
+                } else {
+                    // camera ray (PerspectiveCamera::sampleRay, perspective.cpp:271-298) + first hit
+                    const uint32_t layer = item / npix, lp = item - layer * npix;
+                    const uint32_t pix = local_pixels[pix_begin + lp];
+                    rng = VRng{rngKey(pix, g.seed), sample_base + layer, 1};
+                    float jx, jy;
+                    rng2(rng.key, rng.sample, 0, jx, jy);
+                    const float px = (float)(pix % g.width) + jx, py = (float)(pix / g.width) + jy;
+                    const float sx = px / (float)g.width, sy = py / (float)g.height;
+                    const f3 nearP = mk((1.0f - 2.0f * sx) * g.tan_half, (1.0f - 2.0f * sy) / g.aspect * g.tan_half, 1.0f);
+                    const f3 dl = normalize(nearP);
+                    const float invZ = 1.0f / dl.z;
+                    P.o = mk(g.cam_o[0], g.cam_o[1], g.cam_o[2]);
+                    P.d = mk(g.cam_left[0], g.cam_left[1], g.cam_left[2]) * dl.x +
+                          mk(g.cam_up[0], g.cam_up[1], g.cam_up[2]) * dl.y + mk(g.cam_dir[0], g.cam_dir[1], g.cam_dir[2]) * dl.z;
+                    float t, u, w;
+                    uint32_t tri;
+                    const bool hit = closestHit(sc, P.o, P.d, g.near_clip * invZ, g.far_clip * invZ, t, tri, u, w, stk);
+                    segs++;
+                    P.its = ItsRef{hit, hit ? t : __int_as_float(0x7f800000), u, w, tri};
+                    P.T = mk1(1.f);
+                    P.L = mk1(0.f);
+                    P.eta = 1.0f;
+                    P.medium = v.cam_medium;
+                    P.depth = 1;
+                    P.scattered = false;
+                    P.emission = true;
+                    alive = true;
+                }
+            }
+        }
+        if (!__any(alive)) break;
+        if (alive && !volStep(g, sc, v, P, rng, stk, segs, shadows)) {
+            v.rad[item] = f4(P.L, 0.0f);
+            alive = false;
+        }
+    }
+    // statistics: wave sums, one atomic per wave
+    unsigned long long s0 = segs, s1 = shadows;
+    for (int off = 32; off > 0; off >>= 1) {
+        s0 += __shfl_xor(s0, off);
+        s1 += __shfl_xor(s1, off);
+    }
+    if (lane == 0) {
+        atomicAdd(v.stats, s0);
+        atomicAdd(v.stats + 1, s1);
+    }
+}
+
+// ---- unit-level queries (pg_phase_query / pg_medium_query) --------------------------------------
+__global__ __launch_bounds__(256) void k_phase_query(const GMedium *medium, const float *in, const float *wog,
+                                                     uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float *a = in + 5 * (size_t)i;
+    const f3 wi = mk(a[0], a[1], a[2]);
+    const float g = medium->g;
+    float pdf;
+    const f3 wo = hgSample(g, wi, a[3], a[4], pdf);
+    float *o = out + 5 * (size_t)i;
+    o[0] = wo.x;
+    o[1] = wo.y;
+    o[2] = wo.z;
+    o[3] = pdf;
+    o[4] = wog ? hgEval(g, wi, mk(wog[3 * i], wog[3 * i + 1], wog[3 * i + 2])) : 0.0f;
+}
+__global__ __launch_bounds__(256) void k_medium_query(const GMedium *medium, int op, const float *in,
+                                                      const uint32_t *keys, uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const MedView M = medView(medium, 0);
+    if (op == 0) {
+        out[i] = lookupDensity(M, mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+        return;
+    }
+    const float *r = in + 8 * (size_t)i;
+    VRng rng{keys[2 * i], keys[2 * i + 1], 1};
+    const f3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
+    float *q = out + 4 * (size_t)i;
+    float t0, t1;
+    if (op == 1) {
+        // sampleDistance with an explicit mint (the integrator always passes 0)
+        bool ok = false;
+        float t = 0;
+        if (medClip(M, o, d, r[3], r[7], t0, t1)) {
+            t = t0;
+            for (;;) {
+                t -= logf(1 - rng.next1()) * M.invMax;
+                if (!(t < t1)) break;
+                const float density = lookupDensity(M, o + d * t) * M.scale;
+                if (density * M.invMax > rng.next1()) {
+                    ok = true;
+                    break;
+                }
+            }
+        }
+        q[0] = ok ? 1.0f : 0.0f;
+        q[1] = ok ? t : 0.0f;
+        q[2] = (float)(rng.dim - 1);
+        q[3] = 0;
+    } else {
+        float tr = 1.0f;
+        if (medClip(M, o, d, r[3], r[7], t0, t1)) {
+            // evalTransmittance restricted to [t0, t1] (mint folded into the clip)
+            float result = 0;
+            for (int k = 0; k < 2; ++k) {
+                float t = t0;
+                for (;;) {
+                    t -= logf(1 - rng.next1()) * M.invMax;
+                    if (!(t < t1)) {
+                        result += 1;
+                        break;
+                    }
+                    const float density = lookupDensity(M, o + d * t) * M.scale;
+                    if (density * M.invMax > rng.next1()) break;
+                }
+            }
+            tr = result * 0.5f;
+        }
+        q[0] = tr;
+        q[1] = (float)(rng.dim - 1);
+        q[2] = q[3] = 0;
+    }
+}
+
+void pg_launch_phase_query(hipStream_t s, const GMedium *medium, const float *in, const float *wog, uint32_t n,
+                           float *out) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_phase_query, dim3((n + 255) / 256), dim3(256), 0, s, medium, in, wog, n, out);
+}
+void pg_launch_medium_query(hipStream_t s, const GMedium *medium, int op, const float *in, const uint32_t *keys,
+                            uint32_t n, float *out) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_medium_query, dim3((n + 255) / 256), dim3(256), 0, s, medium, op, in, keys, n, out);
+}
+
+void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v,
+                       const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
+                       uint32_t sample_base) {
+    const uint64_t n = (uint64_t)npix * nlayers;
+    if (!n) return;
+    (void)hipMemsetAsync(v.next, 0, sizeof(uint32_t), s);
+    const uint64_t want = (n + VOL_BLOCK - 1) / VOL_BLOCK;
+    const uint32_t grid = (uint32_t)(want < TRACE_MAX_BLOCKS ? want : TRACE_MAX_BLOCKS);
+    hipLaunchKernelGGL(k_volpath, dim3(grid), dim3(VOL_BLOCK), 0, s, g, sc, v, local_pixels, pix_begin, npix, nlayers,
+                       sample_base);
+}

@@ -3,6 +3,8 @@
     reference                                              here
     -----------------------------------------------------  ---------------------------------------
     ProgressiveMIPathTracer (progressive_path.cpp:89-124)   ProgressivePathTracer
+    ProgressiveVolumetricPathTracer (progressive_volpath.   ProgressiveVolumetricPathTracer
+      cpp:71-96)
     <guided progressive path tracer> (absent)     GuidedPathTracer
     Integrator::preprocess (integrator.h:61)                .preprocess(scene)
     ProgressiveMonteCarloIntegrator::render (progressive-   .render()
@@ -211,11 +213,35 @@ class Device:
         self._chk(self.lib.pg_bsdf_query(self.h, material, _p(wi), _p(u), _p(wg), len(wi), _p(out)))
         return out
 
+    def phase_query(self, medium, wi, u, wo_given=None):
+        """(wo.xyz, pdf, eval(wi, wo_given)) per query, HG of `medium` on the device."""
+        a = np.ascontiguousarray(np.concatenate([np.asarray(wi, np.float32), np.asarray(u, np.float32)], 1))
+        wg = None if wo_given is None else np.ascontiguousarray(wo_given, np.float32)
+        out = np.zeros((len(a), 5), np.float32)
+        self._chk(self.lib.pg_phase_query(self.h, medium, _p(a), _p(wg), len(a), _p(out)))
+        return out
+
+    def medium_lookup(self, medium, pts):
+        pts = np.ascontiguousarray(pts, np.float32)
+        out = np.zeros(len(pts), np.float32)
+        self._chk(self.lib.pg_medium_query(self.h, medium, 0, _p(pts), None, len(pts), _p(out)))
+        return out
+
+    def medium_sample(self, medium, rays, keys, transmittance=False):
+        """rays n x 8 (o, mint, d, maxt); keys n x 2 u32 (rng key, sample); returns n x 4."""
+        rays = np.ascontiguousarray(rays, np.float32)
+        keys = np.ascontiguousarray(keys, np.uint32)
+        out = np.zeros((len(rays), 4), np.float32)
+        self._chk(self.lib.pg_medium_query(self.h, medium, 2 if transmittance else 1, _p(rays), _p(keys), len(rays),
+                                           _p(out)))
+        return out
+
 
 class ProgressivePathTracer:
     """Mirror of ProgressiveMIPathTracer: plain (unguided) progressive path tracing on the GPU."""
 
     guided = False
+    integrator = capi.PG_INTEGRATOR_PATH
 
     def __init__(self, props=None, device=0, rank=0, world_size=1):
         props = dict(props or {})
@@ -231,7 +257,7 @@ class ProgressivePathTracer:
             bsdf_sampling_fraction=float(props.get("bsdfSamplingFraction", 0.5)),
             s_tree_threshold=float(props.get("sTreeThreshold", 12000.0)),
             d_tree_threshold=float(props.get("dTreeThreshold", 0.01)),
-            max_paths_in_flight=int(props.get("maxPathsInFlight", 0)))
+            max_paths_in_flight=int(props.get("maxPathsInFlight", 0)), integrator=self.integrator)
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         self.dev = None
         self.progression = 0
@@ -276,6 +302,14 @@ class ProgressivePathTracer:
         if self.dev:
             self.dev.close()
         return st
+
+
+class ProgressiveVolumetricPathTracer(ProgressivePathTracer):
+    """Mirror of ProgressiveVolumetricPathTracer: unguided progressive volumetric path tracing
+    (heterogeneous media with Woodcock tracking, HG phase functions, null-BSDF medium boundaries)
+    on the GPU.  Same properties as ProgressivePathTracer."""
+
+    integrator = capi.PG_INTEGRATOR_VOLPATH
 
 
 class GuidedPathTracer(ProgressivePathTracer):

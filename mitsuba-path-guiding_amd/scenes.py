@@ -4,6 +4,8 @@
   C3     ajar_door()    Veach ajar-door class: two rooms, door ajar ~7 deg, the only light in the far
                         room, rough-conductor + dielectric objects (~30-60k triangles)
   C4     kitchen()      Country-kitchen class interior: ~1M triangles, several area emitters
+  C5     smoke()        Heterogeneous smoke: seeded fBm density grid (256^3 at full size) inside a
+                        null-BSDF box, HG g = 0.8, albedo 0.9, over a diffuse floor under an area light
 
 A scene is flat numpy arrays (what a Mitsuba adapter extracts from Scene::getShapes() / getBSDFs():
 SURVEY.md §8b "Scene inputs it reads") plus a `desc()` that returns the pg_scene_desc for the C-ABI.
@@ -31,12 +33,12 @@ def _f4(v):
 
 def material(kind, **kw):
     """Build a pg_material.  kind in diffuse|conductor|roughconductor|dielectric|roughdielectric|plastic|
-    roughplastic."""
+    roughplastic|null."""
     m = capi.pg_material()
     types = {"diffuse": capi.PG_BSDF_DIFFUSE, "conductor": capi.PG_BSDF_CONDUCTOR,
              "roughconductor": capi.PG_BSDF_ROUGHCONDUCTOR, "dielectric": capi.PG_BSDF_DIELECTRIC,
              "roughdielectric": capi.PG_BSDF_ROUGHDIELECTRIC, "plastic": capi.PG_BSDF_PLASTIC,
-             "roughplastic": capi.PG_BSDF_ROUGHPLASTIC}
+             "roughplastic": capi.PG_BSDF_ROUGHPLASTIC, "null": capi.PG_BSDF_NULL}
     m.type = types[kind]
     dist = kw.get("distribution", "beckmann")
     m.distribution = capi.PG_DIST_GGX if dist == "ggx" else capi.PG_DIST_BECKMANN
@@ -75,6 +77,8 @@ class Scene:
         self._pos, self._nrm, self._idx = [], [], []
         self._nverts = 0
         self.shapes, self.materials, self.emitters = [], [], []
+        self.media, self._densities = [], []
+        self.camera_medium = -1
         self.camera = None
         self._desc = None
         self.name = "scene"
@@ -84,7 +88,25 @@ class Scene:
         self.materials.append(m)
         return len(self.materials) - 1
 
-    def add_mesh(self, V, F, N=None, material=0, radiance=None):
+    def add_medium(self, density, aabb_min, aabb_max, scale, albedo=(0.9, 0.9, 0.9), g=0.8):
+        """Heterogeneous medium (src/medium/heterogeneous.cpp): density grid indexed [z][y][x] with
+        values in [0, 1] over the data AABB, density multiplier `scale`, constant albedo, HG phase g."""
+        dens = np.ascontiguousarray(density, np.float32)
+        assert dens.ndim == 3
+        m = capi.pg_medium()
+        m.type = capi.PG_MEDIUM_HETEROGENEOUS
+        m.res = (C.c_uint32 * 3)(dens.shape[2], dens.shape[1], dens.shape[0])
+        m.density = dens.ctypes.data_as(C.POINTER(C.c_float))
+        m.aabb_min = (C.c_float * 3)(*aabb_min)
+        m.aabb_max = (C.c_float * 3)(*aabb_max)
+        m.scale = scale
+        m.albedo = (C.c_float * 3)(*albedo)
+        m.g = g
+        self._densities.append(dens)
+        self.media.append(m)
+        return len(self.media) - 1
+
+    def add_mesh(self, V, F, N=None, material=0, radiance=None, interior=-1, exterior=-1):
         V = np.asarray(V, np.float32).reshape(-1, 3)
         F = np.asarray(F, np.uint32).reshape(-1, 3)
         if N is None:  # flat shading: unshare vertices, per-face normals
@@ -100,7 +122,7 @@ class Scene:
         self._nrm.append(N)
         self._idx.append(F + np.uint32(self._nverts))
         self._nverts += len(V)
-        sh = capi.pg_shape(tri_begin, len(F), material, -1)
+        sh = capi.pg_shape(tri_begin, len(F), material, -1, interior, exterior)
         if radiance is not None:
             e = capi.pg_emitter()
             e.shape = len(self.shapes)
@@ -126,6 +148,7 @@ class Scene:
         self._shapes_arr = (capi.pg_shape * len(self.shapes))(*self.shapes)
         self._mats_arr = (capi.pg_material * len(self.materials))(*self.materials)
         self._ems_arr = (capi.pg_emitter * max(1, len(self.emitters)))(*self.emitters)
+        self._media_arr = (capi.pg_medium * max(1, len(self.media)))(*self.media)
         d = capi.pg_scene_desc()
         d.num_vertices = len(self.positions)
         d.num_triangles = len(self.indices)
@@ -139,6 +162,9 @@ class Scene:
         d.materials = C.cast(self._mats_arr, C.POINTER(capi.pg_material))
         d.emitters = C.cast(self._ems_arr, C.POINTER(capi.pg_emitter))
         d.camera = self.camera
+        d.num_media = len(self.media)
+        d.media = C.cast(self._media_arr, C.POINTER(capi.pg_medium))
+        d.camera_medium = self.camera_medium
         self._desc = d
         return self
 
@@ -492,4 +518,57 @@ def kitchen(width=1920, height=1080, target_tris=1_000_000, seed=7):
     return s.finalize()
 
 
-SCENES = {"cornell": cornell, "ajar_door": ajar_door, "kitchen": kitchen}
+# ---------------------------------------------------------------------------------------------
+# C5: heterogeneous smoke
+def fbm_density(res=256, seed=7, octaves=5, base=4):
+    """Seeded fBm density in [0, 1] on a res^3 grid ([z][y][x]): value-noise octaves (trilinear
+    upsampling of random lattices, base * 2^o cells per axis, amplitude 2^-o) shaped by a soft
+    spherical falloff and a threshold, so the cloud has empty space, wisps and a dense core."""
+    rng = np.random.default_rng(seed)
+    x = (np.arange(res, dtype=np.float32) + 0.5) / res  # cell-centred coordinates in (0, 1)
+    acc = np.zeros((res, res, res), np.float32)
+    amp, total = 1.0, 0.0
+    for o in range(octaves):
+        n = base * (2 ** o)
+        lat = rng.random((n + 1, n + 1, n + 1), dtype=np.float32)
+        f = x * n
+        i0 = np.minimum(f.astype(np.int32), n - 1)
+        w = (f - i0).astype(np.float32)
+        w = w * w * (3 - 2 * w)  # smoothstep fade
+        # separable trilinear interpolation: z, then y, then x
+        a = lat[i0] * (1 - w)[:, None, None] + lat[i0 + 1] * w[:, None, None]              # (res, n+1, n+1)
+        a = a[:, i0] * (1 - w)[None, :, None] + a[:, i0 + 1] * w[None, :, None]            # (res, res, n+1)
+        a = a[:, :, i0] * (1 - w)[None, None, :] + a[:, :, i0 + 1] * w[None, None, :]      # (res, res, res)
+        acc += amp * a
+        total += amp
+        amp *= 0.5
+        del a
+    acc /= total
+    c = x - 0.5
+    r2 = c[:, None, None] ** 2 + c[None, :, None] ** 2 + c[None, None, :] ** 2
+    shape = np.clip(1.0 - r2 / 0.22, 0.0, 1.0)
+    d = np.clip((acc * shape - 0.18) * 2.5, 0.0, 1.0).astype(np.float32)
+    return d
+
+
+def smoke(width=1024, height=1024, res=256, seed=7, scale=40.0, albedo=0.9, g=0.8):
+    """C5: the smoke cloud (fBm grid over [-1, 1]^3, enclosed by a null-BSDF box whose interior is
+    the medium) above a diffuse floor, lit by one area light; camera outside the medium."""
+    s = Scene()
+    s.name = "smoke"
+    floor = s.add_material(material("diffuse", reflectance=(0.6, 0.6, 0.6)))
+    lightm = s.add_material(material("diffuse", reflectance=(0.0, 0.0, 0.0)))
+    nullm = s.add_material(material("null"))
+    dens = fbm_density(res, seed)
+    med = s.add_medium(dens, (-1.0, -1.0, -1.0), (1.0, 1.0, 1.0), scale, (albedo, albedo, albedo), g)
+    V, F = box((-1.0, -1.0, -1.0), (1.0, 1.0, 1.0))  # outward normals: interior = inside the box
+    s.add_mesh(V, F, material=nullm, interior=med)
+    V, F = quad((-6, -1.2, -6), (6, -1.2, -6), (6, -1.2, 6), (-6, -1.2, 6), facing=(0, 1, 0))
+    s.add_mesh(V, F, material=floor)
+    V, F = quad((-1.5, 4.0, -2.5), (1.5, 4.0, -2.5), (1.5, 3.0, -0.5), (-1.5, 3.0, -0.5), facing=(0, -1, 0.5))
+    s.add_mesh(V, F, material=lightm, radiance=(30.0, 28.0, 24.0))
+    s.set_camera((0.0, 0.6, 4.2), (0.0, -0.1, 0.0), (0, 1, 0), 45.0, width, height)
+    return s.finalize()
+
+
+SCENES = {"cornell": cornell, "ajar_door": ajar_door, "kitchen": kitchen, "smoke": smoke}

@@ -12,15 +12,19 @@
 // extended with SD-tree guiding (one-sample MIS between BSDF and D-tree, Mueller et al. 2017;
 // PARITY UNPINNED for the guiding arithmetic, see orc_sdtree.h) and training-record emission.
 // Random numbers follow the shared counter-RNG spec, not SFMT.
+// pg_config.integrator == PG_INTEGRATOR_VOLPATH renders with VolLi (orc_volpath.h) instead.
 #include <atomic>
 #include <thread>
 
 #include "orc_scene.h"
 #include "orc_sdtree.h"
+#include "orc_volpath.h"
 
 using namespace orc;
 
 namespace {
+
+bool g_volpathEager = false;  // oracle_set_volpath_eager: the reference's eager transmittance walk
 
 inline float miWeight(float a, float b) {
     a *= a;
@@ -257,7 +261,16 @@ int oracle_render(void *sp, const pg_config *cfg, void *tp, uint32_t spp, uint32
                     float jx, jy;
                     rng.next2(0, jx, jy);
                     Ray ray = S.cameraRay((float)px + jx, (float)py + jy);
-                    V3 L = Li(S, *cfg, tree, rng, ray, rp, cnt);
+                    V3 L;
+                    if (cfg->integrator == PG_INTEGRATOR_VOLPATH) {
+                        SeqRng srng{rng};
+                        VolCounters vc;
+                        L = VolLi(S, *cfg, srng, ray, vc, !g_volpathEager);
+                        cnt.segments += vc.segments;
+                        cnt.shadow += vc.shadow;
+                    } else {
+                        L = Li(S, *cfg, tree, rng, ray, rp, cnt);
+                    }
                     cnt.paths++;
                     float m = maxc(L);
                     if (m > cfg->max_component_value) L = L * (cfg->max_component_value / m);
@@ -445,5 +458,56 @@ void oracle_bsdf_query(const pg_material *pm, const float *wi, const float *u, c
 }
 
 uint32_t oracle_material_type(const pg_material *pm) { return makeMaterial(*pm).type; }
+
+void oracle_set_volpath_eager(int32_t eager) { g_volpathEager = eager != 0; }
+
+// Medium queries on medium `m` of the scene (tests/test_volume.py):
+//   op 0: lookupFloat(p)            in: n x 3 points           out: n
+//   op 1: sampleDistance            in: n x 8 rays (o, mint, d, maxt), key/sample per ray in u32 `aux` (2n)
+//                                   out: n x 4 (hit flag, t, draws used, 0)
+//   op 2: evalTransmittance         same inputs, out: n x 4 (T, draws used, 0, 0)
+void oracle_medium_query(void *sp, int32_t m, int32_t op, const float *in, const uint32_t *aux, uint64_t n, float *out) {
+    const Scene &S = *(const Scene *)sp;
+    const Medium &M = S.media[m];
+    for (uint64_t i = 0; i < n; ++i) {
+        if (op == 0) {
+            out[i] = M.lookup(V3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+            continue;
+        }
+        const float *r = in + 8 * i;
+        SeqRng rng{Rng{aux[2 * i], aux[2 * i + 1]}};
+        V3 o(r[0], r[1], r[2]), d(r[4], r[5], r[6]);
+        float *q = out + 4 * i;
+        if (op == 1) {
+            float t = 0;
+            V3 p;
+            bool ok = M.sampleDistance(o, d, r[3], r[7], rng, t, p);
+            q[0] = ok ? 1.0f : 0.0f;
+            q[1] = ok ? t : 0.0f;
+            q[2] = (float)(rng.dim - 1);
+            q[3] = 0;
+        } else {
+            q[0] = M.evalTransmittance(o, d, r[3], r[7], rng);
+            q[1] = (float)(rng.dim - 1);
+            q[2] = q[3] = 0;
+        }
+    }
+}
+
+// HG phase function: per query (wi.xyz, u0, u1) -> (wo.xyz, pdf, eval(wi, wo_given)) with wo_given in `wog`
+void oracle_hg_query(float g, const float *in, const float *wog, uint64_t n, float *out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const float *a = in + 5 * i;
+        V3 wi(a[0], a[1], a[2]);
+        float pdf;
+        V3 wo = hgSample(g, wi, a[3], a[4], pdf);
+        float *o = out + 5 * i;
+        o[0] = wo.x;
+        o[1] = wo.y;
+        o[2] = wo.z;
+        o[3] = pdf;
+        o[4] = wog ? hgEval(g, wi, V3(wog[3 * i], wog[3 * i + 1], wog[3 * i + 2])) : 0.0f;
+    }
+}
 
 }  // extern "C"

@@ -49,6 +49,9 @@ def lib(capi):
             "oracle_material_type": (C.c_uint32, [C.POINTER(capi.pg_material)]),
             "oracle_rough_transmittance": (None, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
             "oracle_intersect": (None, [VP, VP, C.c_uint64, VP]),
+            "oracle_set_volpath_eager": (None, [C.c_int32]),
+            "oracle_medium_query": (None, [VP, C.c_int32, C.c_int32, VP, VP, C.c_uint64, VP]),
+            "oracle_hg_query": (None, [C.c_float, VP, VP, C.c_uint64, VP]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -84,6 +87,20 @@ class OracleScene:
         rays = np.ascontiguousarray(rays, np.float32)
         out = np.zeros((len(rays), 16), np.float32)
         self.L.oracle_intersect(self.h, _p(rays), len(rays), _p(out))
+        return out
+
+    def medium_lookup(self, m, pts):
+        pts = np.ascontiguousarray(pts, np.float32)
+        out = np.zeros(len(pts), np.float32)
+        self.L.oracle_medium_query(self.h, m, 0, _p(pts), None, len(pts), _p(out))
+        return out
+
+    def medium_sample(self, m, rays, keys, transmittance=False):
+        """rays: n x 8 (o, mint, d, maxt); keys: n x 2 u32 (rng key, sample).  Returns n x 4."""
+        rays = np.ascontiguousarray(rays, np.float32)
+        keys = np.ascontiguousarray(keys, np.uint32)
+        out = np.zeros((len(rays), 4), np.float32)
+        self.L.oracle_medium_query(self.h, m, 2 if transmittance else 1, _p(rays), _p(keys), len(rays), _p(out))
         return out
 
     def trace(self, rays, any_hit=False):
@@ -168,6 +185,19 @@ def bsdf_query(capi, mat, wi, u, wo_given=None):
     wg = None if wo_given is None else np.ascontiguousarray(wo_given, np.float32)
     out = np.zeros((len(wi), 12), np.float32)
     lib(capi).oracle_bsdf_query(C.byref(mat), _p(wi), _p(u), _p(wg), len(wi), _p(out))
+    return out
+
+
+def set_volpath_eager(capi, eager):
+    lib(capi).oracle_set_volpath_eager(int(bool(eager)))
+
+
+def hg_query(capi, g, wi, u, wo_given=None):
+    """(wo.xyz, pdf, eval(wi, wo_given)) per query."""
+    a = np.ascontiguousarray(np.concatenate([np.asarray(wi, np.float32), np.asarray(u, np.float32)], 1), np.float32)
+    wg = None if wo_given is None else np.ascontiguousarray(wo_given, np.float32)
+    out = np.zeros((len(a), 5), np.float32)
+    lib(capi).oracle_hg_query(float(g), _p(a), _p(wg), len(a), _p(out))
     return out
 
 

@@ -25,8 +25,8 @@ enum : uint32_t {
     EDiffuse = EDiffuseReflection | EDiffuseTransmission,
     EGlossy = EGlossyReflection | EGlossyTransmission,
     ESmooth = EDiffuse | EGlossy,
-    EDelta = EDeltaReflection | EDeltaTransmission,
-    ETransmission = EDiffuseTransmission | EGlossyTransmission | EDeltaTransmission,
+    EDelta = ENull | EDeltaReflection | EDeltaTransmission,                            // bsdf.h:280
+    ETransmission = EDiffuseTransmission | EGlossyTransmission | EDeltaTransmission | ENull,  // bsdf.h:270-272
 };
 
 struct Material {
@@ -80,6 +80,7 @@ inline Material makeMaterial(const pg_material &pm) {
             roughPlasticTables((int)pm.distribution, std::max(pm.alpha_u, 1e-4f), M.eta, *M.rtrans, M.fdrInt);
             break;
         }
+        case PG_BSDF_NULL: M.type = ENull; sides |= EBackSide; break;  // null.cpp:40
         default: M.type = 0;
     }
     if (M.twosided()) sides |= EBackSide;
@@ -228,6 +229,13 @@ inline float pdf1(const Material &M, V3 wi, V3 wo) {
 // returns weight = f*cos/pdf (zero on failure); u = (u0,u1) 2D sample, u2 = extra 1D sample
 inline V3 sample1(const Material &M, V3 wi, float u0, float u1, float u2, BSample &bs) {
     switch (M.m.type) {
+        case PG_BSDF_NULL: {  // null.cpp:64-75: pass straight through (eval/pdf of continuous measures are 0)
+            bs.wo = -wi;
+            bs.eta = 1.0f;
+            bs.sampledType = ENull;
+            bs.pdf = 1.0f;
+            return V3(1.0f);
+        }
         case PG_BSDF_DIFFUSE: {
             if (wi.z <= 0) return V3(0.f);
             bs.wo = squareToCosineHemisphere(u0, u1);

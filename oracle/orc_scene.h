@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "orc_bsdf.h"
+#include "orc_medium.h"
 
 namespace orc {
 
@@ -139,10 +140,13 @@ struct Scene {
     std::vector<BvhNode> nodes;
     AABB bounds;
     Camera cam;
+    std::vector<Medium> media;
+    int camMedium = -1;
 
     void build(const pg_scene_desc &d);
     bool intersect(const Ray &ray, Its &its) const;
     bool occluded(const Ray &ray) const;
+    bool intersectRaw(const Ray &ray, float &t, uint32_t &prim) const;
     bool traverse(const Ray &r, float mint, float maxt, bool any, float &t, float &u, float &v, uint32_t &prim) const;
     void fill(const Ray &r, float t, float u, float v, uint32_t prim, Its &its) const;
     Ray cameraRay(float sx, float sy) const;
@@ -176,6 +180,9 @@ inline void Scene::build(const pg_scene_desc &d) {
         for (uint32_t t = 0; t < shapes[s].tri_count; ++t) triShape[shapes[s].tri_begin + t] = s;
     for (uint32_t m = 0; m < d.num_materials; ++m) mats.push_back(makeMaterial(d.materials[m]));
     emitters.assign(d.emitters, d.emitters + d.num_emitters);
+    media.resize(d.num_media);
+    for (uint32_t m = 0; m < d.num_media; ++m) media[m].init(d.media[m]);
+    camMedium = d.camera_medium;
     for (auto &e : emitters) {
         const pg_shape &sh = shapes[e.shape];
         // area CDF: double accumulation of fp32 triangle areas, normalized, stored as fp32
@@ -434,6 +441,23 @@ inline bool Scene::occluded(const Ray &ray) const {
     return traverse(ray, mint, maxt, true, t, u, v, prim);
 }
 
+// ShapeKDTree::rayIntersect(ray, t, shape, n, uv) (skdtree.cpp:144-162): closest hit with the
+// shadow-ray epsilon rule; the caller takes the unflipped face normal from `prim`
+inline bool Scene::intersectRaw(const Ray &ray, float &tOut, uint32_t &prim) const {
+    tOut = kInf;
+    float mint, maxt;
+    if (!bounds.rayIntersect(ray, mint, maxt)) return false;
+    float rayMinT = ray.mint;
+    if (rayMinT == kEpsilon) rayMinT *= std::max(std::max(std::fabs(ray.o.x), std::fabs(ray.o.y)), std::fabs(ray.o.z));
+    if (rayMinT > mint) mint = rayMinT;
+    if (ray.maxt < maxt) maxt = ray.maxt;
+    if (!(maxt > mint)) return false;
+    float t, u, v;
+    if (!traverse(ray, mint, maxt, false, t, u, v, prim)) return false;
+    tOut = t;
+    return true;
+}
+
 // DiscreteDistribution::sampleReuse (pmf.h:124-169) over a normalized CDF
 inline uint32_t sampleReuseCdf(const std::vector<float> &cdf, float &s) {
     auto it = std::lower_bound(cdf.begin(), cdf.end(), s);
@@ -450,13 +474,14 @@ struct DirectRec {
     int emitter = -1;
 };
 
-// Scene::sampleEmitterDirect with visibility (scene.cpp:871-895)
-inline V3 sampleEmitterDirect(const Scene &S, DirectRec &dr, float sx, float sy) {
+// Scene::sampleEmitterDirect without the visibility test (scene.cpp:871-895 up to the shadow ray):
+// returns radiance / pdf with dr.pdf including the emitter-selection pdf; dr.pdf = 0 on failure
+inline V3 sampleEmitterNoVis(const Scene &S, DirectRec &dr, float sx, float sy) {
     uint32_t ne = (uint32_t)S.emitters.size();
+    dr.pdf = 0;
     if (ne == 0) return V3(0.f);
-    // uniform emitter CDF (sampling weight 1 each): index = floor-ish, with reuse
-    float emPdf = 1.0f / (float)ne;
     // uniform emitter pdf (every sampling weight is 1): sampleReuse on a uniform CDF
+    float emPdf = 1.0f / (float)ne;
     uint32_t ei = std::min((uint32_t)(sx * (float)ne), ne - 1);
     sx = sx * (float)ne - (float)ei;
     const pg_emitter &em = S.emitters[ei];
@@ -484,18 +509,23 @@ inline V3 sampleEmitterDirect(const Scene &S, DirectRec &dr, float sx, float sy)
     float dp = absDot(dr.d, dr.n);
     dr.pdf *= dp != 0 ? (distSq / dp) : 0.0f;
     // AreaLight::sampleDirect
-    V3 value;
-    if (dot(dr.d, dr.refN) >= 0 && dot(dr.d, dr.n) < 0 && dr.pdf != 0) {
-        value = V3(em.radiance[0], em.radiance[1], em.radiance[2]) / dr.pdf;
-    } else {
+    if (!(dot(dr.d, dr.refN) >= 0 && dot(dr.d, dr.n) < 0 && dr.pdf != 0)) {
         dr.pdf = 0;
         return V3(0.f);
     }
-    Ray sr{dr.ref, dr.d, kEpsilon, dr.dist * (1 - kShadowEpsilon)};
-    if (S.occluded(sr)) return V3(0.f);
+    V3 value = V3(em.radiance[0], em.radiance[1], em.radiance[2]) / dr.pdf;
     dr.emitter = (int)ei;
     dr.pdf *= emPdf;
     return value / emPdf;
+}
+
+// Scene::sampleEmitterDirect with visibility (scene.cpp:871-895)
+inline V3 sampleEmitterDirect(const Scene &S, DirectRec &dr, float sx, float sy) {
+    V3 value = sampleEmitterNoVis(S, dr, sx, sy);
+    if (dr.pdf == 0) return V3(0.f);
+    Ray sr{dr.ref, dr.d, kEpsilon, dr.dist * (1 - kShadowEpsilon)};
+    if (S.occluded(sr)) return V3(0.f);
+    return value;
 }
 
 // Scene::pdfEmitterDirect for a BSDF-sampled hit on emitter `ei` (records.inl:170-178 setQuery)
