@@ -179,9 +179,13 @@ typedef struct pg_config {
     int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024) */
     int32_t path_lanes;           /* path chunks in flight on separate streams, 1..4 (0 = auto: 3) */
     int32_t integrator;           /* PG_INTEGRATOR_PATH (progressive_path) or _VOLPATH (progressive_volpath) */
-    int32_t pad1;
+    int32_t volume_majorant;      /* volpath free-flight / transmittance tracking: PG_MAJORANT_GRID (default:
+                                     delta tracking against per-cell maxima of 8^3-voxel blocks, skipping empty
+                                     cells) or PG_MAJORANT_GLOBAL (the reference's single majorant, scale * 1,
+                                     heterogeneous.cpp:589-660).  Both sample the same distributions. */
 } pg_config;
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
+enum { PG_MAJORANT_GRID = 0, PG_MAJORANT_GLOBAL = 1 };
 
 /* Training record written per non-delta path vertex (SoA-free 32-byte AoS). */
 typedef struct pg_record {
@@ -271,7 +275,8 @@ pg_status pg_phase_query(void *ctx, uint32_t medium, const float *in, const floa
  * op 0 (density): in n x 3 world points; out n floats = lookupFloat(p) (unscaled).
  * op 1 (free flight) / op 2 (transmittance): in n x 8 rays (o.xyz, mint, d.xyz, maxt) and keys n x 2
  * (rng key, sample): the draws are dimensions 1, 2, ... of that counter stream.  out n x 4:
- * op 1: (interaction 1/0, t, draws used, 0), op 2: (transmittance estimate, draws used, 0, 0). */
+ * op 1: (interaction 1/0, t, draws used, 0), op 2: (transmittance estimate, draws used, 0, 0).
+ * op 3 / op 4: as op 1 / op 2 with PG_MAJORANT_GRID tracking (ops 1, 2 use the global majorant). */
 pg_status pg_medium_query(void *ctx, uint32_t medium, int32_t op, const float *in, const uint32_t *keys, uint64_t n,
                           float *out);
 

@@ -15,6 +15,8 @@ PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, P
  PG_BSDF_PLASTIC, PG_BSDF_ROUGHPLASTIC, PG_BSDF_NULL) = range(8)
 PG_MEDIUM_HETEROGENEOUS = 0
 PG_INTEGRATOR_PATH, PG_INTEGRATOR_VOLPATH = 0, 1
+PG_MAJORANT_GRID, PG_MAJORANT_GLOBAL = 0, 1
+MAJORANT_CELL = 8  # voxels per majorant-grid cell edge (pg_host.cpp / oracle/orc_medium.h)
 PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
 PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
 
@@ -76,7 +78,7 @@ class pg_config(C.Structure):
                 ("s_tree_threshold", C.c_float), ("d_tree_threshold", C.c_float), ("d_tree_max_depth", C.c_int32),
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
-                ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("pad1", C.c_int32)]
+                ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32)]
 
 
 class pg_record(C.Structure):

@@ -131,7 +131,7 @@ struct Ctx {
     GParams g{};
     DevBuf nodes, woop, wnodes, wwoop, tshade, tclass, mats, rtab, ems, emtri, emcdf;
     // media (volpath)
-    DevBuf media, density, tmed;
+    DevBuf media, density, tmed, majorant;
     int32_t cam_medium = -1;
     uint32_t num_media = 0;
     DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
@@ -463,6 +463,52 @@ pg_status validateMedium(Ctx *c, const pg_medium &pm, uint32_t m) {
     return PG_OK;
 }
 
+// per-cell maxima of the density grid (cell c covers voxels [c * CELL - 1, (c + 1) * CELL + 1] per
+// axis, clamped), times scale; appended to `out` in cell order (x fastest)
+void buildMajorants(const pg_medium &pm, const GMedium &gm, std::vector<float> &out) {
+    const int C = PG_MAJORANT_CELL;
+    const int r[3] = {(int)pm.res[0], (int)pm.res[1], (int)pm.res[2]}, n[3] = {(int)gm.mx, (int)gm.my, (int)gm.mz};
+    // separable running maxima: along x, then y, then z, each over the cell's voxel window
+    auto win = [&](int a, int cidx, int &lo, int &hi) {
+        lo = std::max(0, cidx * C - 1);
+        hi = std::min(r[a] - 1, (cidx + 1) * C + 1);
+    };
+    std::vector<float> ax((size_t)n[0] * r[1] * r[2]), ay((size_t)n[0] * n[1] * r[2]);
+    for (int z = 0; z < r[2]; ++z)
+        for (int y = 0; y < r[1]; ++y) {
+            const float *row = pm.density + ((size_t)z * r[1] + y) * r[0];
+            for (int cx = 0; cx < n[0]; ++cx) {
+                int lo, hi;
+                win(0, cx, lo, hi);
+                float m = 0;
+                for (int x = lo; x <= hi; ++x) m = std::max(m, row[x]);
+                ax[((size_t)z * r[1] + y) * n[0] + cx] = m;
+            }
+        }
+    for (int z = 0; z < r[2]; ++z)
+        for (int cy = 0; cy < n[1]; ++cy) {
+            int lo, hi;
+            win(1, cy, lo, hi);
+            for (int cx = 0; cx < n[0]; ++cx) {
+                float m = 0;
+                for (int y = lo; y <= hi; ++y) m = std::max(m, ax[((size_t)z * r[1] + y) * n[0] + cx]);
+                ay[((size_t)z * n[1] + cy) * n[0] + cx] = m;
+            }
+        }
+    const size_t base = out.size();
+    out.resize(base + (size_t)n[0] * n[1] * n[2]);
+    for (int cz = 0; cz < n[2]; ++cz) {
+        int lo, hi;
+        win(2, cz, lo, hi);
+        for (int cy = 0; cy < n[1]; ++cy)
+            for (int cx = 0; cx < n[0]; ++cx) {
+                float m = 0;
+                for (int z = lo; z <= hi; ++z) m = std::max(m, ay[((size_t)z * n[1] + cy) * n[0] + cx]);
+                out[base + ((size_t)cz * n[1] + cy) * n[0] + cx] = m * pm.scale;
+            }
+    }
+}
+
 pg_status pg_config_default(pg_config *c) {
     if (!c) return PG_ERR_INVALID;
     std::memset(c, 0, sizeof *c);
@@ -521,6 +567,10 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     if (c->cfg.integrator != PG_INTEGRATOR_PATH && c->cfg.integrator != PG_INTEGRATOR_VOLPATH) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown integrator");
+    }
+    if (c->cfg.volume_majorant != PG_MAJORANT_GRID && c->cfg.volume_majorant != PG_MAJORANT_GLOBAL) {
+        delete c;
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown volume_majorant");
     }
     if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH && c->cfg.guiding) {
         delete c;
@@ -609,6 +659,9 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         }
         denOff.push_back(denTotal);
         denTotal += (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+        gm.mx = std::max(1u, (pm.res[0] - 1 + PG_MAJORANT_CELL - 1) / PG_MAJORANT_CELL);
+        gm.my = std::max(1u, (pm.res[1] - 1 + PG_MAJORANT_CELL - 1) / PG_MAJORANT_CELL);
+        gm.mz = std::max(1u, (pm.res[2] - 1 + PG_MAJORANT_CELL - 1) / PG_MAJORANT_CELL);
         gmed.push_back(gm);
     }
     // per-triangle (material | emitter+1 << 16) from the shape partition
@@ -726,6 +779,15 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
                                    c->stream));
             gmed[m].density = c->density.as<float>() + at[m];
         }
+        // majorant grids (PG_MAJORANT_GRID tracking): one buffer, per-medium offsets
+        std::vector<float> maj;
+        std::vector<size_t> majAt;
+        for (uint32_t m = 0; m < d->num_media; ++m) {
+            majAt.push_back(maj.size());
+            buildMajorants(d->media[m], gmed[m], maj);
+        }
+        if ((s = upload(c, c->majorant, maj))) return s;
+        for (uint32_t m = 0; m < d->num_media; ++m) gmed[m].maj = c->majorant.as<float>() + majAt[m];
         HIPC(c, hipStreamSynchronize(c->stream));  // the host density arrays are caller-owned
         if ((s = upload(c, c->media, gmed))) return s;
         c->num_media = d->num_media;
@@ -820,6 +882,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
     g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
     const SceneDev sc = sceneView(c);
     VolDev v{};
+    v.grid = c->cfg.volume_majorant == PG_MAJORANT_GRID ? 1 : 0;
     v.media = c->media.as<GMedium>();
     v.tmed = c->tmed.as<uint32_t>();
     v.cam_medium = c->cam_medium;
@@ -1393,7 +1456,7 @@ pg_status pg_medium_query(void *ctx, uint32_t medium, int32_t op, const float *i
     Ctx *c = (Ctx *)ctx;
     if (!c || (!in && n) || (!out && n) || (op != 0 && !keys && n))
         return fail(c, PG_ERR_INVALID, "pg_medium_query: null argument");
-    if (op < 0 || op > 2) return fail(c, PG_ERR_INVALID, "pg_medium_query: bad op");
+    if (op < 0 || op > 4) return fail(c, PG_ERR_INVALID, "pg_medium_query: bad op");
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_medium_query: no scene");
     if (medium >= c->num_media) return fail(c, PG_ERR_INVALID, "pg_medium_query: bad medium");
     HIPC(c, hipSetDevice(c->cfg.device));

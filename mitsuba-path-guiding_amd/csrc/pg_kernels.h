@@ -48,6 +48,7 @@ struct VolDev {
     const uint32_t *tmed;      // per BVH-order triangle: (interior + 1) | (exterior + 1) << 16, 0 = no transition
     int32_t cam_medium;        // -1: none
     uint32_t num_media;
+    int32_t grid;              // 1: majorant-grid tracking, 0: the global majorant
     float4 *rad;               // per work item (layer-major: item = layer * npix + lp), radiance
     uint32_t *next;            // work counter (zeroed by the launcher)
     unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries

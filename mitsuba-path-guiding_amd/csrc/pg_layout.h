@@ -39,17 +39,24 @@ static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 // Heterogeneous medium record: 128 B (volpath).  World -> grid is g = p * gs + go
 // (gridvolume.cpp:186-198); invMax = 1 / (scale * maxFloatValue), maxFloatValue = 1
 // (gridvolume.cpp:583-585, heterogeneous.cpp:236-242).  density: res x*y*z floats, x fastest.
+// maj: the majorant grid, mx*my*mz cells of PG_MAJORANT_CELL^3 voxels, each scale * the maximum
+// voxel over the cell extended by one voxel per side.
+#define PG_MAJORANT_CELL 8
 struct GMedium {
     const float *density;
     uint32_t resx, resy;
     uint32_t resz;
     float scale, invMax, g;
-    float lo[3], pad0;
-    float hi[3], pad1;
-    float gs[3], pad2;
+    float lo[3];
+    uint32_t mx;
+    float hi[3];
+    uint32_t my;
+    float gs[3];
+    uint32_t mz;
     float go[3], pad3;
     float albedo[3], pad4;
-    uint32_t pad5[4];
+    const float *maj;
+    uint32_t pad5[2];
 };
 static_assert(sizeof(GMedium) == 128, "GMedium layout");
 

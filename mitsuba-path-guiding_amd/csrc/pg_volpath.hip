@@ -59,7 +59,9 @@ __device__ __forceinline__ f3 hgSample(float g, f3 wi, float sx, float sy, float
 // ---- heterogeneous medium (heterogeneous.cpp:546-660, gridvolume.cpp:337-380) -----------------
 struct MedView {
     const float *density;
+    const float *maj;
     int rx, ry, rz;
+    int mx, my, mz;
     f3 gs, go, lo, hi;
     float scale, invMax;
 };
@@ -76,6 +78,10 @@ __device__ __forceinline__ MedView medView(const GMedium *media, int m) {
     v.hi = mk(G.hi[0], G.hi[1], G.hi[2]);
     v.scale = G.scale;
     v.invMax = G.invMax;
+    v.maj = G.maj;
+    v.mx = (int)G.mx;
+    v.my = (int)G.my;
+    v.mz = (int)G.mz;
     return v;
 }
 // lookupFloat: trilinear, zero unless all 8 corners are inside the grid
@@ -132,6 +138,79 @@ __device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, flo
         }
     }
 }
+// Delta tracking through the majorant grid over [t0, t1] (oracle/orc_medium.h trackGrid): a 3D DDA
+// over PG_MAJORANT_CELL^3-voxel cells; exponential steps at the cell majorant, restarted at each
+// cell exit (memoryless); empty cells cost no draw and no lookup.
+__device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0, float t1, VRng &rng, float &tHit) {
+    const float B = (float)PG_MAJORANT_CELL, inf = __int_as_float(0x7f800000);
+    const f3 og = mk(o.x * M.gs.x + M.go.x, o.y * M.gs.y + M.go.y, o.z * M.gs.z + M.go.z);
+    const f3 dg = mk(d.x * M.gs.x, d.y * M.gs.y, d.z * M.gs.z);
+    int c[3], stp[3];
+    float tNext[3], tDelta[3];
+    const int n[3] = {M.mx, M.my, M.mz};
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float oa = a == 0 ? og.x : (a == 1 ? og.y : og.z), da = a == 0 ? dg.x : (a == 1 ? dg.y : dg.z);
+        c[a] = min(max((int)floorf((oa + da * t0) / B), 0), n[a] - 1);
+        if (da > 0) {
+            stp[a] = 1;
+            tNext[a] = ((float)(c[a] + 1) * B - oa) / da;
+            tDelta[a] = B / da;
+        } else if (da < 0) {
+            stp[a] = -1;
+            tNext[a] = ((float)c[a] * B - oa) / da;
+            tDelta[a] = -B / da;
+        } else {
+            stp[a] = 0;
+            tNext[a] = inf;
+            tDelta[a] = inf;
+        }
+    }
+    float t = t0;
+    for (;;) {
+        const float tExit = fminf(fminf(tNext[0], tNext[1]), fminf(tNext[2], t1));
+        const float mu = M.maj[((size_t)c[2] * M.my + c[1]) * M.mx + c[0]];
+        if (mu > 0) {
+            for (;;) {
+                const float ts = t - logf(1 - rng.next1()) / mu;
+                if (!(ts < tExit)) break;
+                t = ts;
+                const float density = lookupDensity(M, o + d * t) * M.scale;
+                if (density > mu * rng.next1()) {
+                    tHit = t;
+                    return true;
+                }
+            }
+        }
+        t = fmaxf(t, tExit);
+        if (!(t < t1)) return false;
+        const int a = tNext[0] <= tNext[1] ? (tNext[0] <= tNext[2] ? 0 : 2) : (tNext[1] <= tNext[2] ? 1 : 2);
+        // register-resident indexing: select instead of dynamic array access
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            if (k == a) {
+                c[k] += stp[k];
+                tNext[k] += tDelta[k];
+            }
+        if (c[0] < 0 || c[1] < 0 || c[2] < 0 || c[0] >= n[0] || c[1] >= n[1] || c[2] >= n[2]) return false;
+    }
+}
+__device__ __forceinline__ bool sampleDistanceGrid(const MedView &M, f3 o, f3 d, float maxt, VRng &rng, f3 &pOut) {
+    float t0, t1, t;
+    if (!medClip(M, o, d, 0.0f, maxt, t0, t1) || !(t0 < t1)) return false;
+    if (!trackGrid(M, o, d, t0, t1, rng, t)) return false;
+    pOut = o + d * t;
+    return true;
+}
+__device__ __forceinline__ float evalTransmittanceGrid(const MedView &M, f3 o, f3 d, float maxt, VRng &rng) {
+    float t0, t1, t;
+    if (!medClip(M, o, d, 0.0f, maxt, t0, t1) || !(t0 < t1)) return 1.0f;
+    float result = 0;
+    for (int i = 0; i < 2; ++i)
+        if (!trackGrid(M, o, d, t0, t1, rng, t)) result += 1;
+    return result * 0.5f;
+}
+
 // evalTransmittance with a sampler: mean of 2 delta-tracking survival indicators
 __device__ __forceinline__ float evalTransmittance(const MedView &M, f3 o, f3 d, float maxt, VRng &rng) {
     float t0, t1;
@@ -151,6 +230,15 @@ __device__ __forceinline__ float evalTransmittance(const MedView &M, f3 o, f3 d,
         }
     }
     return result * 0.5f;
+}
+
+__device__ __forceinline__ bool mediumSample(const VolDev &v, int m, f3 o, f3 d, float maxt, VRng &rng, f3 &p) {
+    const MedView M = medView(v.media, m);
+    return v.grid ? sampleDistanceGrid(M, o, d, maxt, rng, p) : sampleDistance(M, o, d, maxt, rng, p);
+}
+__device__ __forceinline__ float mediumTransmittance(const VolDev &v, int m, f3 o, f3 d, float maxt, VRng &rng) {
+    const MedView M = medView(v.media, m);
+    return v.grid ? evalTransmittanceGrid(M, o, d, maxt, rng) : evalTransmittance(M, o, d, maxt, rng);
 }
 
 // ---- scene queries ----------------------------------------------------------------------------
@@ -201,7 +289,7 @@ __device__ __forceinline__ float sceneTransmittance(const SceneDev &sc, const Vo
         segs++;
         if (!surface) t = __int_as_float(0x7f800000);
         if (surface && (interactions == maxInteractions || !isNullMat(sc, triBits(sc, tri)))) return 0.0f;
-        if (medium >= 0) T *= evalTransmittance(medView(v.media, medium), o, d, fminf(t, remaining), rng);
+        if (medium >= 0) T *= mediumTransmittance(v, medium, o, d, fminf(t, remaining), rng);
         if (!surface || T == 0) break;
         const uint32_t tm = v.tmed[tri];
         if (tm) {
@@ -275,7 +363,7 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
             closestHit(sc, oo, d, mt, __int_as_float(0x7f800000), tt, tr, uu, ww, stk);
             segs++;
             if (mm >= 0) {
-                T *= evalTransmittance(medView(v.media, mm), oo, d, tt, rng);
+                T *= mediumTransmittance(v, mm, oo, d, tt, rng);
                 if (T == 0) break;
             }
             const uint32_t tm = v.tmed[tr];
@@ -319,8 +407,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
     bool inMedium = false;
     f3 mp = mk1(0.f);
     if (P.medium >= 0)
-        inMedium = sampleDistance(medView(v.media, P.medium), P.o, P.d, P.its.valid ? P.its.t : __int_as_float(0x7f800000),
-                                  rng, mp);
+        inMedium = mediumSample(v, P.medium, P.o, P.d, P.its.valid ? P.its.t : __int_as_float(0x7f800000), rng, mp);
     if (inMedium) {
         // ---- medium interaction (progressive_volpath.cpp:117-196)
         if (P.depth >= maxDepth && maxDepth != -1) return false;
@@ -434,7 +521,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
 
 }  // namespace
 
-__global__ __launch_bounds__(VOL_BLOCK) void k_volpath(GParams g, SceneDev sc, VolDev v,
+__global__ __launch_bounds__(VOL_BLOCK, 2) void k_volpath(GParams g, SceneDev sc, VolDev v,
                                                        const uint32_t *__restrict__ local_pixels, uint32_t pix_begin,
                                                        uint32_t npix, uint32_t nlayers, uint32_t sample_base) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
@@ -537,44 +624,36 @@ __global__ __launch_bounds__(256) void k_medium_query(const GMedium *medium, int
     VRng rng{keys[2 * i], keys[2 * i + 1], 1};
     const f3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
     float *q = out + 4 * (size_t)i;
+    const bool grid = op >= 3, trans = op == 2 || op == 4;
     float t0, t1;
-    if (op == 1) {
-        // sampleDistance with an explicit mint (the integrator always passes 0)
-        bool ok = false;
-        float t = 0;
-        if (medClip(M, o, d, r[3], r[7], t0, t1)) {
-            t = t0;
-            for (;;) {
-                t -= logf(1 - rng.next1()) * M.invMax;
-                if (!(t < t1)) break;
-                const float density = lookupDensity(M, o + d * t) * M.scale;
-                if (density * M.invMax > rng.next1()) {
-                    ok = true;
-                    break;
-                }
+    const bool overlap = medClip(M, o, d, r[3], r[7], t0, t1);
+    // one tracking run over [t0, t1] with the explicit mint (the integrator always passes 0)
+    auto run = [&](float &tHit) -> bool {
+        if (grid) return t0 < t1 && trackGrid(M, o, d, t0, t1, rng, tHit);
+        float t = t0;
+        for (;;) {
+            t -= logf(1 - rng.next1()) * M.invMax;
+            if (!(t < t1)) return false;
+            const float density = lookupDensity(M, o + d * t) * M.scale;
+            if (density * M.invMax > rng.next1()) {
+                tHit = t;
+                return true;
             }
         }
+    };
+    float t = 0;
+    if (!trans) {
+        const bool ok = overlap && run(t);
         q[0] = ok ? 1.0f : 0.0f;
         q[1] = ok ? t : 0.0f;
         q[2] = (float)(rng.dim - 1);
         q[3] = 0;
     } else {
         float tr = 1.0f;
-        if (medClip(M, o, d, r[3], r[7], t0, t1)) {
-            // evalTransmittance restricted to [t0, t1] (mint folded into the clip)
+        if (overlap && !(grid && !(t0 < t1))) {
             float result = 0;
-            for (int k = 0; k < 2; ++k) {
-                float t = t0;
-                for (;;) {
-                    t -= logf(1 - rng.next1()) * M.invMax;
-                    if (!(t < t1)) {
-                        result += 1;
-                        break;
-                    }
-                    const float density = lookupDensity(M, o + d * t) * M.scale;
-                    if (density * M.invMax > rng.next1()) break;
-                }
-            }
+            for (int k = 0; k < 2; ++k)
+                if (!run(t)) result += 1;
             tr = result * 0.5f;
         }
         q[0] = tr;

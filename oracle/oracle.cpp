@@ -466,6 +466,7 @@ void oracle_set_volpath_eager(int32_t eager) { g_volpathEager = eager != 0; }
 //   op 1: sampleDistance            in: n x 8 rays (o, mint, d, maxt), key/sample per ray in u32 `aux` (2n)
 //                                   out: n x 4 (hit flag, t, draws used, 0)
 //   op 2: evalTransmittance         same inputs, out: n x 4 (T, draws used, 0, 0)
+//   op 3 / 4: as 1 / 2 with the majorant-grid tracking
 void oracle_medium_query(void *sp, int32_t m, int32_t op, const float *in, const uint32_t *aux, uint64_t n, float *out) {
     const Scene &S = *(const Scene *)sp;
     const Medium &M = S.media[m];
@@ -478,16 +479,17 @@ void oracle_medium_query(void *sp, int32_t m, int32_t op, const float *in, const
         SeqRng rng{Rng{aux[2 * i], aux[2 * i + 1]}};
         V3 o(r[0], r[1], r[2]), d(r[4], r[5], r[6]);
         float *q = out + 4 * i;
-        if (op == 1) {
+        const bool grid = op >= 3;
+        if (op == 1 || op == 3) {
             float t = 0;
             V3 p;
-            bool ok = M.sampleDistance(o, d, r[3], r[7], rng, t, p);
+            bool ok = M.sample(grid, o, d, r[3], r[7], rng, t, p);
             q[0] = ok ? 1.0f : 0.0f;
             q[1] = ok ? t : 0.0f;
             q[2] = (float)(rng.dim - 1);
             q[3] = 0;
         } else {
-            q[0] = M.evalTransmittance(o, d, r[3], r[7], rng);
+            q[0] = M.transmittance(grid, o, d, r[3], r[7], rng);
             q[1] = (float)(rng.dim - 1);
             q[2] = q[3] = 0;
         }

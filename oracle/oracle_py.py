@@ -95,12 +95,13 @@ class OracleScene:
         self.L.oracle_medium_query(self.h, m, 0, _p(pts), None, len(pts), _p(out))
         return out
 
-    def medium_sample(self, m, rays, keys, transmittance=False):
+    def medium_sample(self, m, rays, keys, transmittance=False, grid=False):
         """rays: n x 8 (o, mint, d, maxt); keys: n x 2 u32 (rng key, sample).  Returns n x 4."""
         rays = np.ascontiguousarray(rays, np.float32)
         keys = np.ascontiguousarray(keys, np.uint32)
         out = np.zeros((len(rays), 4), np.float32)
-        self.L.oracle_medium_query(self.h, m, 2 if transmittance else 1, _p(rays), _p(keys), len(rays), _p(out))
+        op = (2 if transmittance else 1) + (2 if grid else 0)
+        self.L.oracle_medium_query(self.h, m, op, _p(rays), _p(keys), len(rays), _p(out))
         return out
 
     def trace(self, rays, any_hit=False):

@@ -72,6 +72,13 @@ struct Medium {
     float scale = 1, invMax = 1;
     V3 albedo;
     float g = 0.8f;
+    // majorant grid (pg_config.volume_majorant = PG_MAJORANT_GRID): cell (cx, cy, cz) covers grid
+    // coordinates [c * kCell, (c + 1) * kCell) per axis; its majorant is scale * the maximum voxel
+    // over [c * kCell - 1, (c + 1) * kCell + 1] (every trilinear lookup whose base voxel lies in the
+    // cell, with one voxel of margin for the rounding of the traversal's cell boundaries)
+    static constexpr int kCell = 8;
+    int mres[3] = {1, 1, 1};
+    std::vector<float> maj;
 
     void init(const pg_medium &m) {
         for (int a = 0; a < 3; ++a) res[a] = m.res[a];
@@ -86,6 +93,24 @@ struct Medium {
         invMax = 1.0f / (m.scale * 1.0f);
         albedo = V3(m.albedo[0], m.albedo[1], m.albedo[2]);
         g = m.g;
+        for (int a = 0; a < 3; ++a) mres[a] = std::max(1, ((int)res[a] - 1 + kCell - 1) / kCell);
+        maj.assign((size_t)mres[0] * mres[1] * mres[2], 0.0f);
+        for (int cz = 0; cz < mres[2]; ++cz)
+            for (int cy = 0; cy < mres[1]; ++cy)
+                for (int cx = 0; cx < mres[0]; ++cx) {
+                    const int c[3] = {cx, cy, cz};
+                    int lo3[3], hi3[3];
+                    for (int a = 0; a < 3; ++a) {
+                        lo3[a] = std::max(0, c[a] * kCell - 1);
+                        hi3[a] = std::min((int)res[a] - 1, (c[a] + 1) * kCell + 1);
+                    }
+                    float mx = 0;
+                    for (int z = lo3[2]; z <= hi3[2]; ++z)
+                        for (int y = lo3[1]; y <= hi3[1]; ++y)
+                            for (int x = lo3[0]; x <= hi3[0]; ++x)
+                                mx = std::max(mx, data[((size_t)z * res[1] + y) * res[0] + x]);
+                    maj[((size_t)cz * mres[1] + cy) * mres[0] + cx] = mx * scale;
+                }
     }
 
     // lookupFloat: zero unless all 8 corners lie inside the grid
@@ -140,6 +165,82 @@ struct Medium {
                 return true;
             }
         }
+    }
+
+    // Delta tracking through the majorant grid over [t0, t1] (3D DDA over the cells; in each cell
+    // exponential steps at the cell's majorant mu, tentative collisions accepted with probability
+    // density / mu; an empty cell is crossed without a draw; a step past the cell's exit restarts at
+    // the exit, which the exponential's memorylessness makes exact).  Samples the same collision
+    // distribution as the single-majorant loop above with fewer lookups.
+    bool trackGrid(V3 o, V3 d, float t0, float t1, SeqRng &rng, float &tHit) const {
+        const float B = (float)kCell, inf = std::numeric_limits<float>::infinity();
+        int c[3], step[3];
+        float tNext[3], tDelta[3];
+        for (int a = 0; a < 3; ++a) {
+            const float og = o[a] * gs[a] + go[a], dg = d[a] * gs[a];
+            c[a] = std::min(std::max((int)std::floor((og + dg * t0) / B), 0), mres[a] - 1);
+            if (dg > 0) {
+                step[a] = 1;
+                tNext[a] = ((float)(c[a] + 1) * B - og) / dg;
+                tDelta[a] = B / dg;
+            } else if (dg < 0) {
+                step[a] = -1;
+                tNext[a] = ((float)c[a] * B - og) / dg;
+                tDelta[a] = -B / dg;
+            } else {
+                step[a] = 0;
+                tNext[a] = inf;
+                tDelta[a] = inf;
+            }
+        }
+        float t = t0;
+        for (;;) {
+            const float tExit = std::min(std::min(tNext[0], tNext[1]), std::min(tNext[2], t1));
+            const float mu = maj[((size_t)c[2] * mres[1] + c[1]) * mres[0] + c[0]];
+            if (mu > 0) {
+                for (;;) {
+                    const float ts = t - std::log(1 - rng.next1()) / mu;
+                    if (!(ts < tExit)) break;
+                    t = ts;
+                    const float density = lookup(o + d * t) * scale;
+                    if (density > mu * rng.next1()) {
+                        tHit = t;
+                        return true;
+                    }
+                }
+            }
+            t = std::max(t, tExit);
+            if (!(t < t1)) return false;
+            const int a = tNext[0] <= tNext[1] ? (tNext[0] <= tNext[2] ? 0 : 2) : (tNext[1] <= tNext[2] ? 1 : 2);
+            c[a] += step[a];
+            if (c[a] < 0 || c[a] >= mres[a]) return false;
+            tNext[a] += tDelta[a];
+        }
+    }
+
+    bool sampleDistanceGrid(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut) const {
+        float t0, t1;
+        if (!clip(o, d, mint, maxt, t0, t1) || !(t0 < t1)) return false;
+        if (!trackGrid(o, d, t0, t1, rng, tOut)) return false;
+        pOut = o + d * tOut;
+        return true;
+    }
+
+    float evalTransmittanceGrid(V3 o, V3 d, float mint, float maxt, SeqRng &rng) const {
+        float t0, t1;
+        if (!clip(o, d, mint, maxt, t0, t1) || !(t0 < t1)) return 1.0f;
+        float result = 0, th;
+        for (int i = 0; i < 2; ++i)
+            if (!trackGrid(o, d, t0, t1, rng, th)) result += 1;
+        return result / 2;
+    }
+
+    // dispatch on pg_config.volume_majorant
+    bool sample(bool grid, V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut) const {
+        return grid ? sampleDistanceGrid(o, d, mint, maxt, rng, tOut, pOut) : sampleDistance(o, d, mint, maxt, rng, tOut, pOut);
+    }
+    float transmittance(bool grid, V3 o, V3 d, float mint, float maxt, SeqRng &rng) const {
+        return grid ? evalTransmittanceGrid(o, d, mint, maxt, rng) : evalTransmittance(o, d, mint, maxt, rng);
     }
 
     // evalTransmittance with a sampler: the mean of 2 delta-tracking survival indicators

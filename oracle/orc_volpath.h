@@ -42,7 +42,7 @@ struct VolCounters {
 // Scene::evalTransmittance: transmittance from p1 to p2 through null surfaces and media; any
 // other surface, more than maxInteractions crossings, or a medium inconsistency gives zero
 inline float sceneTransmittance(const Scene &S, V3 p1, bool p1OnSurface, V3 p2, bool p2OnSurface, int medium,
-                                int maxInteractions, SeqRng &rng) {
+                                int maxInteractions, SeqRng &rng, bool grid) {
     V3 d = p2 - p1;
     float remaining = length(d);
     d = d / remaining;
@@ -56,7 +56,7 @@ inline float sceneTransmittance(const Scene &S, V3 p1, bool p1OnSurface, V3 p2, 
         const bool surface = S.intersectRaw(ray, t, prim);
         const pg_shape *sh = surface ? &S.shapes[S.triShape[prim]] : nullptr;
         if (surface && (interactions == maxInteractions || !(S.mats[sh->material].type & ENull))) return 0.0f;
-        if (medium >= 0) T *= S.media[medium].evalTransmittance(ray.o, ray.d, 0.0f, std::min(t, remaining), rng);
+        if (medium >= 0) T *= S.media[medium].transmittance(grid, ray.o, ray.d, 0.0f, std::min(t, remaining), rng);
         if (!surface || T == 0) break;
         // null BSDF in the discrete measure: 1
         if (isMediumTransition(*sh)) {
@@ -83,7 +83,7 @@ struct EmitterQuery {
 // rayIntersectAndLookForEmitter: `its` receives the FIRST intersection; the walk continues through
 // null surfaces (updating the medium) to find an emitter behind them
 inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInteractions, Ray ray, Its &its,
-                           EmitterQuery &q, bool lazy, VolCounters &cnt) {
+                           EmitterQuery &q, bool lazy, bool grid, VolCounters &cnt) {
     q.value = V3(0.f);
     q.emitter = -1;
     Its its2;
@@ -103,7 +103,7 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
         const float segT = surface ? cur->t : kInf;
         if (medium >= 0) {
             if (lazy) segs.push_back({ray.o, segT, medium});
-            else T *= S.media[medium].evalTransmittance(ray.o, ray.d, 0.0f, segT, rng);
+            else T *= S.media[medium].transmittance(grid, ray.o, ray.d, 0.0f, segT, rng);
         }
         if (!surface) break;
         const pg_shape &sh = S.shapes[cur->shape];
@@ -121,7 +121,7 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
     V3 Le = emitterLe(S, *cur, -ray.d);
     if (lazy && !isZero(Le)) {
         for (const Seg &s : segs) {
-            T *= S.media[s.medium].evalTransmittance(s.o, ray.d, 0.0f, s.maxt, rng);
+            T *= S.media[s.medium].transmittance(grid, s.o, ray.d, 0.0f, s.maxt, rng);
             if (T == 0) break;
         }
     }
@@ -134,6 +134,7 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
 
 inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolCounters &cnt, bool lazy) {
     const int maxDepth = cfg.max_depth;
+    const bool grid = cfg.volume_majorant == PG_MAJORANT_GRID;
     Its its;
     if (!S.intersect(ray, its)) its.t = kInf;
     cnt.segments++;
@@ -149,7 +150,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
         float mt = 0;
         V3 mp;
         const bool inMedium =
-            medium >= 0 && S.media[medium].sampleDistance(ray.o, ray.d, 0.0f, its.valid ? its.t : kInf, rng, mt, mp);
+            medium >= 0 && S.media[medium].sample(grid, ray.o, ray.d, 0.0f, its.valid ? its.t : kInf, rng, mt, mp);
         if (inMedium) {
             // ---- medium interaction (progressive_volpath.cpp:117-196)
             const Medium &M = S.media[medium];
@@ -165,7 +166,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 V3 value = sampleEmitterNoVis(S, dr, s0, s1);
                 if (dr.pdf != 0) {
                     cnt.shadow++;
-                    value = value * sceneTransmittance(S, mp, false, dr.p, true, medium, maxInter(depth), rng);
+                    value = value * sceneTransmittance(S, mp, false, dr.p, true, medium, maxInter(depth), rng, grid);
                     if (!isZero(value)) {
                         const float phaseVal = hgEval(M.g, wi, dr.d);
                         if (phaseVal != 0) L += T * value * (phaseVal * miWeightV(dr.pdf, phaseVal));
@@ -177,7 +178,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
             const V3 wo = hgSample(M.g, wi, u0, u1, phasePdf);
             ray = Ray{mp, wo, 0.0f, kInf};
             EmitterQuery q;
-            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, cnt);
+            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, grid, cnt);
             if (!its.valid) its.t = kInf;
             if (!isZero(q.value) && std::min(q.value.x, std::min(q.value.y, q.value.z)) > 0.f) {
                 const float emitterPdf = cfg.use_nee ? pdfEmitterDirect(S, q.emitter, V3(0.f), q.d, q.n, q.dist) : 0.0f;
@@ -204,7 +205,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 if (dr.pdf != 0) {
                     const int med = isMediumTransition(sh) ? targetMedium(sh, dr.d, its.geoN) : medium;
                     cnt.shadow++;
-                    value = value * sceneTransmittance(S, its.p, true, dr.p, true, med, maxInter(depth), rng);
+                    value = value * sceneTransmittance(S, its.p, true, dr.p, true, med, maxInter(depth), rng, grid);
                     if (!isZero(value)) {
                         const V3 woL = its.toLocal(dr.d);
                         const V3 bsdfVal = bsdfEval(Mt, its.wi, woL);
@@ -236,7 +237,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 continue;
             }
             EmitterQuery q;
-            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, cnt);
+            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, grid, cnt);
             if (!its.valid) its.t = kInf;
             if (!isZero(q.value)) {
                 const float emitterPdf = (cfg.use_nee && !(bs.sampledType & EDelta))

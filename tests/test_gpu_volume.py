@@ -46,12 +46,12 @@ def test_phase_and_medium_units(pg, O):
     rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
     rays[:, 7] = rng.uniform(0.5, 4.0, size=n)
     keys = rng.integers(0, 2 ** 32, size=(n, 2), dtype=np.uint32)
-    for tr in (False, True):
-        gg = dev.medium_sample(0, rays, keys, transmittance=tr)
-        cc = osc.medium_sample(0, rays, keys, transmittance=tr)
+    for tr, grid in ((False, False), (True, False), (False, True), (True, True)):
+        gg = dev.medium_sample(0, rays, keys, transmittance=tr, grid=grid)
+        cc = osc.medium_sample(0, rays, keys, transmittance=tr, grid=grid)
         col = 1 if tr else 2
         same = gg[:, col] == cc[:, col]
-        assert same.mean() > 0.999, (tr, same.mean())
+        assert same.mean() > 0.999, (tr, grid, same.mean())
         assert np.array_equal(gg[same, 0], cc[same, 0])
         if not tr:
             hit = same & (cc[:, 0] > 0.5)
@@ -107,6 +107,21 @@ def test_smoke_image_parity(pg, O):
     # same counter streams on both sides: most pixels agree to fp32 noise, not just statistically
     close = np.abs(m1 - m2) <= 1e-3 * np.maximum(np.abs(m2), 1e-3)
     assert close.mean() > 0.5, close.mean()
+
+
+def test_smoke_image_parity_global_majorant(pg, O):
+    """The reference's single-majorant tracking on the GPU against the oracle (same streams)."""
+    sc = pg.scenes.smoke(32, 32, res=48)
+    spp = 64
+    cfg = dict(volume_majorant=pg.capi.PG_MAJORANT_GLOBAL)
+    dev = make_dev(pg, sc, **cfg)
+    dev.render_pass(spp, 0)
+    g = _film(dev)
+    dev.close()
+    c = O.render(O.OracleScene(pg.capi, sc), _vol_cfg(pg, **cfg), spp)[:2]
+    m1, m2, z = _zimg(g, c)
+    assert (np.abs(z) < 5).mean() > 0.999
+    assert abs(_mean_z(g, c)) < 5
 
 
 def test_volpath_surface_scene_matches_path_gpu(pg, O):

@@ -139,6 +139,45 @@ def test_woodcock_free_flight_and_transmittance(pg, O):
     assert np.all(osc.medium_sample(0, miss, keys[:10], transmittance=True)[:, :2] == [1.0, 0.0])
 
 
+def test_majorant_grid_matches_global(pg, O):
+    """Delta tracking against the majorant grid (PG_MAJORANT_GRID) samples the same free-flight
+    distribution and transmittance as the reference's single majorant, with fewer draws."""
+    sc = pg.scenes.smoke(8, 8, res=40)
+    osc = O.OracleScene(pg.capi, sc)
+    rng = np.random.default_rng(5)
+    n = 60000
+    rays = np.zeros((n, 8), np.float32)
+    o = rng.uniform(-1.4, 1.4, size=(n, 3))
+    tgt = rng.uniform(-0.5, 0.5, size=(n, 3))
+    d = tgt - o
+    rays[:, 0:3] = o
+    rays[:, 4:7] = d / np.linalg.norm(d, axis=1, keepdims=True)
+    rays[:, 7] = np.inf
+    keys = np.stack([np.arange(n, dtype=np.uint32), np.full(n, 9, np.uint32)], 1)
+    a = osc.medium_sample(0, rays, keys)
+    b = osc.medium_sample(0, rays, keys, grid=True)
+    pa, pb = a[:, 0].mean(), b[:, 0].mean()
+    se = np.sqrt(pa * (1 - pa) / n + pb * (1 - pb) / n)
+    assert abs(pa - pb) < 5 * se
+    ha, hb = a[:, 0] > 0.5, b[:, 0] > 0.5
+    assert stats.ks_2samp(a[ha, 1], b[hb, 1]).pvalue > 1e-3
+    assert b[:, 2].mean() < 0.5 * a[:, 2].mean()  # empty space is skipped
+    ta = osc.medium_sample(0, rays, keys, transmittance=True)[:, 0]
+    tb = osc.medium_sample(0, rays, keys, transmittance=True, grid=True)[:, 0]
+    se = np.sqrt(ta.var() / n + tb.var() / n)
+    assert abs(ta.mean() - tb.mean()) < 5 * se
+
+
+def test_volpath_majorant_modes_agree(pg, O):
+    sc = pg.scenes.smoke(24, 24, res=32)
+    osc = O.OracleScene(pg.capi, sc)
+    a = O.render(osc, _vol_cfg(pg, volume_majorant=pg.capi.PG_MAJORANT_GLOBAL), 128)[:2]
+    b = O.render(osc, _vol_cfg(pg, seed=11), 128)[:2]
+    m1, m2, z = _zimg(a, b)
+    assert (np.abs(z) < 5).mean() > 0.995
+    assert abs(_mean_z(a, b)) < 5
+
+
 def _vol_cfg(pg, **kw):
     return pg.capi.default_config(integrator=pg.capi.PG_INTEGRATOR_VOLPATH, **kw)
 
