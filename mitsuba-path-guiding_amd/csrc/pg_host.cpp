@@ -445,7 +445,7 @@ pg_status validateMedium(Ctx *c, const pg_medium &pm, uint32_t m) {
     const std::string id = "pg_upload_scene: medium " + std::to_string(m) + ": ";
     if (pm.type != PG_MEDIUM_HETEROGENEOUS) return fail(c, PG_ERR_INVALID, id + "unknown type");
     if (!pm.density || pm.res[0] < 1 || pm.res[1] < 1 || pm.res[2] < 1 ||
-        (uint64_t)pm.res[0] * pm.res[1] * pm.res[2] > (1ull << 32))
+        (uint64_t)pm.res[0] * pm.res[1] * pm.res[2] > (1ull << 30))
         return fail(c, PG_ERR_INVALID, id + "bad density grid");
     double diag2 = 0;
     for (int a = 0; a < 3; ++a) {
@@ -764,19 +764,36 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||
         (s = upload(c, c->emcdf, emcdf)) || (s = upload(c, c->tmed, tmed)))
         return s;
-    // densities: one buffer, each grid 256-B aligned
+    // densities: one buffer, each grid 256-B aligned (bricked, see pg_layout.h GMedium)
     {
         size_t words = 0;
         std::vector<size_t> at;
+        std::vector<float> stage;
         for (uint32_t m = 0; m < d->num_media; ++m) {
+            const pg_medium &pm = d->media[m];
             at.push_back(words);
-            words += ((size_t)d->media[m].res[0] * d->media[m].res[1] * d->media[m].res[2] + 63) & ~(size_t)63;
+            gmed[m].bx = (pm.res[0] + 3) / 4;
+            gmed[m].by = (pm.res[1] + 3) / 4;
+            const size_t n = PG_DENSITY_BRICKS ? (size_t)gmed[m].bx * gmed[m].by * ((pm.res[2] + 3) / 4) * 64
+                                               : (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+            words += (n + 63) & ~(size_t)63;
         }
         HIPC(c, c->density.grow(std::max<size_t>(words * 4, 256)));
         for (uint32_t m = 0; m < d->num_media; ++m) {
-            const size_t n = (size_t)d->media[m].res[0] * d->media[m].res[1] * d->media[m].res[2];
-            HIPC(c, hipMemcpyAsync(c->density.as<float>() + at[m], d->media[m].density, n * 4, hipMemcpyHostToDevice,
-                                   c->stream));
+            const pg_medium &pm = d->media[m];
+            const size_t n = (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+            if (PG_DENSITY_BRICKS) {
+                const uint32_t bx = gmed[m].bx, by = gmed[m].by, bz = (pm.res[2] + 3) / 4;
+                stage.assign((size_t)bx * by * bz * 64, 0.0f);
+                for (uint32_t z = 0; z < pm.res[2]; ++z)
+                    for (uint32_t y = 0; y < pm.res[1]; ++y)
+                        for (uint32_t x = 0; x < pm.res[0]; ++x)
+                            stage[(((size_t)(z >> 2) * by + (y >> 2)) * bx + (x >> 2)) * 64 + (z & 3) * 16 + (y & 3) * 4 +
+                                  (x & 3)] = pm.density[((size_t)z * pm.res[1] + y) * pm.res[0] + x];
+                HIPC(c, hipMemcpy(c->density.as<float>() + at[m], stage.data(), stage.size() * 4, hipMemcpyHostToDevice));
+            } else {
+                HIPC(c, hipMemcpyAsync(c->density.as<float>() + at[m], pm.density, n * 4, hipMemcpyHostToDevice, c->stream));
+            }
             gmed[m].density = c->density.as<float>() + at[m];
         }
         // majorant grids (PG_MAJORANT_GRID tracking): one buffer, per-medium offsets

@@ -41,7 +41,13 @@ static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 // (gridvolume.cpp:583-585, heterogeneous.cpp:236-242).  density: res x*y*z floats, x fastest.
 // maj: the majorant grid, mx*my*mz cells of PG_MAJORANT_CELL^3 voxels, each scale * the maximum
 // voxel over the cell extended by one voxel per side.
+// With PG_DENSITY_BRICKS = 1 the density is stored in 4x4x4-voxel bricks of 256 B (bricks x fastest,
+// bx * by bricks per z layer; inside a brick x, then y, then z): the 2x2x2 corners of a trilinear
+// lookup then touch ~2.3 cache lines instead of 4 rows of the linear layout.
 #define PG_MAJORANT_CELL 8
+#ifndef PG_DENSITY_BRICKS
+#define PG_DENSITY_BRICKS 0  // measured: no gain over the linear layout (DESIGN.md "Volumes")
+#endif
 struct GMedium {
     const float *density;
     uint32_t resx, resy;
@@ -53,8 +59,10 @@ struct GMedium {
     uint32_t my;
     float gs[3];
     uint32_t mz;
-    float go[3], pad3;
-    float albedo[3], pad4;
+    float go[3];
+    uint32_t bx;  // bricks along x (PG_DENSITY_BRICKS)
+    float albedo[3];
+    uint32_t by;  // bricks along y
     const float *maj;
     uint32_t pad5[2];
 };

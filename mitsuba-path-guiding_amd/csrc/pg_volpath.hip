@@ -15,6 +15,9 @@
 namespace {
 
 #define VOL_BLOCK TRACE_BLOCK  // the traversal stack columns assume TRACE_BLOCK threads per block
+#ifndef PG_VOL_WAVES
+#define PG_VOL_WAVES 2  // min waves per SIMD: caps the megakernel at 256 VGPRs (occupancy 2)
+#endif
 
 // Sampler::next1D / next2D over the counter RNG
 struct VRng {
@@ -61,6 +64,7 @@ struct MedView {
     const float *density;
     const float *maj;
     int rx, ry, rz;
+    int bx, by;
     int mx, my, mz;
     f3 gs, go, lo, hi;
     float scale, invMax;
@@ -79,6 +83,8 @@ __device__ __forceinline__ MedView medView(const GMedium *media, int m) {
     v.scale = G.scale;
     v.invMax = G.invMax;
     v.maj = G.maj;
+    v.bx = (int)G.bx;
+    v.by = (int)G.by;
     v.mx = (int)G.mx;
     v.my = (int)G.my;
     v.mz = (int)G.mz;
@@ -90,10 +96,22 @@ __device__ __forceinline__ float lookupDensity(const MedView &M, f3 p) {
     const int x1 = (int)floorf(px), y1 = (int)floorf(py), z1 = (int)floorf(pz);
     if (x1 < 0 || y1 < 0 || z1 < 0 || x1 + 1 >= M.rx || y1 + 1 >= M.ry || z1 + 1 >= M.rz) return 0.0f;
     const float fx = px - x1, fy = py - y1, fz = pz - z1, _fx = 1.0f - fx, _fy = 1.0f - fy, _fz = 1.0f - fz;
+#if PG_DENSITY_BRICKS
+    // per-axis (brick, in-brick) offsets of the two corner coordinates
+    const int x2 = x1 + 1, y2 = y1 + 1, z2 = z1 + 1;
+    const uint32_t ax1 = (uint32_t)((x1 >> 2) * 64 + (x1 & 3)), ax2 = (uint32_t)((x2 >> 2) * 64 + (x2 & 3));
+    const uint32_t ay1 = (uint32_t)((y1 >> 2) * M.bx * 64 + (y1 & 3) * 4), ay2 = (uint32_t)((y2 >> 2) * M.bx * 64 + (y2 & 3) * 4);
+    const uint32_t zs = (uint32_t)(M.bx * M.by * 64);
+    const uint32_t az1 = (uint32_t)(z1 >> 2) * zs + (uint32_t)(z1 & 3) * 16, az2 = (uint32_t)(z2 >> 2) * zs + (uint32_t)(z2 & 3) * 16;
+    const float *D = M.density;
+    const float d000 = D[az1 + ay1 + ax1], d001 = D[az1 + ay1 + ax2], d010 = D[az1 + ay2 + ax1], d011 = D[az1 + ay2 + ax2];
+    const float d100 = D[az2 + ay1 + ax1], d101 = D[az2 + ay1 + ax2], d110 = D[az2 + ay2 + ax1], d111 = D[az2 + ay2 + ax2];
+#else
     const size_t sy = (size_t)M.rx, sz = (size_t)M.rx * M.ry;
     const float *b = M.density + (size_t)z1 * sz + (size_t)y1 * sy + x1;
     const float d000 = b[0], d001 = b[1], d010 = b[sy], d011 = b[sy + 1];
     const float d100 = b[sz], d101 = b[sz + 1], d110 = b[sz + sy], d111 = b[sz + sy + 1];
+#endif
     return ((d000 * _fx + d001 * fx) * _fy + (d010 * _fx + d011 * fx) * fy) * _fz +
            ((d100 * _fx + d101 * fx) * _fy + (d110 * _fx + d111 * fx) * fy) * fz;
 }
@@ -521,7 +539,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
 
 }  // namespace
 
-__global__ __launch_bounds__(VOL_BLOCK, 2) void k_volpath(GParams g, SceneDev sc, VolDev v,
+__global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, SceneDev sc, VolDev v,
                                                        const uint32_t *__restrict__ local_pixels, uint32_t pix_begin,
                                                        uint32_t npix, uint32_t nlayers, uint32_t sample_base) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
