@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 4
+#define PG_ABI_VERSION 5
 
 typedef int32_t pg_status;
 enum {
@@ -183,6 +183,9 @@ typedef struct pg_config {
                                      delta tracking against per-cell maxima of 8^3-voxel blocks, skipping empty
                                      cells) or PG_MAJORANT_GLOBAL (the reference's single majorant, scale * 1,
                                      heterogeneous.cpp:589-660).  Both sample the same distributions. */
+    float distance_guiding;       /* volpath + guiding: mixing weight beta of guided free-flight sampling (weighted
+                                     delta tracking toward the SD-tree's zero-variance collision probability,
+                                     oracle/orc_volpath.h GuidedAccept); 0 = the reference's free flight. 0.25 */
 } pg_config;
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
 enum { PG_MAJORANT_GRID = 0, PG_MAJORANT_GLOBAL = 1 };
@@ -212,6 +215,7 @@ typedef struct pg_stats {
     uint64_t shade_launches;  /* material-class shading launches */
     double volume_ms;         /* device time of the volumetric path kernel (integrator = volpath) */
     uint64_t volume_launches;
+    uint64_t density_lookups; /* volpath: trilinear density-grid lookups (tentative collisions) */
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

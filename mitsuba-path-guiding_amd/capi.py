@@ -78,7 +78,8 @@ class pg_config(C.Structure):
                 ("s_tree_threshold", C.c_float), ("d_tree_threshold", C.c_float), ("d_tree_max_depth", C.c_int32),
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
-                ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32)]
+                ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
+                ("distance_guiding", C.c_float)]
 
 
 class pg_record(C.Structure):
@@ -90,7 +91,8 @@ class pg_stats(C.Structure):
     _fields_ = [("paths", C.c_uint64), ("segments", C.c_uint64), ("shadow_rays", C.c_uint64), ("records", C.c_uint64),
                 ("trace_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double), ("other_ms", C.c_double),
                 ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
-                ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64)]
+                ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64),
+                ("density_lookups", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -117,6 +119,7 @@ def default_config(**overrides):
     c.gpu_depth_cap = 1024
     c.path_lanes = 0
     c.integrator = PG_INTEGRATOR_PATH
+    c.distance_guiding = 0.25
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")
@@ -158,7 +161,7 @@ SIGNATURES = [
 ]
 
 
-PG_ABI_VERSION = 4  # include/pg_capi.h
+PG_ABI_VERSION = 5  # include/pg_capi.h
 
 
 def load_library(path=None):

@@ -135,6 +135,8 @@ struct Ctx {
     int32_t cam_medium = -1;
     uint32_t num_media = 0;
     DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
+    DevBuf vol_vtx;                     // guided volpath training vertices (48 B each)
+    uint64_t vol_vtx_cap = 0;
     uint32_t vol_cap = 0;
     uint32_t num_tris = 0, num_mats = 0;
     std::vector<GMat> host_mats;
@@ -533,6 +535,7 @@ pg_status pg_config_default(pg_config *c) {
     c->gpu_depth_cap = 1024;
     c->path_lanes = 0;
     c->integrator = PG_INTEGRATOR_PATH;
+    c->distance_guiding = 0.25f;
     return PG_OK;
 }
 
@@ -572,9 +575,9 @@ pg_status pg_create(const pg_config *cfg, void **out) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown volume_majorant");
     }
-    if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH && c->cfg.guiding) {
+    if (!(c->cfg.distance_guiding >= 0.0f && c->cfg.distance_guiding < 1.0f)) {
         delete c;
-        return fail(nullptr, PG_ERR_INVALID, "pg_create: guiding is not available with the volpath integrator");
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: distance_guiding must be in [0, 1)");
     }
     if (hipSetDevice(cfg->device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->film_order, hipEventDisableTiming) != hipSuccess ||
@@ -877,13 +880,18 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
 }
 
 // progressive_volpath: chunks of (pixel, sample) items through k_volpath, films in chunk order
-pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
+pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) {
     const uint32_t npix = (uint32_t)c->local_pixels.size();
     const uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
     const uint32_t want = (uint32_t)std::min<uint64_t>((uint64_t)npix * spp, cap);
     if (c->vol_cap < want) {
         HIPC(c, c->vol_rad.alloc((size_t)want * 16));
         c->vol_cap = want;
+    }
+    const int maxV = std::min(std::max(c->cfg.record_max_vertices, 0), 64);
+    if (rec && maxV > 0 && c->vol_vtx_cap < (uint64_t)want * maxV) {
+        HIPC(c, c->vol_vtx.alloc((size_t)want * maxV * 48));
+        c->vol_vtx_cap = (uint64_t)want * maxV;
     }
     if (!c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
     if (!c->vol_work.p) HIPC(c, c->vol_work.alloc(64));
@@ -897,7 +905,12 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
     g.max_component_value = c->cfg.max_component_value;
     g.seed = c->cfg.seed;
     g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
+    g.guiding = c->cfg.guiding;
+    g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
+    g.record = rec && maxV > 0;
+    g.max_vertices = maxV;
     const SceneDev sc = sceneView(c);
+    const SDDev sd = sdView(c);
     VolDev v{};
     v.grid = c->cfg.volume_majorant == PG_MAJORANT_GRID ? 1 : 0;
     v.media = c->media.as<GMedium>();
@@ -908,8 +921,14 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
     v.next = c->vol_work.as<uint32_t>();
     v.stats = (unsigned long long *)(c->vol_work.as<uint8_t>() + 16);
     v.stack_ovf = c->vol_ovf.as<uint32_t>();
+    v.vtx = g.record ? c->vol_vtx.as<float4>() : nullptr;
+    v.vtx_P = want;
+    v.dist_beta = c->cfg.distance_guiding;
     PathDev pv{};
     pv.rad = v.rad;
+    pv.vtx = v.vtx;
+    pv.P = want;
+    pv.pinfo = nullptr;  // k_commit reads the vertex count from rad[item].w
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix), pixPer = std::min(npix, want);
     std::vector<EventPair> evs;
     for (uint32_t layer = 0; layer < spp;) {
@@ -922,8 +941,24 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
             HIPC(c, hipEventCreate(&e.b));
             evs.push_back(e);
             HIPC(c, hipEventRecord(e.a, c->stream));
-            pg_launch_volpath(c->stream, g, sc, v, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_offset + layer);
+            pg_launch_volpath(c->stream, g, sc, v, sd, c->d_local_pixels.as<uint32_t>(), pb, np, nl,
+                              sample_offset + layer);
             HIPC(c, hipEventRecord(e.b, c->stream));
+            if (g.record) {
+                const uint64_t items = (uint64_t)np * nl, add = items * (uint64_t)maxV;
+                if (c->rec_bound + add > c->rec_capacity) {
+                    unsigned long long rc = 0;
+                    HIPC(c, hipStreamSynchronize(c->stream));
+                    HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
+                    c->stats.records += rc - c->rec_host_count;
+                    c->rec_host_count = c->rec_bound = rc;
+                    pg_status st;
+                    if ((st = ensureRecords(c, rc + add))) return st;
+                }
+                c->rec_bound += add;
+                pg_launch_commit(c->stream, pv, (uint32_t)items, maxV, c->records.as<pg_record>(),
+                                 c->rec_count.as<unsigned long long>(), c->rec_capacity);
+            }
             pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
                            c->film_sq.as<float4>());
             HIPC(c, hipGetLastError());
@@ -932,10 +967,17 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset) {
         layer += nl;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
-    unsigned long long st[2];
-    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 16, hipMemcpyDeviceToHost));
+    unsigned long long st[3];
+    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 24, hipMemcpyDeviceToHost));
     c->stats.segments += st[0];
     c->stats.shadow_rays += st[1];
+    c->stats.density_lookups += st[2];
+    if (g.record) {
+        unsigned long long rc = 0;
+        HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
+        c->stats.records += rc - c->rec_host_count;
+        c->rec_host_count = c->rec_bound = rc;
+    }
     for (EventPair &e : evs) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, e.a, e.b);
@@ -955,7 +997,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     HIPC(c, hipSetDevice(c->cfg.device));
     const uint32_t npix = (uint32_t)c->local_pixels.size();
     if (npix == 0 || spp == 0) return PG_OK;
-    if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH) return renderVolpath(c, spp, sample_offset);
+    if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH) return renderVolpath(c, spp, sample_offset, record && c->cfg.guiding);
     const bool rec = record && c->cfg.guiding;
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
     uint64_t total = (uint64_t)npix * spp;

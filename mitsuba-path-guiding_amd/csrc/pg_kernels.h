@@ -51,8 +51,11 @@ struct VolDev {
     int32_t grid;              // 1: majorant-grid tracking, 0: the global majorant
     float4 *rad;               // per work item (layer-major: item = layer * npix + lp), radiance
     uint32_t *next;            // work counter (zeroed by the launcher)
-    unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries
+    unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries, [2] density lookups
     uint32_t *stack_ovf;       // pg_stack_overflow_words(0) words
+    float4 *vtx;               // guided training vertices [max_vertices][vtx_P][3] (PathDev::vtx layout)
+    uint32_t vtx_P;            // slot stride of vtx (>= items per launch)
+    float dist_beta;           // pg_config.distance_guiding
 };
 
 // Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).
@@ -86,11 +89,12 @@ void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const Scene
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);
 void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
                     uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq);
+// p.pinfo == nullptr: the vertex count of slot i is bits(p.rad[i].w) (volpath items)
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
                       unsigned long long *rec_count, unsigned long long rec_capacity);
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n);
 // one volpath sample per (pixel, layer) item of the chunk, written to v.rad[item]
-void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v,
+void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                        const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
                        uint32_t sample_base);
 void pg_launch_phase_query(hipStream_t s, const GMedium *medium, const float *in, const float *wog, uint32_t n,

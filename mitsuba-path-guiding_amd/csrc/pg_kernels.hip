@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int 
                                                 unsigned long long capacity) {
     uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t nv = 0;
-    if (slot < nslots) nv = min(p.pinfo[slot].w, (uint32_t)maxV);
+    if (slot < nslots) nv = min(p.pinfo ? p.pinfo[slot].w : __float_as_uint(p.rad[slot].w), (uint32_t)maxV);
     // wave inclusive scan of nv
     int lane = threadIdx.x & 63;
     uint32_t incl = nv;

@@ -22,6 +22,7 @@ namespace {
 // Sampler::next1D / next2D over the counter RNG
 struct VRng {
     uint32_t key, sample, dim;
+    uint32_t lookups;  // density-grid lookups of this path (statistics)
     __device__ __forceinline__ float next1() { return rng1(key, sample, dim++); }
     __device__ __forceinline__ void next2(float &a, float &b) { rng2(key, sample, dim++, a, b); }
 };
@@ -140,8 +141,20 @@ __device__ __forceinline__ bool medClip(const MedView &M, f3 o, f3 d, float mint
     t1 = fminf(farT, maxt);
     return true;
 }
+// Tentative-collision rules: accept(p, density, mu, u).  The reference's (heterogeneous.cpp:640)
+// for the global majorant and its majorant-grid equivalent; AcceptGuided (below) is the weighted
+// rule of guided free flight.
+struct AcceptGlobal {
+    float invMax;
+    __device__ __forceinline__ bool operator()(f3, float density, float, float u) const { return density * invMax > u; }
+};
+struct AcceptGrid {
+    __device__ __forceinline__ bool operator()(f3, float density, float mu, float u) const { return density > mu * u; }
+};
+
 // Woodcock tracking: true with the collision point (sampleDistance, 'woodcock' branch)
-__device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, float maxt, VRng &rng, f3 &pOut) {
+template <class Accept>
+__device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, float maxt, VRng &rng, f3 &pOut, Accept &acc) {
     float t0, t1;
     if (!medClip(M, o, d, 0.0f, maxt, t0, t1)) return false;
     float t = t0;
@@ -150,7 +163,8 @@ __device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, flo
         if (!(t < t1)) return false;
         const f3 p = o + d * t;
         const float density = lookupDensity(M, p) * M.scale;
-        if (density * M.invMax > rng.next1()) {
+        rng.lookups++;
+        if (acc(p, density, M.scale, rng.next1())) {
             pOut = p;
             return true;
         }
@@ -159,7 +173,9 @@ __device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, flo
 // Delta tracking through the majorant grid over [t0, t1] (oracle/orc_medium.h trackGrid): a 3D DDA
 // over PG_MAJORANT_CELL^3-voxel cells; exponential steps at the cell majorant, restarted at each
 // cell exit (memoryless); empty cells cost no draw and no lookup.
-__device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0, float t1, VRng &rng, float &tHit) {
+template <class Accept>
+__device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0, float t1, VRng &rng, float &tHit,
+                                          Accept &acc) {
     const float B = (float)PG_MAJORANT_CELL, inf = __int_as_float(0x7f800000);
     const f3 og = mk(o.x * M.gs.x + M.go.x, o.y * M.gs.y + M.go.y, o.z * M.gs.z + M.go.z);
     const f3 dg = mk(d.x * M.gs.x, d.y * M.gs.y, d.z * M.gs.z);
@@ -193,8 +209,10 @@ __device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0
                 const float ts = t - logf(1 - rng.next1()) / mu;
                 if (!(ts < tExit)) break;
                 t = ts;
-                const float density = lookupDensity(M, o + d * t) * M.scale;
-                if (density > mu * rng.next1()) {
+                const f3 p = o + d * t;
+                const float density = lookupDensity(M, p) * M.scale;
+                rng.lookups++;
+                if (acc(p, density, mu, rng.next1())) {
                     tHit = t;
                     return true;
                 }
@@ -213,10 +231,15 @@ __device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0
         if (c[0] < 0 || c[1] < 0 || c[2] < 0 || c[0] >= n[0] || c[1] >= n[1] || c[2] >= n[2]) return false;
     }
 }
-__device__ __forceinline__ bool sampleDistanceGrid(const MedView &M, f3 o, f3 d, float maxt, VRng &rng, f3 &pOut) {
+__device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0, float t1, VRng &rng, float &tHit) {
+    AcceptGrid acc;
+    return trackGrid(M, o, d, t0, t1, rng, tHit, acc);
+}
+template <class Accept>
+__device__ __forceinline__ bool sampleDistanceGrid(const MedView &M, f3 o, f3 d, float maxt, VRng &rng, f3 &pOut, Accept &acc) {
     float t0, t1, t;
     if (!medClip(M, o, d, 0.0f, maxt, t0, t1) || !(t0 < t1)) return false;
-    if (!trackGrid(M, o, d, t0, t1, rng, t)) return false;
+    if (!trackGrid(M, o, d, t0, t1, rng, t, acc)) return false;
     pOut = o + d * t;
     return true;
 }
@@ -244,6 +267,7 @@ __device__ __forceinline__ float evalTransmittance(const MedView &M, f3 o, f3 d,
             }
             const f3 p = o + d * t;
             const float density = lookupDensity(M, p) * M.scale;
+            rng.lookups++;
             if (density * M.invMax > rng.next1()) break;
         }
     }
@@ -252,7 +276,60 @@ __device__ __forceinline__ float evalTransmittance(const MedView &M, f3 o, f3 d,
 
 __device__ __forceinline__ bool mediumSample(const VolDev &v, int m, f3 o, f3 d, float maxt, VRng &rng, f3 &p) {
     const MedView M = medView(v.media, m);
-    return v.grid ? sampleDistanceGrid(M, o, d, maxt, rng, p) : sampleDistance(M, o, d, maxt, rng, p);
+    if (v.grid) {
+        AcceptGrid acc;
+        return sampleDistanceGrid(M, o, d, maxt, rng, p, acc);
+    }
+    AcceptGlobal acc{M.invMax};
+    return sampleDistance(M, o, d, maxt, rng, p, acc);
+}
+
+// Guided free flight (pg_config.distance_guiding = beta; oracle/orc_volpath.h GuidedAccept):
+// weighted delta tracking toward P_g = sigma_s s / (sigma_s s + sigma_n x), x = 4 pi p_guide(x, d),
+// s = |g| x + (1 - |g|): the zero-variance collision probability with the SD-tree's incident
+// radiance for the unknowns; the path weight takes P_std / P (collision) or (1 - P_std) / (1 - P)
+// (null collision).  The D-tree pdf of the (fixed) flight direction is re-walked only when the
+// S-tree leaf changes.
+struct AcceptGuided {
+    SDView sv;
+    const uint4 *meta;
+    float beta, albedo, invMax;  // invMax > 0: global majorant
+    float gAbs;
+    float cu, cv;
+    float w;
+    uint32_t lastDt;
+    float lastPg;
+    __device__ __forceinline__ bool operator()(f3 p, float density, float mu, float u) {
+        float pStd = invMax > 0 ? density * invMax : density / mu;
+        pStd = fminf(fmaxf(pStd, 0.0f), 1.0f);
+        const uint32_t dt = sdLookup(sv, p);
+        if (dt != lastDt) {
+            lastDt = dt;
+            lastPg = sdPdfCanon(sv, meta[dt], cu, cv);
+        }
+        const float x = 12.566370614359172f * lastPg;
+        const float sS = albedo * density * (gAbs * x + (1 - gAbs)), sN = fmaxf(mu - density, 0.0f);
+        const float den = sS + sN * x;
+        const float pG = den > 0 ? sS / den : pStd;
+        const float P = (1 - beta) * pStd + beta * pG;
+        if (u < P) {
+            w *= pStd / P;
+            return true;
+        }
+        w *= (1 - pStd) / (1 - P);
+        return false;
+    }
+};
+__device__ __forceinline__ bool mediumSampleGuided(const VolDev &v, const SDDev &sd, int m, f3 o, f3 d, float maxt,
+                                                   VRng &rng, f3 &p, float &w) {
+    const MedView M = medView(v.media, m);
+    const GMedium &GM = v.media[m];
+    AcceptGuided acc{sdv(sd), sd.meta, v.dist_beta, (GM.albedo[0] + GM.albedo[1] + GM.albedo[2]) * (1.0f / 3.0f),
+                     v.grid ? 0.0f : M.invMax, fabsf(GM.g), 0.0f, 0.0f, 1.0f, 0xFFFFFFFFu, 0.0f};
+    dirToCanonical(d, acc.cu, acc.cv);
+    const bool hit = v.grid ? sampleDistanceGrid(M, o, d, maxt, rng, p, acc) : sampleDistance(M, o, d, maxt, rng, p, acc);
+    w = acc.w;
+    return hit;
 }
 __device__ __forceinline__ float mediumTransmittance(const VolDev &v, int m, f3 o, f3 d, float maxt, VRng &rng) {
     const MedView M = medView(v.media, m);
@@ -414,18 +491,45 @@ struct VPath {
     float eta;
     int medium, depth;
     bool scattered, emission;
+    uint32_t nv;  // training vertices written (GUIDED with g.record)
 };
 
-// one iteration of the Li loop; false when the path ends
-__device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, VPath &P, VRng &rng,
-                        const TStack &stk, uint32_t &segs, uint32_t &shadows) {
+// training vertex nv of this item: (x, woPdf), (T after the bounce, packed canonical wo), (L snapshot)
+__device__ __forceinline__ void writeVertex(const VolDev &v, uint32_t item, uint32_t k, f3 x, f3 wo, float woPdf, f3 Tn,
+                                            f3 L) {
+    float cu, cv;
+    dirToCanonical(wo, cu, cv);
+    float4 *vb = v.vtx + ((size_t)k * v.vtx_P + item) * 3;
+    vb[0] = f4(x, woPdf);
+    vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
+    vb[2] = f4(L, 0.0f);
+}
+
+// one iteration of the Li loop; false when the path ends.  GUIDED: SD-tree guiding at medium and
+// smooth surface vertices (one-sample MIS with the phase function / BSDF, oracle/orc_volpath.h),
+// guided free flight and training vertices; with an unbuilt tree it only writes the vertices.
+template <bool GUIDED>
+__device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                                        VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
+                                        uint32_t &shadows) {
     const int maxDepth = g.max_depth;
     if (!(P.depth <= maxDepth || maxDepth < 0) || P.depth > g.depth_cap) return false;
     const int maxInter = maxDepth - P.depth - 1;
+    const bool guiding = GUIDED && sd.built;
+    const bool record = GUIDED && g.record;
+    const float alpha = g.bsdf_fraction;
     bool inMedium = false;
     f3 mp = mk1(0.f);
-    if (P.medium >= 0)
-        inMedium = mediumSample(v, P.medium, P.o, P.d, P.its.valid ? P.its.t : __int_as_float(0x7f800000), rng, mp);
+    if (P.medium >= 0) {
+        const float maxt = P.its.valid ? P.its.t : __int_as_float(0x7f800000);
+        if (guiding && v.dist_beta > 0) {
+            float w;
+            inMedium = mediumSampleGuided(v, sd, P.medium, P.o, P.d, maxt, rng, mp, w);
+            P.T = P.T * w;
+        } else {
+            inMedium = mediumSample(v, P.medium, P.o, P.d, maxt, rng, mp);
+        }
+    }
     if (inMedium) {
         // ---- medium interaction (progressive_volpath.cpp:117-196)
         if (P.depth >= maxDepth && maxDepth != -1) return false;
@@ -433,10 +537,19 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         P.T = P.T * mk(GM.albedo[0], GM.albedo[1], GM.albedo[2]);
         const float hg = GM.g;
         const f3 wi = -P.d;
+        const SDView sv = sdv(sd);
+        uint4 meta = make_uint4(0, 0, 0, 0);
+        if (guiding) meta = sd.meta[sdLookup(sv, mp)];
+        const float alphaM = alpha + (1 - alpha) * fabsf(hg);  // anisotropy-raised phase fraction (oracle)
+        // NEE: the light sample and its transmittance now; with guiding its MIS weight waits for the
+        // D-tree pdf of the light direction, resolved in one lockstep walk with the direction (sdDual)
+        f3 neeV = mk1(0.f), dD = mk1(0.f);
+        float neePdf = 0, neePhase = 0;
+        bool neePending = false;
         if (g.use_nee) {
             float s0, s1;
             rng.next2(s0, s1);
-            f3 dD, ep;
+            f3 ep;
             float dist, pdf;
             f3 value = sampleEmitter(g, sc, mp, mk1(0.f), s0, s1, dD, dist, pdf, &ep);
             if (pdf != 0) {
@@ -444,13 +557,51 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
                 value = value * sceneTransmittance(sc, v, mp, false, ep, P.medium, maxInter, rng, stk, segs);
                 if (!isZero(value)) {
                     const float phaseVal = hgEval(hg, wi, dD);
-                    if (phaseVal != 0) P.L = P.L + P.T * value * (phaseVal * miWeight(pdf, phaseVal));
+                    if (phaseVal != 0) {
+                        if (guiding) {
+                            neeV = P.T * value * phaseVal;
+                            neePdf = pdf;
+                            neePhase = phaseVal;
+                            neePending = true;
+                        } else {
+                            P.L = P.L + P.T * value * (phaseVal * miWeight(pdf, phaseVal));
+                        }
+                    }
                 }
             }
         }
         float u0, u1, phasePdf;
         rng.next2(u0, u1);
-        const f3 wo = hgSample(hg, wi, u0, u1, phasePdf);
+        f3 wo;
+        float woPdf, pw = 1.0f;
+        if (!guiding) {
+            wo = hgSample(hg, wi, u0, u1, phasePdf);
+            woPdf = phasePdf;
+        } else {
+            int mode;  // 1: phase sample (D-tree pdf query), 2: D-tree sample
+            float bu, bw;
+            if (rng.next1() < alphaM) {
+                mode = 1;
+                wo = hgSample(hg, wi, u0, u1, phasePdf);
+                dirToCanonical(wo, bu, bw);
+            } else {
+                mode = 2;
+                rng.next2(bu, bw);
+            }
+            float au = 0, aw = 0, aPdf, dPdf, cu, cv;
+            if (neePending) dirToCanonical(dD, au, aw);
+            sdDual(sv, meta, neePending, au, aw, aPdf, true, mode == 2, bu, bw, cu, cv, dPdf);
+            if (neePending) P.L = P.L + neeV * miWeight(neePdf, alphaM * neePhase + (1 - alphaM) * aPdf);
+            if (mode == 2) {
+                wo = canonicalToDir(cu, cv);
+                phasePdf = hgEval(hg, wi, wo);
+            }
+            woPdf = alphaM * phasePdf + (1 - alphaM) * dPdf;
+            if (!(woPdf > 0)) return false;
+            pw = phasePdf / woPdf;
+        }
+        if (record && P.nv < (uint32_t)g.max_vertices) writeVertex(v, item, P.nv++, mp, wo, woPdf, P.T * pw, P.L);
+        P.T = P.T * pw;
         P.o = mp;
         P.d = wo;
         f3 value, qn;
@@ -459,7 +610,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         lookForEmitter(sc, v, P.medium, maxInter, mp, wo, 0.0f, P.its, value, qn, qdist, qem, rng, stk, segs);
         if (!isZero(value) && fminf(value.x, fminf(value.y, value.z)) > 0.f) {
             const float emitterPdf = g.use_nee ? pdfEmitter(g, sc, qem, mk1(0.f), wo, qn, qdist) : 0.0f;
-            P.L = P.L + P.T * value * (g.use_nee ? miWeight(phasePdf, emitterPdf) : 1.0f);
+            P.L = P.L + P.T * value * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
         }
         P.emission = false;
     } else {
@@ -476,10 +627,17 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         const GMat M = sc.mats[h.mat];
         const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
         const uint32_t tm = v.tmed[P.its.tri];
+        const bool guide = guiding && (M.type & ESmooth) && !(M.type & EDelta);
+        const SDView sv = sdv(sd);
+        uint4 meta = make_uint4(0, 0, 0, 0);
+        if (guide) meta = sd.meta[sdLookup(sv, h.p)];
+        f3 neeV = mk1(0.f), dD = mk1(0.f);
+        float neePdf = 0, neeBp = 0;
+        bool neePending = false;
         if (g.use_nee && (M.type & ESmooth)) {
             float s0, s1;
             rng.next2(s0, s1);
-            f3 dD, ep;
+            f3 ep;
             float dist, pdf;
             f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, dD, dist, pdf, &ep);
             if (pdf != 0) {
@@ -489,8 +647,17 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
                 if (!isZero(value)) {
                     const f3 woL = h.sh.toLocal(dD);
                     const f3 f = bsdfEval(M, h.wi, woL);
-                    if (!isZero(f) && (!g.strict_normals || dot(h.geoN, dD) * woL.z > 0))
-                        P.L = P.L + P.T * value * f * miWeight(pdf, bsdfPdf(M, h.wi, woL));
+                    if (!isZero(f) && (!g.strict_normals || dot(h.geoN, dD) * woL.z > 0)) {
+                        const float bp = bsdfPdf(M, h.wi, woL);
+                        if (guide) {
+                            neeV = P.T * value * f;
+                            neePdf = pdf;
+                            neeBp = bp;
+                            neePending = true;
+                        } else {
+                            P.L = P.L + P.T * value * f * miWeight(pdf, bp);
+                        }
+                    }
                 }
             }
         }
@@ -498,10 +665,52 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         rng.next2(b0, b1);
         const float b2 = rng.next1();
         BS bs;
-        const f3 weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+        f3 weight;
+        float woPdf;
+        if (!guide) {
+            weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+            woPdf = bs.pdf;
+        } else {
+            int mode = 0;  // 0: BSDF sample failed, 1: BSDF sample (D-tree pdf query), 2: D-tree sample
+            float bu = 0, bw = 0;
+            if (rng.next1() < alpha) {
+                weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+                if (!isZero(weight)) {
+                    mode = 1;
+                    dirToCanonical(h.sh.toWorld(bs.wo), bu, bw);
+                }
+            } else {
+                mode = 2;
+                rng.next2(bu, bw);
+            }
+            float au = 0, aw = 0, aPdf, dPdf, cu, cv;
+            if (neePending) dirToCanonical(dD, au, aw);
+            sdDual(sv, meta, neePending, au, aw, aPdf, mode != 0, mode == 2, bu, bw, cu, cv, dPdf);
+            if (neePending) P.L = P.L + neeV * miWeight(neePdf, alpha * neeBp + (1 - alpha) * aPdf);
+            if (mode == 0) return false;
+            if (mode == 1) {
+                woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
+                weight = weight * (bs.pdf / woPdf);
+            } else {
+                const f3 woL = h.sh.toLocal(canonicalToDir(cu, cv));
+                const f3 f = bsdfEval(M, h.wi, woL);
+                const float bp = bsdfPdf(M, h.wi, woL);
+                woPdf = alpha * bp + (1 - alpha) * dPdf;
+                if (!(woPdf > 0) || isZero(f)) return false;
+                weight = f / woPdf;
+                bs.wo = woL;
+                bs.pdf = bp;
+                const bool refl = h.wi.z * woL.z > 0;
+                bs.type = refl ? ((M.type & EDiffuseReflection) ? EDiffuseReflection : EGlossyReflection)
+                               : EGlossyTransmission;
+                bs.eta = refl ? 1.0f : (h.wi.z > 0 ? M.eta : M.invEta);
+            }
+        }
         if (isZero(weight)) return false;
         const f3 wo = h.sh.toWorld(bs.wo);
         if (g.strict_normals && dot(h.geoN, wo) * bs.wo.z <= 0) return false;
+        if (record && !(bs.type & EDelta) && bs.type != ENull && P.nv < (uint32_t)g.max_vertices)
+            writeVertex(v, item, P.nv++, h.p, wo, woPdf, P.T * weight, P.L);
         P.o = h.p;
         P.d = wo;
         P.T = P.T * weight;
@@ -524,7 +733,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         if (!isZero(value)) {
             const float emitterPdf =
                 (g.use_nee && !(bs.type & EDelta)) ? pdfEmitter(g, sc, qem, refN, wo, qn, qdist) : 0.0f;
-            P.L = P.L + P.T * value * (g.use_nee ? miWeight(bs.pdf, emitterPdf) : 1.0f);
+            P.L = P.L + P.T * value * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
         }
         P.emission = false;
     }
@@ -539,18 +748,19 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
 
 }  // namespace
 
-__global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, SceneDev sc, VolDev v,
+template <bool GUIDED>
+__global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, SceneDev sc, VolDev v, SDDev sd,
                                                        const uint32_t *__restrict__ local_pixels, uint32_t pix_begin,
                                                        uint32_t npix, uint32_t nlayers, uint32_t sample_base) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, v.stack_ovf);
     const uint32_t nitems = npix * nlayers;
     const int lane = threadIdx.x & 63;
-    uint32_t segs = 0, shadows = 0;
+    uint32_t segs = 0, shadows = 0, lookups = 0;
     bool alive = false, done = false;
     uint32_t item = 0;
     VPath P;
-    VRng rng{0, 0, 0};
+    VRng rng{0, 0, 0, 0};
     for (;;) {
         // refill finished lanes from the work counter (one atomic per wave)
         const unsigned long long need = __ballot(!alive && !done);
@@ -567,7 +777,7 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
                     // camera ray (PerspectiveCamera::sampleRay, perspective.cpp:271-298) + first hit
                     const uint32_t layer = item / npix, lp = item - layer * npix;
                     const uint32_t pix = local_pixels[pix_begin + lp];
-                    rng = VRng{rngKey(pix, g.seed), sample_base + layer, 1};
+                    rng = VRng{rngKey(pix, g.seed), sample_base + layer, 1, 0};
                     float jx, jy;
                     rng2(rng.key, rng.sample, 0, jx, jy);
                     const float px = (float)(pix % g.width) + jx, py = (float)(pix / g.width) + jy;
@@ -590,25 +800,29 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
                     P.depth = 1;
                     P.scattered = false;
                     P.emission = true;
+                    P.nv = 0;
                     alive = true;
                 }
             }
         }
         if (!__any(alive)) break;
-        if (alive && !volStep(g, sc, v, P, rng, stk, segs, shadows)) {
-            v.rad[item] = f4(P.L, 0.0f);
+        if (alive && !volStep<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows)) {
+            v.rad[item] = f4(P.L, __uint_as_float(P.nv));  // .w: training vertices (k_commit)
+            lookups += rng.lookups;
             alive = false;
         }
     }
     // statistics: wave sums, one atomic per wave
-    unsigned long long s0 = segs, s1 = shadows;
+    unsigned long long s0 = segs, s1 = shadows, s2 = lookups;
     for (int off = 32; off > 0; off >>= 1) {
         s0 += __shfl_xor(s0, off);
         s1 += __shfl_xor(s1, off);
+        s2 += __shfl_xor(s2, off);
     }
     if (lane == 0) {
         atomicAdd(v.stats, s0);
         atomicAdd(v.stats + 1, s1);
+        atomicAdd(v.stats + 2, s2);
     }
 }
 
@@ -639,7 +853,7 @@ __global__ __launch_bounds__(256) void k_medium_query(const GMedium *medium, int
         return;
     }
     const float *r = in + 8 * (size_t)i;
-    VRng rng{keys[2 * i], keys[2 * i + 1], 1};
+    VRng rng{keys[2 * i], keys[2 * i + 1], 1, 0};
     const f3 o = mk(r[0], r[1], r[2]), d = mk(r[4], r[5], r[6]);
     float *q = out + 4 * (size_t)i;
     const bool grid = op >= 3, trans = op == 2 || op == 4;
@@ -691,7 +905,7 @@ void pg_launch_medium_query(hipStream_t s, const GMedium *medium, int op, const 
     hipLaunchKernelGGL(k_medium_query, dim3((n + 255) / 256), dim3(256), 0, s, medium, op, in, keys, n, out);
 }
 
-void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v,
+void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                        const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
                        uint32_t sample_base) {
     const uint64_t n = (uint64_t)npix * nlayers;
@@ -699,6 +913,10 @@ void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, cons
     (void)hipMemsetAsync(v.next, 0, sizeof(uint32_t), s);
     const uint64_t want = (n + VOL_BLOCK - 1) / VOL_BLOCK;
     const uint32_t grid = (uint32_t)(want < TRACE_MAX_BLOCKS ? want : TRACE_MAX_BLOCKS);
-    hipLaunchKernelGGL(k_volpath, dim3(grid), dim3(VOL_BLOCK), 0, s, g, sc, v, local_pixels, pix_begin, npix, nlayers,
-                       sample_base);
+    if (g.guiding)
+        hipLaunchKernelGGL(k_volpath<true>, dim3(grid), dim3(VOL_BLOCK), 0, s, g, sc, v, sd, local_pixels, pix_begin,
+                           npix, nlayers, sample_base);
+    else
+        hipLaunchKernelGGL(k_volpath<false>, dim3(grid), dim3(VOL_BLOCK), 0, s, g, sc, v, sd, local_pixels, pix_begin,
+                           npix, nlayers, sample_base);
 }

@@ -6,6 +6,7 @@
     ProgressiveVolumetricPathTracer (progressive_volpath.   ProgressiveVolumetricPathTracer
       cpp:71-96)
     <guided progressive path tracer> (absent)     GuidedPathTracer
+    <guided volumetric path tracer> (absent; config C5)     GuidedVolumetricPathTracer
     Integrator::preprocess (integrator.h:61)                .preprocess(scene)
     ProgressiveMonteCarloIntegrator::render (progressive-   .render()
       integrator.cpp:170-220) / renderSamples (:65-114)
@@ -15,7 +16,7 @@
 
 Properties use the reference's XML names (maxDepth, rrDepth, strictNormals, hideEmitters, useNee,
 samplesPerProgression, maxComponentValue; guiding: trainingIterations, sTreeThreshold,
-dTreeThreshold, bsdfSamplingFraction).  Errors raise RuntimeError with pg_last_error(), like
+dTreeThreshold, bsdfSamplingFraction, distanceGuiding).  Errors raise RuntimeError with pg_last_error(), like
 Log(EError, ...) throws in Mitsuba.  There is no CPU fallback: without libpgamd.so or a gfx950
 device every entry point raises.
 """
@@ -257,7 +258,8 @@ class ProgressivePathTracer:
             bsdf_sampling_fraction=float(props.get("bsdfSamplingFraction", 0.5)),
             s_tree_threshold=float(props.get("sTreeThreshold", 12000.0)),
             d_tree_threshold=float(props.get("dTreeThreshold", 0.01)),
-            max_paths_in_flight=int(props.get("maxPathsInFlight", 0)), integrator=self.integrator)
+            max_paths_in_flight=int(props.get("maxPathsInFlight", 0)), integrator=self.integrator,
+            distance_guiding=float(props.get("distanceGuiding", 0.25)))
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         self.dev = None
         self.progression = 0
@@ -361,3 +363,13 @@ class GuidedPathTracer(ProgressivePathTracer):
         self.train()
         self.dev.reset_film()
         return super().render(spp)
+
+
+class GuidedVolumetricPathTracer(GuidedPathTracer):
+    """SD-tree guided progressive volumetric path tracer (config C5).  Training records come from
+    medium vertices and smooth surface vertices; directions at both are one-sample MIS between the
+    phase function / BSDF and the D-tree (`bsdfSamplingFraction`), and free flights use guided
+    weighted delta tracking with mixing weight `distanceGuiding` (0 = the reference's free flight;
+    oracle/orc_volpath.h GuidedAccept).  Same training schedule and exchange as GuidedPathTracer."""
+
+    integrator = capi.PG_INTEGRATOR_VOLPATH

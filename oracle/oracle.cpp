@@ -265,9 +265,10 @@ int oracle_render(void *sp, const pg_config *cfg, void *tp, uint32_t spp, uint32
                     if (cfg->integrator == PG_INTEGRATOR_VOLPATH) {
                         SeqRng srng{rng};
                         VolCounters vc;
-                        L = VolLi(S, *cfg, srng, ray, vc, !g_volpathEager);
+                        L = VolLi(S, *cfg, srng, ray, vc, !g_volpathEager, tree, rp);
                         cnt.segments += vc.segments;
                         cnt.shadow += vc.shadow;
+                        cnt.records += vc.records;
                     } else {
                         L = Li(S, *cfg, tree, rng, ray, rp, cnt);
                     }

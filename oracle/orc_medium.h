@@ -150,7 +150,10 @@ struct Medium {
     // Woodcock tracking (sampleDistance, method 'woodcock'): true with the interaction point.
     // A sample that reaches maxt fails; a NaN distance also ends the loop (no reference analogue:
     // it can only arise from 1 - u == 0, which the reference's sampler never returns).
-    bool sampleDistance(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut) const {
+    // `accept(p, density, mu, u)` decides a tentative collision at p; the reference's rule is
+    // StdAccept (density / mu > u); orc_volpath.h's guided free flight passes a weighted rule.
+    template <class Accept>
+    bool sampleDistanceA(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut, Accept &&accept) const {
         float t0, t1;
         if (!clip(o, d, mint, maxt, t0, t1)) return false;
         float t = t0;
@@ -159,12 +162,22 @@ struct Medium {
             if (!(t < t1)) return false;
             V3 p = o + d * t;
             float density = lookup(p) * scale;
-            if (density * invMax > rng.next1()) {
+            if (accept(p, density, scale, rng.next1())) {
                 tOut = t;
                 pOut = p;
                 return true;
             }
         }
+    }
+    struct StdAcceptGlobal {  // heterogeneous.cpp:640: density * m_invMaxDensity > sampler->next1D()
+        float invMax;
+        bool operator()(V3, float density, float, float u) const { return density * invMax > u; }
+    };
+    struct StdAcceptGrid {
+        bool operator()(V3, float density, float mu, float u) const { return density > mu * u; }
+    };
+    bool sampleDistance(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut) const {
+        return sampleDistanceA(o, d, mint, maxt, rng, tOut, pOut, StdAcceptGlobal{invMax});
     }
 
     // Delta tracking through the majorant grid over [t0, t1] (3D DDA over the cells; in each cell
@@ -172,7 +185,8 @@ struct Medium {
     // density / mu; an empty cell is crossed without a draw; a step past the cell's exit restarts at
     // the exit, which the exponential's memorylessness makes exact).  Samples the same collision
     // distribution as the single-majorant loop above with fewer lookups.
-    bool trackGrid(V3 o, V3 d, float t0, float t1, SeqRng &rng, float &tHit) const {
+    template <class Accept>
+    bool trackGridA(V3 o, V3 d, float t0, float t1, SeqRng &rng, float &tHit, Accept &&accept) const {
         const float B = (float)kCell, inf = std::numeric_limits<float>::infinity();
         int c[3], step[3];
         float tNext[3], tDelta[3];
@@ -202,8 +216,9 @@ struct Medium {
                     const float ts = t - std::log(1 - rng.next1()) / mu;
                     if (!(ts < tExit)) break;
                     t = ts;
-                    const float density = lookup(o + d * t) * scale;
-                    if (density > mu * rng.next1()) {
+                    const V3 p = o + d * t;
+                    const float density = lookup(p) * scale;
+                    if (accept(p, density, mu, rng.next1())) {
                         tHit = t;
                         return true;
                     }
@@ -218,12 +233,19 @@ struct Medium {
         }
     }
 
-    bool sampleDistanceGrid(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut) const {
+    bool trackGrid(V3 o, V3 d, float t0, float t1, SeqRng &rng, float &tHit) const {
+        return trackGridA(o, d, t0, t1, rng, tHit, StdAcceptGrid{});
+    }
+    template <class Accept>
+    bool sampleDistanceGridA(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut, Accept &&accept) const {
         float t0, t1;
         if (!clip(o, d, mint, maxt, t0, t1) || !(t0 < t1)) return false;
-        if (!trackGrid(o, d, t0, t1, rng, tOut)) return false;
+        if (!trackGridA(o, d, t0, t1, rng, tOut, accept)) return false;
         pOut = o + d * tOut;
         return true;
+    }
+    bool sampleDistanceGrid(V3 o, V3 d, float mint, float maxt, SeqRng &rng, float &tOut, V3 &pOut) const {
+        return sampleDistanceGridA(o, d, mint, maxt, rng, tOut, pOut, StdAcceptGrid{});
     }
 
     float evalTransmittanceGrid(V3 o, V3 d, float mint, float maxt, SeqRng &rng) const {

@@ -140,7 +140,7 @@ def test_volpath_surface_scene_matches_path_gpu(pg, O):
 def test_volpath_config_errors(pg):
     from mitsuba_path_guiding_amd.integrator import Device, PGError
     with pytest.raises(PGError):
-        Device(pg.capi.default_config(integrator=pg.capi.PG_INTEGRATOR_VOLPATH, guiding=1))
+        Device(pg.capi.default_config(integrator=pg.capi.PG_INTEGRATOR_VOLPATH, guiding=1, distance_guiding=1.0))
     with pytest.raises(PGError):
         Device(pg.capi.default_config(integrator=7))
     sc = pg.scenes.smoke(8, 8, res=8)
@@ -149,3 +149,68 @@ def test_volpath_config_errors(pg):
     with pytest.raises(PGError):
         d.upload(sc)
     d.close()
+
+
+# ---- guided volpath (GuidedVolumetricPathTracer; oracle/orc_volpath.h, PARITY UNPINNED vs the
+# reference, which has no guiding: pinned here by unbiasedness and by the oracle on injected trees)
+
+def _guided(pg, sc, beta, iters=4, spp=128, **props):
+    from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer
+    p = {"trainingIterations": iters, "sTreeThreshold": 400.0, "distanceGuiding": beta}
+    p.update(props)
+    integ = GuidedVolumetricPathTracer(p)
+    integ.preprocess(sc)
+    rgbw, sq = integ.render(spp)
+    tree = integ.dev.get_sdtree()
+    st = integ.postprocess()
+    return (rgbw, sq), st, tree
+
+
+@pytest.mark.parametrize("beta", [0.0, 0.5, 0.9])
+def test_guided_volpath_furnace_gpu(pg, beta):
+    (rgbw, sq), st, _ = _guided(pg, furnace_scene(pg), beta, iters=3, spp=128)
+    n = rgbw[..., 3:].sum()
+    m = rgbw[..., :3].sum((0, 1)) / n
+    se = np.sqrt((sq[..., :3].sum((0, 1)) / n - m ** 2) / n)
+    assert np.all(np.abs(m - 1) < 5 * se + 1e-3), (beta, m, se)
+    assert st["records"] > 0 and st["stree_nodes"] > 1
+
+
+def test_guided_smoke_gpu_matches_unguided_oracle(pg, O):
+    sc = pg.scenes.smoke(32, 32, res=48)
+    g, st, _ = _guided(pg, sc, 0.5, iters=4, spp=256)
+    c = O.render(O.OracleScene(pg.capi, sc), _vol_cfg(pg, seed=77), 256)[:2]
+    m1, m2, z = _zimg(g, c)
+    assert (np.abs(z) < 5).mean() > 0.995
+    assert abs(_mean_z(g, c)) < 5
+
+
+@pytest.mark.parametrize("beta", [0.0, 0.5])
+def test_guided_volpath_same_tree_parity(pg, O, beta):
+    """One SD-tree (trained by the oracle) injected on both sides, the same counter streams: the
+    guided GPU render and its training records against the oracle's."""
+    sc = pg.scenes.smoke(32, 32, res=48)
+    osc = O.OracleScene(pg.capi, sc)
+    cfg = _vol_cfg(pg, guiding=1, s_tree_threshold=400.0, distance_guiding=beta)
+    from test_volume_guided import train_oracle
+    otree, off = train_oracle(pg, O, osc, cfg, iters=3)
+    blob = otree.serialize()
+    dev = make_dev(pg, sc, guiding=1, s_tree_threshold=400.0, distance_guiding=beta)
+    dev.put_sdtree(blob)
+    assert np.array_equal(dev.get_sdtree(), blob)
+    spp = 64
+    dev.render_pass(spp, off, record=True)
+    g = _film(dev)
+    nrec_gpu = dev.record_count()
+    recs = dev.get_records()
+    dev.close()
+    c = O.render(osc, cfg, spp, sample_offset=off, record=True, sdtree=otree)
+    nrec_cpu = int(c[2][3])
+    m1, m2, z = _zimg(g, c[:2])
+    assert (np.abs(z) < 5).mean() > 0.999
+    assert abs(_mean_z(g, c[:2])) < 5
+    close = np.abs(m1 - m2) <= 1e-3 * np.maximum(np.abs(m2), 1e-3)
+    assert close.mean() > 0.5, close.mean()
+    assert abs(nrec_gpu - nrec_cpu) <= 0.01 * nrec_cpu, (nrec_gpu, nrec_cpu)
+    r = np.frombuffer(recs.tobytes(), np.float32).reshape(-1, 8)
+    assert np.all(np.isfinite(r[:, [0, 1, 2, 4, 5]])) and np.all(r[:, 5] > 0)
