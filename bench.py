@@ -14,6 +14,7 @@ CPU oracle timed on a bounded sample of the same job (kind "port"), plus the equ
 between GPU and CPU on that sample.
 
   python bench.py [--gpus N --steps K --warmup W] [--spp 1024] [--no-cpu] [--quick]
+  python bench.py --scene smoke      # C5: the guided volumetric job on the 256^3 smoke cloud at 1024^2
 """
 import argparse
 import json
@@ -32,6 +33,7 @@ BYTES_TRACE_PER_RAY = 52      # queue id 4 + ray o/tmin 16 + ray d/tmax 16 + hit
 BYTES_SHADOW_PER_RAY = 84     # queue id 4 + shadow ray 32 + contribution 16 + radiance RMW 32
 BYTES_SHADE_PER_VERTEX = 488  # path state read 96 + write 96 + tri gather 80 + material 32 + shadow write 48
 #                               + emitter-tri gather 80 + training vertex 48 + queue writes 8
+BYTES_DENSITY_LOOKUP = 32     # k_volpath (C5): one trilinear lookup gathers 8 f32 voxels
 
 
 def parse():
@@ -40,8 +42,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="ajar_door")
-    ap.add_argument("--width", type=int, default=1280)
-    ap.add_argument("--height", type=int, default=720)
+    ap.add_argument("--width", type=int, default=None, help="default 1280 (C3), 1024 (C5 smoke)")
+    ap.add_argument("--height", type=int, default=None, help="default 720 (C3), 1024 (C5 smoke)")
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--train", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
@@ -53,12 +55,17 @@ def parse():
 
 def main():
     a = parse()
+    vol = a.scene == "smoke"  # C5: guided volumetric path tracer on the smoke cloud
+    if a.width is None:
+        a.width = 1024 if vol else 1280
+    if a.height is None:
+        a.height = 1024 if vol else 720
     if a.quick:
         a.width, a.height, a.spp, a.steps, a.warmup = 320, 180, 64, 1, 1
     import pgload
     pg = pgload.load()
     from mitsuba_path_guiding_amd import distributed as D
-    from mitsuba_path_guiding_amd.integrator import GuidedPathTracer
+    from mitsuba_path_guiding_amd.integrator import GuidedPathTracer, GuidedVolumetricPathTracer
 
     rank, world, local = D.env_rank()
     world = max(world, 1)
@@ -75,8 +82,9 @@ def main():
     # postprogression exchange: all-reduce of the SD-tree building statistics
     exchange = D.make_exchange(on_dev, mode=a.exchange) if world > 1 else None
     # one progression for the final render (the device chunks it into waves of <= 4M paths)
-    integ = GuidedPathTracer({"trainingIterations": a.train, "samplesPerProgression": a.spp}, device=device,
-                             rank=rank, world_size=world, exchange=exchange)
+    Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
+    integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp}, device=device,
+                   rank=rank, world_size=world, exchange=exchange)
     integ.preprocess(scene)
     dev = integ.dev
 
@@ -108,12 +116,20 @@ def main():
 
     # ---- timed-region pipeline figure: algorithmic bytes of trace + shade + shadow per wall second
     d = {k: s1[k] - s0[k] for k in s1}
-    pipe_bytes = d["segments"] * (BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX) + d["shadow_rays"] * BYTES_SHADOW_PER_RAY
-    pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
-                "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
-                "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
-                "note": "all path kernels over the timed wall clock (3 path lanes run concurrently)"}
-    roofline = kernel_roofline(pg, scene, integ, device, a)
+    if vol:
+        pipe_bytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
+        pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
+                    "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
+                    "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
+                    "note": "density-grid gathers of k_volpath over the timed wall clock"}
+        roofline = volume_roofline(d)
+    else:
+        pipe_bytes = d["segments"] * (BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX) + d["shadow_rays"] * BYTES_SHADOW_PER_RAY
+        pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
+                    "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
+                    "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
+                    "note": "all path kernels over the timed wall clock (3 path lanes run concurrently)"}
+        roofline = kernel_roofline(pg, scene, integ, device, a)
 
     # ---- CPU baseline (oracle, rank 0, N = 1, bounded sample) + equal-spp RMSE on the sample
     cpu = None
@@ -127,7 +143,8 @@ def main():
             "value": round(value, 3), "unit": "Mpaths/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"C3 {a.scene} {a.width}x{a.height}, guided SD-tree, {a.train} training "
+            "config": {"workload": f"{'C5' if vol else 'C3'} {a.scene} {a.width}x{a.height}, guided SD-tree"
+                                   f"{' volpath (phase MIS + guided free flight)' if vol else ''}, {a.train} training "
                                    f"iterations (1..{2 ** (a.train - 1)} spp) + {a.spp} spp render",
                        "scene": a.scene, "triangles": scene.num_triangles, "width": a.width, "height": a.height,
                        "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
@@ -137,7 +154,8 @@ def main():
             "cpu_baseline": cpu,
             "rmse_vs_cpu": rmse,
             "segments_per_path": round(d["segments"] / max(d["paths"], 1), 3),
-            "kernel_event_ms_per_step": {k: round(d[k] / a.steps, 2) for k in ("trace_ms", "shade_ms", "shadow_ms")},
+            "kernel_event_ms_per_step": {k: round(d[k] / a.steps, 2)
+                                         for k in (("volume_ms",) if vol else ("trace_ms", "shade_ms", "shadow_ms"))},
         }
         print(json.dumps(line), flush=True)
     integ.postprocess()
@@ -189,6 +207,28 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
                         for k, v in kernels.items()}}
 
 
+def volume_roofline(d):
+    """k_volpath (C5) roofline from the timed job itself: the volumetric path runs one launch at a time
+    on the context stream, so its HIP-event durations are exact.  Algorithmic bytes = density-grid
+    gathers (8 voxels x 4 B per lookup); the 64 MiB grid stays in the 256 MiB Infinity Cache, so
+    this is an on-die gather rate measured against the HBM peak."""
+    ms, launches = d["volume_ms"], max(d["volume_launches"], 1)
+    nbytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
+    achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_volpath_latest.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("kernels", {}).get("k_volpath", {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "k_volpath",
+            "algorithmic_bytes_per_launch": int(nbytes / launches), "avg_launch_ms": round(ms / launches, 4),
+            "density_lookups_per_launch": int(d["density_lookups"] / launches),
+            "measured": "timed job, HIP events around every k_volpath launch (one stream)"}
+
+
 def cpu_baseline(pg, scene, integ, a):
     """Time the oracle (CPU restatement, all host cores) on a bounded sample of the same job: the
     guided final render of the first tiles with the GPU-trained SD-tree, then compare GPU vs CPU at
@@ -201,6 +241,9 @@ def cpu_baseline(pg, scene, integ, a):
     tree = O.OracleSDTree(osc)
     tree.deserialize(integ.dev.get_sdtree())
     cfg = pg.capi.default_config(guiding=1)
+    vol = a.scene == "smoke"
+    if vol:
+        cfg = integ.cfg  # guided volpath, same parameters as the GPU job
     W = scene.width
     T = 32
     tiles = []
@@ -224,7 +267,7 @@ def cpu_baseline(pg, scene, integ, a):
     c_rgbw, _, st = O.render(osc, cfg, spp, off, sdtree=tree, pixels=pix, nthreads=cores)
     dt = time.perf_counter() - t
     cpu = {"value": round(float(st[0]) / dt / 1e6, 4), "unit": "Mpaths/s", "cores": cores, "kind": "port",
-           "sample": f"{ntiles} tiles of 32x32 ({len(pix)} px) x {spp} spp of the guided C3 final render "
+           "sample": f"{ntiles} tiles of 32x32 ({len(pix)} px) x {spp} spp of the guided {'C5' if vol else 'C3'} final render "
                      f"with the GPU-trained SD-tree ({int(st[0])} paths, {dt:.1f} s)"}
     # equal-spp GPU render of the same sample indices (fresh film; timed region is over)
     integ.dev.reset_film()

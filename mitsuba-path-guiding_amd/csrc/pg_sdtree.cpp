@@ -2,8 +2,10 @@
 #include "pg_sdtree.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
+#include <thread>
 
 namespace pgh {
 namespace {
@@ -12,6 +14,27 @@ constexpr uint32_t kMagic = 0x44534750u;  // 'PGSD'
 constexpr uint32_t kLeafMark = 0xFFFFFFFFu;
 
 inline float fixedToFloat(uint64_t x) { return (float)std::ldexp((double)x, -24); }
+
+// f(i) for i in [0, n) on up to 16 host threads, in blocks of 8 leaves.  Every D-tree is refit,
+// rebuilt and flattened independently of the others, so the result does not depend on the split.
+template <class F>
+void parallelFor(size_t n, F &&f) {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t T = std::min<size_t>(std::min(hw, 16u), (n + 63) / 64);
+    if (T <= 1) {
+        for (size_t i = 0; i < n; ++i) f(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (size_t b; (b = next.fetch_add(8)) < n;)
+            for (size_t i = b, e = std::min(n, b + 8); i < e; ++i) f(i);
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < T; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+}
 inline float total4(const float *s) { return ((s[0] + s[1]) + s[2]) + s[3]; }
 
 // bottom-up quadrant sums of a building tree (integer, exact)
@@ -82,7 +105,8 @@ void SdTree::reset(const float bmin[3], const float bmax[3]) {
 
 void SdTree::refit(uint32_t iteration, float sThreshold, float rho, int maxDepth) {
     // 1. build: building -> sampling (fp32 from the exact integer sums)
-    for (SdLeaf &L : leaves) {
+    parallelFor(leaves.size(), [&](size_t li) {
+        SdLeaf &L = leaves[li];
         propagate(L.building, 0);
         L.sampling.assign(L.building.size(), SdNodeS{});
         for (size_t i = 0; i < L.building.size(); ++i)
@@ -91,7 +115,7 @@ void SdTree::refit(uint32_t iteration, float sThreshold, float rho, int maxDepth
                 L.sampling[i].child[q] = L.building[i].child[q];
             }
         L.total = total4(L.sampling[0].sum);
-    }
+    });
     // 2. refine the S-tree: split leaves whose record count exceeds c * sqrt(2^k); children copy
     //    the D-trees and halve the count; recursion continues into the children (DFS, child0 first)
     const double thr = (double)sThreshold * std::sqrt(std::pow(2.0, (double)iteration));
@@ -118,7 +142,7 @@ void SdTree::refit(uint32_t iteration, float sThreshold, float rho, int maxDepth
         }
     }
     // 3. reset the building trees
-    for (SdLeaf &L : leaves) rebuildTopology(L, maxDepth, rho);
+    parallelFor(leaves.size(), [&](size_t li) { rebuildTopology(leaves[li], maxDepth, rho); });
     built = true;
 }
 
@@ -171,9 +195,16 @@ void SdTree::flatten(Flat &f) const {
     f.bchild.assign(4 * nb, 0);
     f.bsum.assign(4 * nb, 0);
     f.count.assign(leaves.size(), 0);
-    uint32_t sb = 0, bb = 0;
-    for (size_t i = 0; i < leaves.size(); ++i) {
+    std::vector<uint32_t> sbase(leaves.size()), bbase(leaves.size());
+    for (size_t i = 0, sb = 0, bb = 0; i < leaves.size(); ++i) {
+        sbase[i] = (uint32_t)sb;
+        bbase[i] = (uint32_t)bb;
+        sb += leaves[i].sampling.size();
+        bb += leaves[i].building.size();
+    }
+    parallelFor(leaves.size(), [&](size_t i) {
         const SdLeaf &L = leaves[i];
+        const uint32_t sb = sbase[i], bb = bbase[i];
         f.meta[4 * i + 0] = sb;
         f.meta[4 * i + 1] = bb;
         f.meta[4 * i + 2] = L.count;
@@ -189,20 +220,21 @@ void SdTree::flatten(Flat &f) const {
                 f.bsum[4 * (bb + k) + q] = L.building[k].sum[q];
             }
         f.count[i] = L.count;
-        sb += (uint32_t)L.sampling.size();
-        bb += (uint32_t)L.building.size();
-    }
+    });
 }
 
 void SdTree::absorb(const uint64_t *bsum, const uint32_t *count) {
-    size_t bb = 0;
-    for (size_t i = 0; i < leaves.size(); ++i) {
+    std::vector<size_t> bbase(leaves.size());
+    for (size_t i = 0, bb = 0; i < leaves.size(); ++i) {
+        bbase[i] = bb;
+        bb += leaves[i].building.size();
+    }
+    parallelFor(leaves.size(), [&](size_t i) {
         SdLeaf &L = leaves[i];
         for (size_t k = 0; k < L.building.size(); ++k)
-            for (int q = 0; q < 4; ++q) L.building[k].sum[q] = bsum[4 * (bb + k) + q];
+            for (int q = 0; q < 4; ++q) L.building[k].sum[q] = bsum[4 * (bbase[i] + k) + q];
         L.count = count[i];
-        bb += L.building.size();
-    }
+    });
 }
 
 // Wire format (little endian), shared with the oracle's golden vectors:
