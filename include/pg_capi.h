@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 5
+#define PG_ABI_VERSION 6
 
 typedef int32_t pg_status;
 enum {
@@ -121,6 +121,25 @@ typedef struct pg_emitter {
     float radiance[4];
 } pg_emitter;
 
+/* Environment emitter with Mitsuba 'envmap' semantics (src/emitters/envmap.cpp:100-677): a
+ * latitude-longitude RGB image (x = phi, y = theta from +Y, texel (x, y) at rgb[3 * (y * width + x)]),
+ * stored at half precision as the reference's MIP map does (SpectrumHalf, envmap.cpp:101-103;
+ * negative texels are clamped, mipmap.h:232-240), bilinear lookups with repeat in x and clamp in y
+ * (mipmap.h:503-596), importance sampling by the sin(theta)-weighted luminance CDFs of
+ * EnvironmentMap::configure (envmap.cpp:260-329) with a tent-filtered in-pixel offset
+ * (internalSampleDirection, :567-600).  to_world is the rotation part of the 'toWorld' transform,
+ * row-major (world = R * local).  It is the last emitter of the uniform emitter pick
+ * (Scene::sampleEmitterDirect, scene.cpp:871-895).  The volumetric integrator does not support it. */
+typedef struct pg_envmap {
+    uint32_t width;
+    uint32_t height;
+    const float *rgb;      /* width * height * 3, copied at upload */
+    float to_world[9];
+    float scale;           /* 'scale' (envmap.cpp:188) */
+    uint32_t pad0;
+    uint32_t pad1;
+} pg_envmap;
+
 /* Pinhole camera with Mitsuba 'perspective' semantics (src/sensors/perspective.cpp:271-298,
  * Transform::lookAt src/libcore/transform.cpp:191-214): fov along x, near/far clip. */
 typedef struct pg_camera {
@@ -152,6 +171,7 @@ typedef struct pg_scene_desc {
     const pg_medium *media;     /* num_media entries (may be NULL when 0) */
     int32_t camera_medium;      /* Sensor::getMedium, index into media or -1 */
     int32_t pad1;
+    const pg_envmap *envmap;    /* Scene::getEnvironmentEmitter (scene.h), or NULL */
 } pg_scene_desc;
 
 /* Integrator parameters (MonteCarloIntegrator props: src/librender/integrator.cpp:195-230;
@@ -186,6 +206,9 @@ typedef struct pg_config {
     float distance_guiding;       /* volpath + guiding: mixing weight beta of guided free-flight sampling (weighted
                                      delta tracking toward the SD-tree's zero-variance collision probability,
                                      oracle/orc_volpath.h GuidedAccept); 0 = the reference's free flight. 0.25 */
+    int32_t aovs;                 /* 1: accumulate the denoiser feature buffers (Denoiser::Sample albedo + normal,
+                                     include/mitsuba/render/denoiser.h:12-16) of every camera sample's first hit;
+                                     read with pg_read_aovs.  Path integrator only.  0 */
 } pg_config;
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
 enum { PG_MAJORANT_GRID = 0, PG_MAJORANT_GLOBAL = 1 };
@@ -257,6 +280,12 @@ pg_status pg_sdtree_sample(void *ctx, const float *pos, const float *u, uint64_t
  * Pixels outside this rank's tiles are zero.  Either pointer may be NULL. */
 pg_status pg_read_film(void *ctx, float *rgbw, float *sumsq);
 pg_status pg_reset_film(void *ctx);
+/* Denoiser feature buffers (pg_config.aovs = 1), the per-pixel inputs Denoiser::add averages
+ * (src/librender/denoiser.cpp:138-144): albedo: width*height*4 floats (sum of BSDF::getAlbedo at the
+ * first hit, r, g, b, sample count); normal: width*height*4 (sum of first-hit shading normals, world
+ * space, 0).  A camera ray that escapes contributes Denoiser::Sample's defaults: albedo 0, normal
+ * (0, 0, -1).  Cleared by pg_reset_film.  Either pointer may be NULL. */
+pg_status pg_read_aovs(void *ctx, float *albedo, float *normal);
 pg_status pg_get_stats(void *ctx, pg_stats *stats);
 /* Number of pixels owned by this rank (tile shard). */
 pg_status pg_local_pixel_count(void *ctx, uint64_t *count);
@@ -283,6 +312,14 @@ pg_status pg_phase_query(void *ctx, uint32_t medium, const float *in, const floa
  * op 3 / op 4: as op 1 / op 2 with PG_MAJORANT_GRID tracking (ops 1, 2 use the global majorant). */
 pg_status pg_medium_query(void *ctx, uint32_t medium, int32_t op, const float *in, const uint32_t *keys, uint64_t n,
                           float *out);
+/* Environment emitter of the uploaded scene on the device (envmap.cpp).
+ * op 0 (EnvironmentMap::sampleDirect, :516-543, from the scene's bounding-sphere centre):
+ *      in n x 2 samples; out n x 8 = d.xyz (world), pdf (solid angle), value / pdf (rgb), distance.
+ *      pdf = 0 where the sample fails.
+ * op 1 (pdfDirect, :545-556): in n x 3 world directions; out n floats (solid-angle pdf).
+ * op 2 (evalEnvironment without ray differentials, :380-410): in n x 3 world ray directions;
+ *      out n x 3 radiance. */
+pg_status pg_envmap_query(void *ctx, int32_t op, const float *in, uint64_t n, float *out);
 
 /* Rough dielectric transmittance slice of a roughplastic material, as RoughPlastic::configure
  * reduces it (roughplastic.cpp:283-299, src/bsdfs/rtrans.h setEta/setAlpha/evalDiffuse):

@@ -55,6 +55,11 @@ class pg_emitter(C.Structure):
     _fields_ = [("shape", C.c_uint32), ("pad", C.c_uint32 * 3), ("radiance", F4)]
 
 
+class pg_envmap(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("height", C.c_uint32), ("rgb", C.POINTER(C.c_float)),
+                ("to_world", C.c_float * 9), ("scale", C.c_float), ("pad0", C.c_uint32), ("pad1", C.c_uint32)]
+
+
 class pg_camera(C.Structure):
     _fields_ = [("origin", C.c_float * 3), ("target", C.c_float * 3), ("up", C.c_float * 3),
                 ("fov_x_deg", C.c_float), ("near_clip", C.c_float), ("far_clip", C.c_float),
@@ -68,7 +73,7 @@ class pg_scene_desc(C.Structure):
                 ("indices", C.POINTER(C.c_uint32)), ("shapes", C.POINTER(pg_shape)),
                 ("materials", C.POINTER(pg_material)), ("emitters", C.POINTER(pg_emitter)),
                 ("camera", pg_camera), ("media", C.POINTER(pg_medium)), ("camera_medium", C.c_int32),
-                ("pad1", C.c_int32)]
+                ("pad1", C.c_int32), ("envmap", C.POINTER(pg_envmap))]
 
 
 class pg_config(C.Structure):
@@ -79,7 +84,7 @@ class pg_config(C.Structure):
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
                 ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
-                ("distance_guiding", C.c_float)]
+                ("distance_guiding", C.c_float), ("aovs", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -120,6 +125,7 @@ def default_config(**overrides):
     c.path_lanes = 0
     c.integrator = PG_INTEGRATOR_PATH
     c.distance_guiding = 0.25
+    c.aovs = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")
@@ -149,19 +155,21 @@ SIGNATURES = [
     ("pg_sdtree_sample", C.c_int32, [VP, VP, VP, C.c_uint64, VP, VP]),
     ("pg_read_film", C.c_int32, [VP, VP, VP]),
     ("pg_reset_film", C.c_int32, [VP]),
+    ("pg_read_aovs", C.c_int32, [VP, VP, VP]),
     ("pg_get_stats", C.c_int32, [VP, C.POINTER(pg_stats)]),
     ("pg_local_pixel_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
     ("pg_trace_rays", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_bsdf_query", C.c_int32, [VP, C.c_uint32, VP, VP, VP, C.c_uint64, VP]),
     ("pg_phase_query", C.c_int32, [VP, C.c_uint32, VP, VP, C.c_uint64, VP]),
     ("pg_medium_query", C.c_int32, [VP, C.c_uint32, C.c_int32, VP, VP, C.c_uint64, VP]),
+    ("pg_envmap_query", C.c_int32, [VP, C.c_int32, VP, C.c_uint64, VP]),
     ("pg_rough_transmittance", C.c_int32, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
     ("pg_get_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_put_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32]),
 ]
 
 
-PG_ABI_VERSION = 5  # include/pg_capi.h
+PG_ABI_VERSION = 6  # include/pg_capi.h
 
 
 def load_library(path=None):

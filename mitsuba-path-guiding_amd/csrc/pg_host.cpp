@@ -15,6 +15,7 @@
 
 #include "../../include/pg_capi.h"
 #include "pg_bvh.h"
+#include "pg_envmap.h"
 #include "pg_kernels.h"
 #include "pg_layout.h"
 #include "pg_rtrans.h"
@@ -105,6 +106,7 @@ struct Lane {
     uint32_t P = 0;
     int vtx_slots = 0;
     DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
+    DevBuf aov;  // denoiser features per slot (pg_config.aovs), 2 x float4
     uint32_t *h_counts = nullptr;  // pinned: per-bounce class counts of the running chunk
     uint32_t *h_stats = nullptr;   // pinned: counters of the last finished chunk
     std::vector<EventPair> ev[2];  // kernel-timing events: running chunk / last finished chunk
@@ -130,6 +132,8 @@ struct Ctx {
     bool has_scene = false;
     GParams g{};
     DevBuf nodes, woop, wnodes, wwoop, tshade, tclass, mats, rtab, ems, emtri, emcdf;
+    DevBuf env, envtex, envtab;  // environment emitter: GEnv record, texels, CDFs + row weights
+    bool has_env = false;
     // media (volpath)
     DevBuf media, density, tmed, majorant;
     int32_t cam_medium = -1;
@@ -153,6 +157,7 @@ struct Ctx {
     EventPair timing;                 // context-stream kernel timing (splat)
     // film
     DevBuf film, film_sq;
+    DevBuf aov_albedo, aov_normal;  // per-pixel denoiser feature sums (pg_config.aovs)
     // records
     DevBuf records, rec_count;
     uint64_t rec_capacity = 0;
@@ -294,7 +299,8 @@ SceneDev sceneView(const Ctx *c) {
     return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->wnodes.as<float4>(), c->wwoop.as<float4>(),
                     c->tshade.as<float4>(), c->tclass.as<uint8_t>(),
                     c->mats.as<GMat>(),
-                    c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>()};
+                    c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>(),
+                    c->has_env ? c->env.as<GEnv>() : nullptr};
 }
 SDDev sdView(const Ctx *c) {
     SDDev s{};
@@ -316,7 +322,7 @@ PathDev pathView(const Lane *c) {
     return PathDev{c->ray_o.as<float4>(), c->ray_d.as<float4>(), c->hit.as<float4>(), c->thr.as<float4>(),
                    c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(), c->sh_o.as<float4>(),
                    c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->stack_ovf.as<uint32_t>(),
-                   c->P};
+                   c->P,                  c->aov.as<float4>()};
 }
 
 pg_status uploadSd(Ctx *c) {
@@ -393,7 +399,8 @@ pg_status ensurePaths(Ctx *c, uint32_t want) {
             HIPC(c, l.counters.alloc(kCounterWords * 4));
             HIPC(c, l.stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
         }
-        if (want <= l.P && vslots <= l.vtx_slots) continue;
+        const bool aovMissing = c->cfg.aovs && !l.aov.p;
+        if (want <= l.P && vslots <= l.vtx_slots && !aovMissing) continue;
         const uint32_t P = std::max(want, l.P);
         const int vs = std::max(vslots, l.vtx_slots);
         size_t f4 = (size_t)P * 16;
@@ -413,6 +420,7 @@ pg_status ensurePaths(Ctx *c, uint32_t want) {
         HIPC(c, l.qs.alloc(qbytes));
         HIPC(c, l.class_q.alloc((size_t)PG_NUM_CLASSES * qbytes));
         if (vs > 0) HIPC(c, l.vtx.alloc((size_t)vs * P * 48));
+        if (c->cfg.aovs) HIPC(c, l.aov.alloc((size_t)P * 16));
         l.P = P;
         l.vtx_slots = vs;
     }
@@ -575,6 +583,10 @@ pg_status pg_create(const pg_config *cfg, void **out) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown volume_majorant");
     }
+    if (c->cfg.aovs && c->cfg.integrator != PG_INTEGRATOR_PATH) {
+        delete c;
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: aovs need the path integrator");
+    }
     if (!(c->cfg.distance_guiding >= 0.0f && c->cfg.distance_guiding < 1.0f)) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: distance_guiding must be in [0, 1)");
@@ -640,6 +652,8 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     if (d->num_media && !d->media) return fail(c, PG_ERR_INVALID, "pg_upload_scene: media missing");
     if (d->camera_medium < -1 || d->camera_medium >= (int32_t)d->num_media)
         return fail(c, PG_ERR_INVALID, "pg_upload_scene: bad camera medium");
+    if (d->envmap && c->cfg.integrator != PG_INTEGRATOR_PATH)
+        return fail(c, PG_ERR_INVALID, "pg_upload_scene: the volumetric integrator does not support an environment emitter");
     std::vector<GMedium> gmed;
     std::vector<size_t> denOff;
     size_t denTotal = 0;
@@ -839,8 +853,9 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     g.far_clip = cam.far_clip;
     g.width = cam.width;
     g.height = cam.height;
-    g.num_emitters = d->num_emitters;
+    g.num_emitters = d->num_emitters + (d->envmap ? 1u : 0u);
     g.num_materials = d->num_materials;
+    g.aovs = c->cfg.aovs;
 
     // tile shard of this rank: 32x32 tiles dealt round-robin
     const uint32_t T = c->cfg.tile_size, tx = (cam.width + T - 1) / T, ty = (cam.height + T - 1) / T;
@@ -857,6 +872,12 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     HIPC(c, c->film_sq.alloc(fb));
     HIPC(c, hipMemsetAsync(c->film.p, 0, fb, c->stream));
     HIPC(c, hipMemsetAsync(c->film_sq.p, 0, fb, c->stream));
+    if (c->cfg.aovs) {
+        HIPC(c, c->aov_albedo.alloc(fb));
+        HIPC(c, c->aov_normal.alloc(fb));
+        HIPC(c, hipMemsetAsync(c->aov_albedo.p, 0, fb, c->stream));
+        HIPC(c, hipMemsetAsync(c->aov_normal.p, 0, fb, c->stream));
+    }
     HIPC(c, c->rec_count.alloc(16));
     HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 16, c->stream));
     c->rec_host_count = 0;
@@ -871,6 +892,39 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         hi = hi + ((hi - lo) * eps + eps);
         c->scene_lo[a] = lo;
         c->scene_hi[a] = hi;
+    }
+    // environment emitter (EnvironmentMap::configure + createShape, envmap.cpp:260-356)
+    c->has_env = false;
+    if (d->envmap) {
+        pgh::EnvTables et;
+        std::string err;
+        if (!pgh::buildEnvTables(*d->envmap, c->scene_lo, c->scene_hi, et, err))
+            return fail(c, PG_ERR_INVALID, "pg_upload_scene: " + err);
+        std::vector<float> tab;  // cdf_rows | cdf_cols | row_weights, each 16-B aligned
+        auto put = [&](const std::vector<float> &v) {
+            const size_t at = tab.size();
+            tab.insert(tab.end(), v.begin(), v.end());
+            tab.resize((tab.size() + 3) & ~(size_t)3, 0.0f);
+            return at;
+        };
+        const size_t oRows = put(et.cdf_rows), oCols = put(et.cdf_cols), oW = put(et.row_weights);
+        if ((s = upload(c, c->envtex, et.texels)) || (s = upload(c, c->envtab, tab))) return s;
+        GEnv ge{};
+        ge.texels = c->envtex.as<float>();
+        ge.cdf_rows = c->envtab.as<float>() + oRows;
+        ge.cdf_cols = c->envtab.as<float>() + oCols;
+        ge.row_weights = c->envtab.as<float>() + oW;
+        ge.width = et.width;
+        ge.height = et.height;
+        ge.scale = et.scale;
+        ge.normalization = et.normalization;
+        ge.pixel_size[0] = et.pixel_size[0];
+        ge.pixel_size[1] = et.pixel_size[1];
+        ge.radius = et.radius;
+        for (int a = 0; a < 3; ++a) ge.center[a] = et.center[a];
+        for (int k = 0; k < 9; ++k) ge.R[k] = et.R[k];
+        if ((s = upload(c, c->env, std::vector<GEnv>{ge}))) return s;
+        c->has_env = true;
     }
     c->sd.reset(c->scene_lo, c->scene_hi);
     if ((s = uploadSd(c))) return s;
@@ -959,7 +1013,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
                 pg_launch_commit(c->stream, pv, (uint32_t)items, maxV, c->records.as<pg_record>(),
                                  c->rec_count.as<unsigned long long>(), c->rec_capacity);
             }
-            pg_launch_film(c->stream, g, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
+            pg_launch_film(c->stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
                            c->film_sq.as<float4>());
             HIPC(c, hipGetLastError());
             c->stats.paths += (uint64_t)np * nl;
@@ -1048,7 +1102,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         classQueues(l, cb, cls);
         EventPair et = nextEvents(&l);
         HIPC(c, hipEventRecord(et.a, l.stream));
-        pg_launch_trace(l.stream, sc, pathView(&l), lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb),
+        pg_launch_trace(l.stream, g, sc, pathView(&l), lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb),
                         l.bound, cls);
         HIPC(c, hipEventRecord(et.b, l.stream));
         HIPC(c, hipMemcpyAsync(l.h_counts + (size_t)kBounceWords * l.b + kClassCounts, cb + kClassCounts,
@@ -1115,8 +1169,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         const PathDev pv = pathView(&l);
         HIPC(c, hipMemcpyAsync(l.h_stats, l.counters.p, (size_t)kBounceWords * l.b * 4, hipMemcpyDeviceToHost, l.stream));
         HIPC(c, hipStreamWaitEvent(l.stream, c->film_order, 0));
-        pg_launch_film(l.stream, g, pv, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
-                       c->film_sq.as<float4>());
+        pg_launch_film(l.stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
+                       c->film_sq.as<float4>(), c->aov_albedo.as<float4>(), c->aov_normal.as<float4>());
         if (rec) {
             // every slot can emit at most max_vertices records; grow the buffer (lanes idle) when the
             // bound could overflow it
@@ -1425,6 +1479,43 @@ pg_status pg_reset_film(void *ctx) {
     size_t fb = (size_t)c->g.width * c->g.height * 16;
     HIPC(c, hipMemsetAsync(c->film.p, 0, fb, c->stream));
     HIPC(c, hipMemsetAsync(c->film_sq.p, 0, fb, c->stream));
+    if (c->aov_albedo.p) {
+        HIPC(c, hipMemsetAsync(c->aov_albedo.p, 0, fb, c->stream));
+        HIPC(c, hipMemsetAsync(c->aov_normal.p, 0, fb, c->stream));
+    }
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_read_aovs(void *ctx, float *albedo, float *normal) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_read_aovs: null context");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_read_aovs: no scene");
+    if (!c->cfg.aovs) return fail(c, PG_ERR_STATE, "pg_read_aovs: the context was created with aovs = 0");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    size_t fb = (size_t)c->g.width * c->g.height * 16;
+    if (albedo) HIPC(c, hipMemcpyAsync(albedo, c->aov_albedo.p, fb, hipMemcpyDeviceToHost, c->stream));
+    if (normal) HIPC(c, hipMemcpyAsync(normal, c->aov_normal.p, fb, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_envmap_query(void *ctx, int32_t op, const float *in, uint64_t n, float *out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!in && n) || (!out && n)) return fail(c, PG_ERR_INVALID, "pg_envmap_query: null argument");
+    if (op < 0 || op > 2) return fail(c, PG_ERR_INVALID, "pg_envmap_query: bad op");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_envmap_query: no scene");
+    if (!c->has_env) return fail(c, PG_ERR_STATE, "pg_envmap_query: the scene has no environment emitter");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!n) return PG_OK;
+    const size_t inBytes = n * (op == 0 ? 8 : 12), outBytes = n * (op == 0 ? 32 : op == 1 ? 4 : 12);
+    DevBuf a, o;
+    HIPC(c, a.alloc(inBytes));
+    HIPC(c, o.alloc(outBytes));
+    HIPC(c, hipMemcpyAsync(a.p, in, inBytes, hipMemcpyHostToDevice, c->stream));
+    pg_launch_envmap_query(c->stream, sceneView(c), op, a.as<float>(), (uint32_t)n, o.as<float>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(out, o.p, outBytes, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }

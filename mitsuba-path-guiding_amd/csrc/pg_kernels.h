@@ -16,6 +16,7 @@ struct SceneDev {
     const GEmitter *ems;
     const float4 *emtri;    // PG_TRI_SHADE_F4 float4 per emitter triangle
     const float *emcdf;
+    const GEnv *env;        // environment emitter (the last emitter), or nullptr
 };
 
 struct PathDev {
@@ -25,6 +26,9 @@ struct PathDev {
     float4 *vtx;       // [max_vertices][P][3]
     uint32_t *stack_ovf;  // traversal-stack overflow ring, pg_stack_overflow_words(0) words
     uint32_t P;        // capacity (slot stride of vtx)
+    // denoiser features (pg_config.aovs), 1 per slot: the first hit (t, tri | ~0, u, v), written by
+    // k_camera (no hit) and k_shade (depth 1); k_film turns it into albedo + normal sums.  nullptr: off.
+    float4 *aov;
 };
 
 struct SDDev {
@@ -82,13 +86,17 @@ void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const u
 // goes to class_queues[c] (shard s -> shard s); escaped paths are only counted, in
 // class_queues[PG_NUM_CLASSES].counts.  max_shard: upper bound of the largest shard count (sizes
 // the grid; the kernels read the counts).
-void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
+void pg_launch_trace(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
                      const Queue *class_queues);
 void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
                            const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shadow);
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);
-void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
-                    uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq);
+// aov_albedo / aov_normal: per-pixel feature sums, read when p.aov is set
+void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels,
+                    uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq,
+                    float4 *aov_albedo = nullptr, float4 *aov_normal = nullptr);
+// unit-level environment-emitter queries (pg_envmap_query)
+void pg_launch_envmap_query(hipStream_t s, const SceneDev &sc, int op, const float *in, uint32_t n, float *out);
 // p.pinfo == nullptr: the vertex count of slot i is bits(p.rad[i].w) (volpath items)
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
                       unsigned long long *rec_count, unsigned long long rec_capacity);

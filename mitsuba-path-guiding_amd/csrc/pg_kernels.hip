@@ -40,7 +40,51 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     p.rad[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.prev[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.pinfo[slot] = make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u);
+    if (p.aov) p.aov[slot] = make_float4(0.f, __uint_as_float(0xFFFFFFFFu), 0.f, 0.f);  // no first hit yet
     q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
+}
+
+// BSDF::getAlbedo of the config BSDFs (diffuse.cpp:112, conductor.cpp:225, roughconductor.cpp:264,
+// dielectric.cpp:230, roughdielectric.cpp:272, plastic.cpp:266, roughplastic.cpp:354; null: the
+// BSDF default 0, bsdf.h:361).  twosided picks the nested BSDF by side, which is the same BSDF here.
+__device__ __forceinline__ f3 bsdfAlbedo(const GMat &M) {
+    const f3 diff = mk(M.diff[0], M.diff[1], M.diff[2]), spec = mk(M.spec[0], M.spec[1], M.spec[2]);
+    const f3 trans = mk(M.trans[0], M.trans[1], M.trans[2]);
+    switch (M.model) {
+        case PG_BSDF_DIFFUSE: return diff;
+        case PG_BSDF_CONDUCTOR:
+        case PG_BSDF_ROUGHCONDUCTOR: return spec;
+        case PG_BSDF_DIELECTRIC: return trans * 0.5f + spec * (1 - 0.5f);
+        case PG_BSDF_ROUGHDIELECTRIC: return spec * 0.5f + trans * (1 - 0.5f);
+        case PG_BSDF_PLASTIC: return diff * 0.5f + spec * (1 - 0.5f);
+        case PG_BSDF_ROUGHPLASTIC: return spec * 0.5f + diff * (1 - 0.5f);
+        default: return mk1(0.f);
+    }
+}
+
+// A path whose extension ray escaped (progressive_path.cpp:150-158 for the camera ray, :252-267 +
+// :276-284 after a bounce): the environment emitter's radiance, MIS-weighted against its NEE pdf.
+__device__ __forceinline__ void envEscape(const GParams &g, const SceneDev &sc, const PathDev &p, uint32_t slot,
+                                          f3 rd) {
+    const uint4 pi = p.pinfo[slot];
+    const uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16;
+    const float4 T4 = p.thr[slot];
+    f3 add;
+    if (depth == 1) {  // camera ray: the loop-top miss with EEmittedRadiance
+        if (!(flags & PF_EMITTED_QUERY) || (g.hide_emitters && !(flags & PF_SCATTERED))) return;
+        add = xyz(T4) * envEval(*sc.env, rd);
+    } else {
+        if (g.hide_emitters && !(flags & PF_SCATTERED)) return;
+        const float4 pv = p.prev[slot];
+        float w = 1.0f;
+        if (g.use_nee) {
+            const float lumPdf = (flags & PF_PREV_DELTA) ? 0.0f : envPdf(*sc.env, rd) * (1.0f / (float)g.num_emitters);
+            w = miWeight(pv.w, lumPdf);
+        }
+        add = xyz(T4) * envEval(*sc.env, rd) * w;
+    }
+    const float4 L = p.rad[slot];
+    p.rad[slot] = make_float4(L.x + add.x, L.y + add.y, L.z + add.z, L.w);
 }
 
 
@@ -70,7 +114,9 @@ __device__ __forceinline__ void classAppend(int cls, uint32_t slot, const ClassQ
     }
 }
 
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, Queue q, ClassQueues cqs) {
+// ENV: the scene has an environment emitter (escaped paths pick up its radiance)
+template <bool ENV>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, p.stack_ovf);
     const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
@@ -92,6 +138,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(SceneDev sc, PathDev p, Q
             cls = h ? (int)sc.tclass[tri] : PG_NUM_CLASSES;
         }
         classAppend(cls, slot, cqs, s);
+        if (ENV && cls == PG_NUM_CLASSES) envEscape(g, sc, p, slot, xyz(p.ray_d[slot]));
     }
 }
 
@@ -127,7 +174,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
 // MODEL >= 0 compiles only that BSDF model's code (material-class queues filled by k_trace);
 // CAN_GUIDE = false drops the SD-tree code for classes that are never guided (delta lobes).
-template <int MODEL, bool CAN_GUIDE>
+// ENV compiles in environment-emitter sampling for NEE (kept out of the other instantiations: it
+// costs 4-8 VGPRs).
+template <int MODEL, bool CAN_GUIDE, bool ENV>
 __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue in,
                                                        Queue out, Queue shq) {
     // one item per thread (a grid-stride loop here cost ~45 VGPRs of hoisted invariants): block b
@@ -188,6 +237,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
             }
             if (depth > g.depth_cap) break;
             const GMat M = sc.mats[h.mat];
+            if (p.aov && depth == 1) p.aov[slot] = hv;  // first hit, resolved into denoiser features by k_film
             if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
                 L = L + T * Le;
                 dirtyL = true;
@@ -212,7 +262,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 float s0, s1;
                 rng2(key, sample, dimOf(depth, SLOT_NEE), s0, s1);
                 float emPdf;
-                f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, neeD, neeDist, emPdf);
+                f3 value = sampleEmitter<ENV>(g, sc, h.p, refN, s0, s1, neeD, neeDist, emPdf);
                 if (!isZero(value)) {
                     f3 woL = h.sh.toLocal(neeD);
                     f3 bsdfVal = bsdfEval<MODEL>(M, h.wi, woL);
@@ -325,12 +375,32 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
 
 // film: box-filtered accumulation of every layer's sample into its pixel, in sample order
 // (ProgressiveMonteCarloIntegrator::renderBlock clamp + ImageBlock::put validity check)
-__global__ __launch_bounds__(256) void k_film(GParams g, PathDev p, const uint32_t *__restrict__ local_pixels,
+__global__ __launch_bounds__(256) void k_film(GParams g, SceneDev sc, PathDev p, const uint32_t *__restrict__ local_pixels,
                                               uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
-                                              float4 *__restrict__ film, float4 *__restrict__ sumsq) {
+                                              float4 *__restrict__ film, float4 *__restrict__ sumsq,
+                                              float4 *__restrict__ aov_albedo, float4 *__restrict__ aov_normal) {
     uint32_t lp = blockIdx.x * blockDim.x + threadIdx.x;
     if (lp >= npix) return;
     uint32_t pix = local_pixels[pix_begin + lp];
+    if (p.aov) {  // feature sums of every sample (Denoiser::add averages all of them, denoiser.cpp:138-144)
+        float4 sa = aov_albedo[pix], sn = aov_normal[pix];
+        for (uint32_t l = 0; l < nlayers; ++l) {
+            const float4 hv = p.aov[(size_t)l * npix + lp];
+            const uint32_t tri = __float_as_uint(hv.y);
+            f3 a = mk1(0.f), n = mk(0.f, 0.f, -1.f);  // Denoiser::Sample defaults (denoiser.h:12-16): escaped ray
+            if (tri != 0xFFFFFFFFu) {
+                const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
+                const float4 s1 = r[1], s3 = r[3], s4 = r[4];
+                const float b0 = 1 - hv.z - hv.w;
+                n = normalize(xyz(s3) * b0 + mk(s3.w, s4.x, s4.y) * hv.z + mk(s4.z, s4.w, s1.w) * hv.w);  // fetchHit's shN
+                a = bsdfAlbedo(sc.mats[__float_as_uint(r[0].w) & 0xFFFFu]);
+            }
+            sa = make_float4(sa.x + a.x, sa.y + a.y, sa.z + a.z, sa.w + 1.0f);
+            sn = make_float4(sn.x + n.x, sn.y + n.y, sn.z + n.z, 0.0f);
+        }
+        aov_albedo[pix] = sa;
+        aov_normal[pix] = sn;
+    }
     float4 a = film[pix], q = sumsq[pix];
     for (uint32_t l = 0; l < nlayers; ++l) {
         float4 L = p.rad[(size_t)l * npix + lp];
@@ -563,48 +633,90 @@ static inline dim3 shardGrid(uint32_t max_shard, uint32_t block, uint32_t max_ro
     const uint32_t rows = blocks(max_shard, block);
     return dim3(PG_QSHARDS * (rows < max_rows ? rows : max_rows));
 }
-void pg_launch_trace(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
+void pg_launch_trace(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
                      const Queue *class_queues) {
     if (!max_shard) return;
     ClassQueues cq;
     for (int c = 0; c <= PG_NUM_CLASSES; ++c) cq.q[c] = class_queues[c];
-    hipLaunchKernelGGL(k_trace, shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS), dim3(TRACE_BLOCK), 0,
-                       s, sc, p, q, cq);
+    const dim3 grid = shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS);
+    if (sc.env) hipLaunchKernelGGL(k_trace<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq);
+    else hipLaunchKernelGGL(k_trace<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq);
+}
+template <bool ENV>
+static void launchShade(hipStream_t s, int cls, dim3 grid, const GParams &g, const SceneDev &sc, const SDDev &sd,
+                        const PathDev &p, Queue in, Queue out, Queue shq) {
+    const dim3 block(SHADE_BLOCK);
+    switch (cls) {
+        case PG_CLASS_DIFFUSE:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_DIFFUSE, true, ENV>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_ROUGHCONDUCTOR:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHCONDUCTOR, true, ENV>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_ROUGHDIELECTRIC:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHDIELECTRIC, true, ENV>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_PLASTIC:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_PLASTIC, false, ENV>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        case PG_CLASS_ROUGHPLASTIC:
+            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHPLASTIC, true, ENV>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+            break;
+        default:  // delta lobes: conductor, dielectric (runtime switch, never guided)
+            hipLaunchKernelGGL((k_shade<-1, false, ENV>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
+    }
 }
 void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
                            const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shq) {
     if (!max_shard) return;
-    dim3 grid = shardGrid(max_shard, SHADE_BLOCK, 0xFFFFFFFFu), block(SHADE_BLOCK);
-    switch (cls) {
-        case PG_CLASS_DIFFUSE:
-            hipLaunchKernelGGL((k_shade<PG_BSDF_DIFFUSE, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
-            break;
-        case PG_CLASS_ROUGHCONDUCTOR:
-            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHCONDUCTOR, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
-            break;
-        case PG_CLASS_ROUGHDIELECTRIC:
-            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHDIELECTRIC, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
-            break;
-        case PG_CLASS_PLASTIC:
-            hipLaunchKernelGGL((k_shade<PG_BSDF_PLASTIC, false>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
-            break;
-        case PG_CLASS_ROUGHPLASTIC:
-            hipLaunchKernelGGL((k_shade<PG_BSDF_ROUGHPLASTIC, true>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
-            break;
-        default:  // delta lobes: conductor, dielectric (runtime switch, never guided)
-            hipLaunchKernelGGL((k_shade<-1, false>), grid, block, 0, s, g, sc, sd, p, in, out, shq);
-    }
+    const dim3 grid = shardGrid(max_shard, SHADE_BLOCK, 0xFFFFFFFFu);
+    if (sc.env) launchShade<true>(s, cls, grid, g, sc, sd, p, in, out, shq);
+    else launchShade<false>(s, cls, grid, g, sc, sd, p, in, out, shq);
 }
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard) {
     if (!max_shard) return;
     hipLaunchKernelGGL(k_shadow, shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS), dim3(TRACE_BLOCK), 0,
                        s, sc, p, q);
 }
-void pg_launch_film(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
-                    uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq) {
+void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
+                    uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq, float4 *aov_albedo,
+                    float4 *aov_normal) {
     if (!npix) return;
-    hipLaunchKernelGGL(k_film, dim3(blocks(npix, 256)), dim3(256), 0, s, g, p, local_pixels, pix_begin, npix, nlayers,
-                       film_rgbw, film_sumsq);
+    hipLaunchKernelGGL(k_film, dim3(blocks(npix, 256)), dim3(256), 0, s, g, sc, p, local_pixels, pix_begin, npix, nlayers,
+                       film_rgbw, film_sumsq, aov_albedo, aov_normal);
+}
+
+// op 0: sampleDirect from the bounding-sphere centre (in: n x 2 samples; out n x 8: d, pdf, value/pdf, dist)
+// op 1: pdfDirect (in: n x 3 world directions; out n); op 2: evalEnvironment (in n x 3; out n x 3)
+__global__ __launch_bounds__(256) void k_envmap_query(SceneDev sc, int op, const float *in, uint32_t n, float *out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !sc.env) return;
+    const GEnv &e = *sc.env;
+    if (op == 0) {
+        f3 d = mk1(0.f);
+        float dist = 0, pdf;
+        const f3 v = envSampleDirect(e, mk(e.center[0], e.center[1], e.center[2]), in[2 * i], in[2 * i + 1], d, dist, pdf);
+        float *o = out + 8 * (size_t)i;
+        o[0] = d.x;
+        o[1] = d.y;
+        o[2] = d.z;
+        o[3] = pdf;
+        o[4] = v.x;
+        o[5] = v.y;
+        o[6] = v.z;
+        o[7] = dist;
+    } else if (op == 1) {
+        out[i] = envPdf(e, mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+    } else {
+        const f3 v = envEval(e, mk(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+        out[3 * (size_t)i] = v.x;
+        out[3 * (size_t)i + 1] = v.y;
+        out[3 * (size_t)i + 2] = v.z;
+    }
+}
+void pg_launch_envmap_query(hipStream_t s, const SceneDev &sc, int op, const float *in, uint32_t n, float *out) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_envmap_query, dim3(blocks(n, 256)), dim3(256), 0, s, sc, op, in, n, out);
 }
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
                       unsigned long long *rec_count, unsigned long long rec_capacity) {

@@ -36,6 +36,27 @@ struct GEmitter {
 };
 static_assert(sizeof(GEmitter) == 32, "GEmitter layout");
 
+// Environment emitter record: 128 B (EnvironmentMap, envmap.cpp:260-329).  texels: width x height
+// float4 (rgb rounded to half precision, as the reference's SpectrumHalf MIP level 0; w = 0), row
+// y = theta.  cdf_rows: height + 1 marginal CDF entries; cdf_cols: height rows of width + 1
+// conditional CDF entries; row_weights: sin((y + 0.5) pi / height).  R: toWorld rotation,
+// row-major (world = R local, local = R^T world).  center/radius: the scene's bounding sphere
+// enlarged by 1.5 (EnvironmentMap::createShape, envmap.cpp:331-356).
+struct GEnv {
+    const float *texels;  // float4 per texel
+    const float *cdf_rows;
+    const float *cdf_cols;
+    const float *row_weights;
+    uint32_t width, height;
+    float scale, normalization;
+    float pixel_size[2];
+    float radius, pad0;
+    float center[3], pad1;
+    float R[9];
+    float pad2[3];
+};
+static_assert(sizeof(GEnv) == 128, "GEnv layout");
+
 // Heterogeneous medium record: 128 B (volpath).  World -> grid is g = p * gs + go
 // (gridvolume.cpp:186-198); invMax = 1 / (scale * maxFloatValue), maxFloatValue = 1
 // (gridvolume.cpp:583-585, heterogeneous.cpp:236-242).  density: res x*y*z floats, x fastest.
@@ -119,5 +140,6 @@ struct GParams {
     // integrator
     int32_t max_depth, rr_depth, use_nee, hide_emitters, strict_normals, guiding, record, max_vertices;
     float max_component_value, bsdf_fraction;
-    uint32_t seed, num_emitters, num_materials, depth_cap;
+    uint32_t seed, num_emitters, num_materials, depth_cap;  // num_emitters counts the environment emitter
+    int32_t aovs, pad_aov[3];
 };

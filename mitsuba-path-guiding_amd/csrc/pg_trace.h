@@ -333,8 +333,141 @@ __device__ __forceinline__ void fetchHit(const SceneDev &sc, uint32_t tri, float
     h.wi = h.sh.toLocal(-rd);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Environment emitter (src/emitters/envmap.cpp).  Texel lookups follow TMIPMap::evalTexel at level 0
+// (mipmap.h:503-563: repeat in x, clamp in y); the summation orders of evalBilinear (mipmap.h:575-596)
+// and internalSampleDirection / internalPdfDirection (envmap.cpp:567-633) are kept as written.
+constexpr float kInvTwoPi = 0.15915494309189533577f;
+__device__ __forceinline__ f3 envTexel(const GEnv &e, int x, int y) {
+    const int w = (int)e.width, h = (int)e.height;
+    if (x < 0 || x >= w) {  // math::modulo
+        x %= w;
+        if (x < 0) x += w;
+    }
+    y = min(max(y, 0), h - 1);
+    const float4 t = reinterpret_cast<const float4 *>(e.texels)[(size_t)y * (uint32_t)w + (uint32_t)x];
+    return mk(t.x, t.y, t.z);
+}
+__device__ __forceinline__ float envLum(f3 c) { return c.x * 0.212671f + c.y * 0.715160f + c.z * 0.072169f; }
+// Transform::inverse()(v) of the rotation (R^T v) and Transform::operator()(v) (R v)
+__device__ __forceinline__ f3 envToLocal(const GEnv &e, f3 d) {
+    return mk(e.R[0] * d.x + e.R[3] * d.y + e.R[6] * d.z, e.R[1] * d.x + e.R[4] * d.y + e.R[7] * d.z,
+              e.R[2] * d.x + e.R[5] * d.y + e.R[8] * d.z);
+}
+__device__ __forceinline__ f3 envToWorld(const GEnv &e, f3 d) {
+    return mk(e.R[0] * d.x + e.R[1] * d.y + e.R[2] * d.z, e.R[3] * d.x + e.R[4] * d.y + e.R[5] * d.z,
+              e.R[6] * d.x + e.R[7] * d.y + e.R[8] * d.z);
+}
+__device__ __forceinline__ float safeAcos(float v) { return acosf(fminf(1.0f, fmaxf(-1.0f, v))); }
+
+// EnvironmentMap::evalEnvironment without ray differentials (envmap.cpp:380-410)
+__device__ __forceinline__ f3 envEval(const GEnv &e, f3 dWorld) {
+#pragma clang fp contract(off)
+    const f3 v = envToLocal(e, dWorld);
+    const float ux = atan2f(v.x, -v.z) * kInvTwoPi, uy = safeAcos(v.y) * kInvPi;
+    if (!isfinite(ux) || !isfinite(uy)) return mk1(0.f);
+    const float u = ux * (float)e.width - 0.5f, w = uy * (float)e.height - 0.5f;
+    const int xPos = (int)floorf(u), yPos = (int)floorf(w);
+    const float dx1 = u - (float)xPos, dx2 = 1.0f - dx1, dy1 = w - (float)yPos, dy2 = 1.0f - dy1;
+    const f3 r = envTexel(e, xPos, yPos) * dx2 * dy2 + envTexel(e, xPos, yPos + 1) * dx2 * dy1 +
+                 envTexel(e, xPos + 1, yPos) * dx1 * dy2 + envTexel(e, xPos + 1, yPos + 1) * dx1 * dy1;
+    return r * e.scale;
+}
+
+// internalPdfDirection (envmap.cpp:603-633) of a local direction
+__device__ __forceinline__ float envPdfLocal(const GEnv &e, f3 d) {
+#pragma clang fp contract(off)
+    const float ux = atan2f(d.x, -d.z) * kInvTwoPi, uy = safeAcos(d.y) * kInvPi;
+    if (!isfinite(ux) || !isfinite(uy)) return 0.0f;
+    const float u = ux * (float)e.width - 0.5f, w = uy * (float)e.height - 0.5f;
+    const int xPos = (int)floorf(u), yPos = (int)floorf(w);
+    const float dx1 = u - (float)xPos, dx2 = 1.0f - dx1, dy1 = w - (float)yPos, dy2 = 1.0f - dy1;
+    const f3 v1 = envTexel(e, xPos, yPos) * dx2 * dy2 + envTexel(e, xPos + 1, yPos) * dx1 * dy2;
+    const f3 v2 = envTexel(e, xPos, yPos + 1) * dx2 * dy1 + envTexel(e, xPos + 1, yPos + 1) * dx1 * dy1;
+    const int h = (int)e.height;
+    const float sinTheta = safe_sqrt(1 - d.y * d.y);
+    return (envLum(v1) * e.row_weights[min(max(yPos, 0), h - 1)] +
+            envLum(v2) * e.row_weights[min(max(yPos + 1, 0), h - 1)]) *
+           e.normalization / fmaxf(fabsf(sinTheta), kEpsilon);
+}
+// EnvironmentMap::pdfDirect for a solid-angle record (envmap.cpp:545-556)
+__device__ __forceinline__ float envPdf(const GEnv &e, f3 dWorld) { return envPdfLocal(e, envToLocal(e, dWorld)); }
+
+// EnvironmentMap::sampleReuse (envmap.cpp:658-663): lower_bound over cdf[0..size]
+__device__ __forceinline__ uint32_t envSampleReuse(const float *cdf, uint32_t size, float &s) {
+    uint32_t lo = 0, hi = size + 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cdf[mid] < s) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t index = min((uint32_t)max((int)lo - 1, 0), size - 1);
+    s = (s - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    return index;
+}
+// warp::squareToTent's intervalToTent (warp.cpp:143-155)
+__device__ __forceinline__ float intervalToTent(float s) {
+    float sign;
+    if (s < 0.5f) {
+        sign = 1;
+        s *= 2;
+    } else {
+        sign = -1;
+        s = 2 * (s - 0.5f);
+    }
+    return sign * (1 - sqrtf(s));
+}
+// internalSampleDirection (envmap.cpp:567-600): local direction, value (incl. scale) and pdf
+__device__ __forceinline__ f3 envSampleLocal(const GEnv &e, float sx, float sy, f3 &value, float &pdf) {
+#pragma clang fp contract(off)
+    const uint32_t row = envSampleReuse(e.cdf_rows, e.height, sy);
+    const uint32_t col = envSampleReuse(e.cdf_cols + (size_t)row * (e.width + 1), e.width, sx);
+    const float px = (float)col + intervalToTent(sx), py = (float)row + intervalToTent(sy);
+    const int xPos = (int)floorf(px), yPos = (int)floorf(py);
+    const float dx1 = px - (float)xPos, dx2 = 1.0f - dx1, dy1 = py - (float)yPos, dy2 = 1.0f - dy1;
+    const f3 v1 = envTexel(e, xPos, yPos) * dx2 * dy2 + envTexel(e, xPos + 1, yPos) * dx1 * dy2;
+    const f3 v2 = envTexel(e, xPos, yPos + 1) * dx2 * dy1 + envTexel(e, xPos + 1, yPos + 1) * dx1 * dy1;
+    value = (v1 + v2) * e.scale;
+    const int h = (int)e.height;
+    pdf = (envLum(v1) * e.row_weights[min(max(yPos, 0), h - 1)] +
+           envLum(v2) * e.row_weights[min(max(yPos + 1, 0), h - 1)]) *
+          e.normalization;
+    float sinPhi, cosPhi, sinTheta, cosTheta;
+    sincosf(e.pixel_size[0] * (px + 0.5f), &sinPhi, &cosPhi);
+    sincosf(e.pixel_size[1] * (py + 0.5f), &sinTheta, &cosTheta);
+    pdf /= fmaxf(fabsf(sinTheta), kEpsilon);
+    return mk(sinPhi * sinTheta, cosTheta, -cosPhi * sinTheta);
+}
+// EnvironmentMap::sampleDirect (envmap.cpp:516-543): value / pdf, with the far intersection of the
+// scene's bounding sphere as the light distance (BSphere::rayIntersect + solveQuadratic, util.cpp)
+__device__ __forceinline__ f3 envSampleDirect(const GEnv &e, f3 ref, float sx, float sy, f3 &dOut, float &dist,
+                                              float &pdfOut) {
+    f3 value;
+    float pdf;
+    const f3 d = envToWorld(e, envSampleLocal(e, sx, sy, value, pdf));
+    pdfOut = 0;
+    if (isZero(value) || pdf == 0) return mk1(0.f);
+    const f3 o = ref - mk(e.center[0], e.center[1], e.center[2]);
+    const float A = dot(d, d), B = 2 * dot(o, d), C = dot(o, o) - e.radius * e.radius;
+    const float disc = B * B - 4.0f * A * C;
+    if (disc < 0) return mk1(0.f);
+    const float sq = sqrtf(disc), temp = (B < 0) ? -0.5f * (B - sq) : -0.5f * (B + sq);
+    float x0 = temp / A, x1 = C / temp;
+    if (x0 > x1) {
+        const float t = x0;
+        x0 = x1;
+        x1 = t;
+    }
+    if (x0 >= 0 || x1 <= 0) return mk1(0.f);
+    dOut = d;
+    dist = x1;
+    pdfOut = pdf;
+    return value / pdf;
+}
+
 // Scene::sampleEmitterDirect without the visibility test (scene.cpp:871-895 + area.cpp:158-171 +
-// shape.cpp:102-115 + trimesh.cpp:412-423 + triangle.cpp:24-45); returns radiance/pdf.
+// shape.cpp:102-115 + trimesh.cpp:412-423 + triangle.cpp:24-45); returns radiance/pdf.  With an
+// environment emitter (sc.env; compiled in with ENV only), it is emitter g.num_emitters - 1.
+template <bool ENV = false>
 __device__ __forceinline__ f3 sampleEmitter(const GParams &g, const SceneDev &sc, f3 ref, f3 refN, float sx, float sy,
                                             f3 &dOut, float &dist, float &pdfOut, f3 *pOut = nullptr) {
     uint32_t ne = g.num_emitters;
@@ -342,6 +475,15 @@ __device__ __forceinline__ f3 sampleEmitter(const GParams &g, const SceneDev &sc
     if (ne == 0) return mk1(0.f);
     uint32_t ei = min((uint32_t)(sx * (float)ne), ne - 1);
     sx = sx * (float)ne - (float)ei;
+    if (ENV && ei == ne - 1) {
+        float pdf;
+        const f3 v = envSampleDirect(*sc.env, ref, sx, sy, dOut, dist, pdf);
+        if (pdf == 0) return mk1(0.f);
+        const float emPdf = 1.0f / (float)ne;
+        pdfOut = pdf * emPdf;
+        if (pOut) *pOut = ref + dOut * dist;
+        return v / emPdf;
+    }
     const GEmitter em = sc.ems[ei];
     // DiscreteDistribution::sampleReuse over the area CDF (lower_bound)
     const float *cdf = sc.emcdf + em.cdf_begin;

@@ -189,6 +189,14 @@ class Device:
     def reset_film(self):
         self._chk(self.lib.pg_reset_film(self.h))
 
+    def read_aovs(self):
+        """Denoiser feature sums (pg_config.aovs = 1): (albedo rgb + count, normal xyz + 0), (H, W, 4) each."""
+        W, H = self.scene.width, self.scene.height
+        alb = np.zeros((H, W, 4), np.float32)
+        nrm = np.zeros((H, W, 4), np.float32)
+        self._chk(self.lib.pg_read_aovs(self.h, _p(alb), _p(nrm)))
+        return alb, nrm
+
     def stats(self):
         s = capi.pg_stats()
         self._chk(self.lib.pg_get_stats(self.h, C.byref(s)))
@@ -220,6 +228,15 @@ class Device:
         wg = None if wo_given is None else np.ascontiguousarray(wo_given, np.float32)
         out = np.zeros((len(a), 5), np.float32)
         self._chk(self.lib.pg_phase_query(self.h, medium, _p(a), _p(wg), len(a), _p(out)))
+        return out
+
+    def envmap_query(self, op, x):
+        """Environment emitter on the device: op 0 sampleDirect (x: n x 2 samples -> n x 8: d, pdf,
+        value/pdf, dist), op 1 pdfDirect (x: n x 3 directions -> n), op 2 evalEnvironment (-> n x 3)."""
+        x = np.ascontiguousarray(x, np.float32)
+        n = len(x)
+        out = np.zeros((n, 8) if op == 0 else (n,) if op == 1 else (n, 3), np.float32)
+        self._chk(self.lib.pg_envmap_query(self.h, int(op), _p(x), n, _p(out)))
         return out
 
     def medium_lookup(self, medium, pts):
@@ -259,7 +276,8 @@ class ProgressivePathTracer:
             s_tree_threshold=float(props.get("sTreeThreshold", 12000.0)),
             d_tree_threshold=float(props.get("dTreeThreshold", 0.01)),
             max_paths_in_flight=int(props.get("maxPathsInFlight", 0)), integrator=self.integrator,
-            distance_guiding=float(props.get("distanceGuiding", 0.25)))
+            distance_guiding=float(props.get("distanceGuiding", 0.25)),
+            aovs=int(bool(props.get("aovs", False))))
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         self.dev = None
         self.progression = 0
@@ -293,6 +311,13 @@ class ProgressivePathTracer:
                 return None
             self.render_progression(self.spp_per_progression)
         return self.dev.read_film()
+
+    def denoiser_features(self):
+        """Per-pixel means of the first-hit albedo and normal (what Denoiser::add averages,
+        denoiser.cpp:138-144), shape (H, W, 3) each; needs props {"aovs": True}."""
+        alb, nrm = self.dev.read_aovs()
+        n = np.maximum(alb[..., 3:4], 1)
+        return alb[..., :3] / n, nrm[..., :3] / n
 
     def cancel(self):
         self._cancel.set()

@@ -6,6 +6,8 @@
   C4     kitchen()      Country-kitchen class interior: ~1M triangles, several area emitters
   C5     smoke()        Heterogeneous smoke: seeded fBm density grid (256^3 at full size) inside a
                         null-BSDF box, HG g = 0.8, albedo 0.9, over a diffuse floor under an area light
+  (f4)   sky_courtyard()  An open courtyard lit by a procedural HDR sky envmap (sky_envmap()), the
+                        environment-emitter case of SURVEY.md §8f f4
 
 A scene is flat numpy arrays (what a Mitsuba adapter extracts from Scene::getShapes() / getBSDFs():
 SURVEY.md §8b "Scene inputs it reads") plus a `desc()` that returns the pg_scene_desc for the C-ABI.
@@ -80,6 +82,8 @@ class Scene:
         self.media, self._densities = [], []
         self.camera_medium = -1
         self.camera = None
+        self.envmap = None  # pg_envmap (set_envmap)
+        self._env_rgb = None
         self._desc = None
         self.name = "scene"
 
@@ -132,6 +136,21 @@ class Scene:
         self.shapes.append(sh)
         return len(self.shapes) - 1
 
+    def set_envmap(self, rgb, to_world=None, scale=1.0):
+        """Environment emitter (src/emitters/envmap.cpp): `rgb` is a latitude-longitude image of shape
+        (height, width, 3), row 0 at theta = 0 (+Y of the local frame); `to_world` a 3x3 rotation."""
+        rgb = np.ascontiguousarray(rgb, np.float32)
+        assert rgb.ndim == 3 and rgb.shape[2] == 3
+        e = capi.pg_envmap()
+        e.height, e.width = rgb.shape[0], rgb.shape[1]
+        e.rgb = rgb.ctypes.data_as(C.POINTER(C.c_float))
+        R = np.eye(3, dtype=np.float32) if to_world is None else np.asarray(to_world, np.float32)
+        e.to_world = (C.c_float * 9)(*R.reshape(-1).tolist())
+        e.scale = scale
+        self._env_rgb = rgb
+        self.envmap = e
+        self._desc = None
+
     def set_camera(self, origin, target, up, fov_x, width, height, near=1e-2, far=1e4):
         c = capi.pg_camera()
         c.origin = (C.c_float * 3)(*origin)
@@ -165,6 +184,7 @@ class Scene:
         d.num_media = len(self.media)
         d.media = C.cast(self._media_arr, C.POINTER(capi.pg_medium))
         d.camera_medium = self.camera_medium
+        d.envmap = C.pointer(self.envmap) if self.envmap is not None else None
         self._desc = d
         return self
 
@@ -520,6 +540,72 @@ def kitchen(width=1920, height=1080, target_tris=1_000_000, seed=7):
 
 # ---------------------------------------------------------------------------------------------
 # C5: heterogeneous smoke
+# ---------------------------------------------------------------------------------------------
+# environment-lit scenes (the envmap emitter of data/tests/test_emitter.xml)
+def rot_x(deg):
+    a = np.radians(deg)
+    return np.array([[1, 0, 0], [0, np.cos(a), -np.sin(a)], [0, np.sin(a), np.cos(a)]], np.float32)
+
+
+def sky_envmap(width=256, height=128, sun_theta=40.0, sun_phi=60.0, sun_radius=3.0, sun_radiance=400.0, seed=7):
+    """Procedural latitude-longitude sky (seeded): a zenith-to-horizon gradient, a dim ground half with
+    a little noise, and a small bright sun disk, i.e. the high-dynamic-range, strongly peaked kind of
+    map guiding and envmap importance sampling are for.  Returns (height, width, 3) float32."""
+    rng = np.random.default_rng(seed)
+    th = (np.arange(height) + 0.5) / height * np.pi
+    ph = (np.arange(width) + 0.5) / width * 2 * np.pi
+    T, P = np.meshgrid(th, ph, indexing="ij")
+    img = np.zeros((height, width, 3), np.float32)
+    up = np.cos(T)
+    sky = np.stack([0.35 + 0.4 * (1 - up), 0.55 + 0.3 * (1 - up), 0.95 + 0.05 * up], -1) * (up > 0)[..., None]
+    ground = np.stack([0.12, 0.1, 0.08], -1) * (up <= 0)[..., None] * (0.8 + 0.4 * rng.random((height, width, 1)))
+    img += sky + ground
+    # local direction (envmap.cpp:598): (sin phi sin theta, cos theta, -cos phi sin theta)
+    d = np.stack([np.sin(P) * np.sin(T), np.cos(T), -np.cos(P) * np.sin(T)], -1)
+    st, sp = np.radians(sun_theta), np.radians(sun_phi)
+    sd = np.array([np.sin(sp) * np.sin(st), np.cos(st), -np.cos(sp) * np.sin(st)])
+    ang = np.degrees(np.arccos(np.clip(d @ sd, -1, 1)))
+    img += (ang < sun_radius)[..., None] * np.array([1.0, 0.9, 0.75], np.float32) * sun_radiance
+    return img.astype(np.float32)
+
+
+def sky_courtyard(width=512, height=384, seed=7, env=None, area_light=False):
+    """An open courtyard under a sky envmap: a ground plane, walls that shade part of it, and
+    diffuse / rough-conductor / glass / plastic objects (optionally one area light).  Light reaches
+    most shading points only through the environment emitter."""
+    rng = np.random.default_rng(seed)
+    s = Scene()
+    s.name = "sky_courtyard"
+    ground = s.add_material(material("diffuse", reflectance=(0.45, 0.42, 0.38)))
+    wall = s.add_material(material("diffuse", reflectance=(0.7, 0.65, 0.6), twosided=True))
+    gold = s.add_material(material("roughconductor", conductor="Au", alpha=0.2, distribution="ggx"))
+    glass = s.add_material(material("roughdielectric", int_ior=1.5, ext_ior=1.0, alpha=0.1, distribution="ggx"))
+    red = s.add_material(material("roughplastic", alpha=0.3, distribution="ggx", diffuse_reflectance=(0.6, 0.15, 0.1)))
+    V, F = quad((-6, 0, -6), (6, 0, -6), (6, 0, 6), (-6, 0, 6), facing=(0, 1, 0))
+    s.add_mesh(V, F, material=ground)
+    V, F = box((-4, 0, 2.5), (4, 2.5, 2.8))
+    s.add_mesh(V, F, material=wall)
+    V, F = box((2.5, 0, -3), (2.8, 2.0, 2.5))
+    s.add_mesh(V, F, material=wall)
+    V, F, N = uv_sphere((-1.0, 0.8, 0.5), 0.8, 64, 32)
+    s.add_mesh(V, F, N, material=gold)
+    V, F, N = uv_sphere((0.9, 0.6, -0.4), 0.6, 64, 32)
+    s.add_mesh(V, F, N, material=glass)
+    V, F = box((-0.3, 0, -1.8), (0.5, 0.9, -1.0))
+    s.add_mesh(transform(V, rot_y(25), t=(0, 0, 0)), F, material=red)
+    for i in range(5):
+        c = (rng.uniform(-3, 2), 0.15, rng.uniform(-3, 2))
+        V, F, N = uv_sphere(c, 0.15, 24, 12)
+        s.add_mesh(V, F, N, material=[gold, red, ground][i % 3])
+    if area_light:
+        lm = s.add_material(material("diffuse", reflectance=(0, 0, 0)))
+        V, F = quad((1.5, 2.4, 1.5), (2.3, 2.4, 1.5), (2.3, 2.4, 2.3), (1.5, 2.4, 2.3), facing=(0, -1, 0))
+        s.add_mesh(V, F, material=lm, radiance=(8.0, 7.0, 6.0))
+    s.set_envmap(sky_envmap(seed=seed) if env is None else env, to_world=rot_y(0))
+    s.set_camera((-4.5, 2.2, -5.5), (0.2, 0.6, 0.3), (0, 1, 0), 60.0, width, height)
+    return s.finalize()
+
+
 def fbm_density(res=256, seed=7, octaves=5, base=4):
     """Seeded fBm density in [0, 1] on a res^3 grid ([z][y][x]): value-noise octaves (trilinear
     upsampling of random lattices, base * 2^o cells per axis, amplitude 2^-o) shaped by a soft

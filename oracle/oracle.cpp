@@ -61,7 +61,10 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
     int depth = 1;
 
     while (depth <= maxDepth || maxDepth < 0) {
-        if (!its.valid) break;  // no environment emitter in these scenes
+        if (!its.valid) {  // only the camera ray gets here (EEmittedRadiance, progressive_path.cpp:150-158)
+            if (S.env.valid && emittedQuery && (!cfg.hide_emitters || scattered)) L += T * S.env.eval(ray.d);
+            break;
+        }
         const pg_shape &shp = S.shapes[its.shape];
         const Material &M = S.mats[shp.material];
         if (shp.emitter >= 0 && emittedQuery && (!cfg.hide_emitters || scattered)) L += T * emitterLe(S, its, -ray.d);
@@ -163,18 +166,22 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                 hitEmitter = true;
             }
         } else {
-            break;
+            // escaped: the environment emitter, if any (progressive_path.cpp:252-267)
+            if (!S.env.valid || (cfg.hide_emitters && !scattered)) break;
+            value = S.env.eval(ray.d);
+            hitEmitter = true;
         }
         T *= weight;
         eta *= bs.eta;
         if (hitEmitter) {
-            float lumPdf = (cfg.use_nee && !(bs.sampledType & EDelta))
-                               ? pdfEmitterDirect(S, em, prevRefN, ray.d, its.sh.n, its.t)
-                               : 0.0f;
+            float lumPdf = 0.0f;
+            if (cfg.use_nee && !(bs.sampledType & EDelta))
+                lumPdf = hit ? pdfEmitterDirect(S, em, prevRefN, ray.d, its.sh.n, its.t) : pdfEnvDirect(S, ray.d);
             float w = cfg.use_nee ? miWeight(woPdf, lumPdf) : 1.0f;
             L += T * value * w;
         }
         emittedQuery = false;
+        if (!hit) break;
         if (depth++ >= cfg.rr_depth) {
             float q = std::min(maxc(T) * eta * eta, 0.95f);
             if (rng.next1(dimOf(depth - 1, SLOT_RR)) >= q) break;
@@ -459,6 +466,60 @@ void oracle_bsdf_query(const pg_material *pm, const float *wi, const float *u, c
 }
 
 uint32_t oracle_material_type(const pg_material *pm) { return makeMaterial(*pm).type; }
+
+// Denoiser feature sums (pg_read_aovs): per camera sample, BSDF::getAlbedo and the shading normal
+// of the first hit (Denoiser::Sample defaults albedo 0, normal (0, 0, -1) for an escaped ray).
+// albedo / normal: width*height*4 each (sum rgb + count / sum xyz + 0), accumulated.
+void oracle_render_aovs(void *sp, uint32_t seed, uint32_t spp, uint32_t sample_offset, float *albedo, float *normal) {
+    const Scene &S = *(const Scene *)sp;
+    const uint32_t W = S.cam.W, H = S.cam.H;
+    for (uint32_t pix = 0; pix < W * H; ++pix)
+        for (uint32_t s = 0; s < spp; ++s) {
+            Rng rng{rngKey(pix, seed), sample_offset + s};
+            float jx, jy;
+            rng.next2(0, jx, jy);
+            Ray ray = S.cameraRay((float)(pix % W) + jx, (float)(pix / W) + jy);
+            Its its;
+            V3 a(0.f), n(0.f, 0.f, -1.f);
+            if (S.intersect(ray, its)) {
+                a = S.mats[S.shapes[its.shape].material].albedoOf();
+                n = its.sh.n;
+            }
+            float *fa = albedo + 4 * (size_t)pix, *fn = normal + 4 * (size_t)pix;
+            fa[0] += a.x;
+            fa[1] += a.y;
+            fa[2] += a.z;
+            fa[3] += 1.0f;
+            fn[0] += n.x;
+            fn[1] += n.y;
+            fn[2] += n.z;
+        }
+}
+
+// Environment emitter queries (same layout as pg_envmap_query): op 0 sampleDirect from the bounding-
+// sphere centre (in n x 2, out n x 8), op 1 pdfDirect (in n x 3, out n), op 2 evalEnvironment (out n x 3)
+int oracle_envmap_query(void *sp, int32_t op, const float *in, uint64_t n, float *out) {
+    const Scene &S = *(const Scene *)sp;
+    if (!S.env.valid) return 1;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (op == 0) {
+            V3 d(0.f);
+            float dist = 0, pdf;
+            V3 v = S.env.sampleDirect(S.env.center, in[2 * i], in[2 * i + 1], d, dist, pdf);
+            float *o = out + 8 * i;
+            float vals[8] = {d.x, d.y, d.z, pdf, v.x, v.y, v.z, dist};
+            std::memcpy(o, vals, sizeof vals);
+        } else if (op == 1) {
+            out[i] = S.env.pdf(V3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+        } else {
+            V3 v = S.env.eval(V3(in[3 * i], in[3 * i + 1], in[3 * i + 2]));
+            out[3 * i] = v.x;
+            out[3 * i + 1] = v.y;
+            out[3 * i + 2] = v.z;
+        }
+    }
+    return 0;
+}
 
 void oracle_set_volpath_eager(int32_t eager) { g_volpathEager = eager != 0; }
 

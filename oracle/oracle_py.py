@@ -52,6 +52,8 @@ def lib(capi):
             "oracle_set_volpath_eager": (None, [C.c_int32]),
             "oracle_medium_query": (None, [VP, C.c_int32, C.c_int32, VP, VP, C.c_uint64, VP]),
             "oracle_hg_query": (None, [C.c_float, VP, VP, C.c_uint64, VP]),
+            "oracle_render_aovs": (None, [VP, C.c_uint32, C.c_uint32, C.c_uint32, VP, VP]),
+            "oracle_envmap_query": (C.c_int, [VP, C.c_int32, VP, C.c_uint64, VP]),
         }
         for k, (r, a) in sig.items():
             f = getattr(L, k)
@@ -103,6 +105,23 @@ class OracleScene:
         op = (2 if transmittance else 1) + (2 if grid else 0)
         self.L.oracle_medium_query(self.h, m, op, _p(rays), _p(keys), len(rays), _p(out))
         return out
+
+    def envmap_query(self, op, x):
+        """Same layout as integrator.Device.envmap_query."""
+        x = np.ascontiguousarray(x, np.float32)
+        n = len(x)
+        out = np.zeros((n, 8) if op == 0 else (n,) if op == 1 else (n, 3), np.float32)
+        if self.L.oracle_envmap_query(self.h, int(op), _p(x), n, _p(out)) != 0:
+            raise ValueError("the scene has no environment emitter")
+        return out
+
+    def render_aovs(self, spp, sample_offset=0, seed=1337):
+        """First-hit denoiser feature sums: (albedo rgb + count, normal xyz + 0), (H, W, 4) each."""
+        W, H = self.scene.width, self.scene.height
+        alb = np.zeros((H, W, 4), np.float32)
+        nrm = np.zeros((H, W, 4), np.float32)
+        self.L.oracle_render_aovs(self.h, seed, spp, sample_offset, _p(alb), _p(nrm))
+        return alb, nrm
 
     def trace(self, rays, any_hit=False):
         rays = np.ascontiguousarray(rays, np.float32)

@@ -44,6 +44,20 @@ struct Material {
     V3 ceta() const { return {m.eta[0], m.eta[1], m.eta[2]}; }
     V3 ck() const { return {m.k[0], m.k[1], m.k[2]}; }
     bool twosided() const { return (m.flags & PG_MAT_TWOSIDED) != 0; }
+    // BSDF::getAlbedo (diffuse.cpp:112, conductor.cpp:225, roughconductor.cpp:264, dielectric.cpp:230,
+    // roughdielectric.cpp:272, plastic.cpp:266, roughplastic.cpp:354; null: bsdf.h:361)
+    V3 albedoOf() const {
+        switch (m.type) {
+            case PG_BSDF_DIFFUSE: return diff();
+            case PG_BSDF_CONDUCTOR:
+            case PG_BSDF_ROUGHCONDUCTOR: return spec();
+            case PG_BSDF_DIELECTRIC: return trans() * 0.5f + spec() * (1 - 0.5f);
+            case PG_BSDF_ROUGHDIELECTRIC: return spec() * 0.5f + trans() * (1 - 0.5f);
+            case PG_BSDF_PLASTIC: return diff() * 0.5f + spec() * (1 - 0.5f);
+            case PG_BSDF_ROUGHPLASTIC: return spec() * 0.5f + diff() * (1 - 0.5f);
+            default: return V3(0.f);
+        }
+    }
     Microfacet distr() const {
         return Microfacet((int)m.distribution, m.alpha_u, m.alpha_v, (m.flags & PG_MAT_SAMPLE_ALL) == 0);
     }

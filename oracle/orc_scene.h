@@ -9,6 +9,10 @@
 //   TriMesh::samplePosition, Triangle::sample                  src/librender/trimesh.cpp:412-423, src/libcore/triangle.cpp:24-60
 //   DiscreteDistribution::sampleReuse                          include/mitsuba/core/pmf.h:124-188
 //   PerspectiveCamera::sampleRay + Transform::lookAt           src/sensors/perspective.cpp:271-298, transform.cpp:191-214
+//   EnvironmentMap configure / evalEnvironment / sampleDirect / pdfDirect
+//                                                              src/emitters/envmap.cpp:260-356,380-410,516-663
+//   TMIPMap level 0: half storage, evalTexel, evalBilinear     include/mitsuba/render/mipmap.h:225-240,503-596
+//   solveQuadratic / BSphere::rayIntersect                     src/libcore/util.cpp, include/mitsuba/core/bsphere.h
 // The kd-tree (sahkdtree3.h) is replaced by a binned-SAH BVH: only the closest hit matters.
 #pragma once
 #include <limits>
@@ -127,6 +131,178 @@ struct Camera {
     uint32_t W, H;
 };
 
+// binary16 round-to-nearest-even (the MIP map's SpectrumHalf texel storage), as a float
+inline float halfRound(float f) {
+    if (!std::isfinite(f) || f == 0.0f) return f;
+    const float a = std::fabs(f);
+    if (a >= 65520.0f) return std::copysign(kInf, f);
+    float q;
+    if (a < 6.103515625e-05f) {
+        q = 5.9604644775390625e-08f;
+    } else {
+        int e;
+        std::frexp(a, &e);
+        q = std::ldexp(1.0f, e - 11);
+    }
+    return std::copysign(std::nearbyint(a / q) * q, f);
+}
+// Environment emitter (EnvironmentMap, envmap.cpp) restated on the latitude-longitude level 0
+struct Env {
+    bool valid = false;
+    int W = 0, H = 0;
+    std::vector<V3> tex;  // half-rounded, negatives clamped (mipmap.h:232-240)
+    std::vector<float> cdfRows, cdfCols, rowWeights;
+    float normalization = 0, pixelSize[2] = {0, 0}, scale = 1, radius = 0;
+    V3 center;
+    float R[9];
+
+    V3 texel(int x, int y) const {  // evalTexel: ERepeat in u, EClamp in v
+        if (x < 0 || x >= W) {
+            x %= W;
+            if (x < 0) x += W;
+        }
+        y = std::min(std::max(y, 0), H - 1);
+        return tex[(size_t)y * W + x];
+    }
+    V3 toLocal(V3 d) const {
+        return V3(R[0] * d.x + R[3] * d.y + R[6] * d.z, R[1] * d.x + R[4] * d.y + R[7] * d.z,
+                  R[2] * d.x + R[5] * d.y + R[8] * d.z);
+    }
+    V3 toWorld(V3 d) const {
+        return V3(R[0] * d.x + R[1] * d.y + R[2] * d.z, R[3] * d.x + R[4] * d.y + R[5] * d.z,
+                  R[6] * d.x + R[7] * d.y + R[8] * d.z);
+    }
+    static float safeAcos(float v) { return std::acos(std::min(1.0f, std::max(-1.0f, v))); }
+
+    // EnvironmentMap::configure (envmap.cpp:260-329) + createShape's bounding sphere (:331-356)
+    void build(const pg_envmap &e, const AABB &box) {
+        W = (int)e.width;
+        H = (int)e.height;
+        scale = e.scale;
+        for (int k = 0; k < 9; ++k) R[k] = e.to_world[k];
+        tex.resize((size_t)W * H);
+        for (size_t i = 0; i < (size_t)W * H; ++i)
+            tex[i] = V3(halfRound(std::max(e.rgb[3 * i], 0.0f)), halfRound(std::max(e.rgb[3 * i + 1], 0.0f)),
+                        halfRound(std::max(e.rgb[3 * i + 2], 0.0f)));
+        cdfCols.assign((size_t)(W + 1) * H, 0.0f);
+        cdfRows.assign(H + 1, 0.0f);
+        rowWeights.assign(H, 0.0f);
+        size_t colPos = 0, rowPos = 0;
+        float rowSum = 0.0f;
+        cdfRows[rowPos++] = 0;
+        for (int y = 0; y < H; ++y) {
+            float colSum = 0;
+            cdfCols[colPos++] = 0;
+            for (int x = 0; x < W; ++x) {
+                colSum += luminance(tex[(size_t)y * W + x]);
+                cdfCols[colPos++] = colSum;
+            }
+            if (colSum > 0) {
+                float normalization_ = 1.0f / colSum;
+                for (int x = 1; x < W; ++x) cdfCols[colPos - x - 1] *= normalization_;
+            } else {  // black row: zero marginal mass; uniform conditional (the reference divides by 0)
+                for (int x = 1; x < W; ++x) cdfCols[colPos - x - 1] = (float)(W - x) / (float)W;
+            }
+            cdfCols[colPos - 1] = 1.0f;
+            float weight = (float)std::sin((y + 0.5f) * M_PI / H);
+            rowWeights[y] = weight;
+            rowSum += colSum * weight;
+            cdfRows[rowPos++] = rowSum;
+        }
+        float normalization_ = 1.0f / rowSum;
+        for (int y = 1; y < H; ++y) cdfRows[rowPos - y - 1] *= normalization_;
+        cdfRows[rowPos - 1] = 1.0f;
+        normalization = (float)(1.0f / (rowSum * (2 * M_PI / W) * (M_PI / H)));
+        pixelSize[0] = (float)(2 * M_PI / W);
+        pixelSize[1] = (float)(M_PI / H);
+        center = (box.lo + box.hi) * 0.5f;
+        radius = std::max(kEpsilon, length(box.hi - center) * 1.5f);
+        valid = true;
+    }
+    // evalEnvironment without differentials -> evalBilinear(0, uv) * scale (envmap.cpp:380-410)
+    V3 eval(V3 dWorld) const {
+        V3 v = toLocal(dWorld);
+        float ux = std::atan2(v.x, -v.z) * (0.5f * kInvPi), uy = safeAcos(v.y) * kInvPi;
+        if (!std::isfinite(ux) || !std::isfinite(uy)) return V3(0.f);
+        float u = ux * W - 0.5f, w = uy * H - 0.5f;
+        int xPos = (int)std::floor(u), yPos = (int)std::floor(w);
+        float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = w - yPos, dy2 = 1.0f - dy1;
+        V3 r = texel(xPos, yPos) * dx2 * dy2 + texel(xPos, yPos + 1) * dx2 * dy1 + texel(xPos + 1, yPos) * dx1 * dy2 +
+               texel(xPos + 1, yPos + 1) * dx1 * dy1;
+        return r * scale;
+    }
+    // internalPdfDirection (envmap.cpp:603-633) of a local direction
+    float pdfLocal(V3 d) const {
+        float ux = std::atan2(d.x, -d.z) * (0.5f * kInvPi), uy = safeAcos(d.y) * kInvPi;
+        if (!std::isfinite(ux) || !std::isfinite(uy)) return 0.0f;
+        float u = ux * W - 0.5f, w = uy * H - 0.5f;
+        int xPos = (int)std::floor(u), yPos = (int)std::floor(w);
+        float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = w - yPos, dy2 = 1.0f - dy1;
+        V3 v1 = texel(xPos, yPos) * dx2 * dy2 + texel(xPos + 1, yPos) * dx1 * dy2;
+        V3 v2 = texel(xPos, yPos + 1) * dx2 * dy1 + texel(xPos + 1, yPos + 1) * dx1 * dy1;
+        float sinTheta = safe_sqrt(1 - d.y * d.y);
+        return (luminance(v1) * rowWeights[std::min(std::max(yPos, 0), H - 1)] +
+                luminance(v2) * rowWeights[std::min(std::max(yPos + 1, 0), H - 1)]) *
+               normalization / std::max(std::fabs(sinTheta), kEpsilon);
+    }
+    float pdf(V3 dWorld) const { return pdfLocal(toLocal(dWorld)); }
+    // sampleReuse (envmap.cpp:658-663)
+    static uint32_t sampleReuse(const float *cdf, uint32_t size, float &s) {
+        const float *entry = std::lower_bound(cdf, cdf + size + 1, s);
+        uint32_t index = std::min((uint32_t)std::max((ptrdiff_t)0, entry - cdf - 1), size - 1);
+        s = (s - cdf[index]) / (cdf[index + 1] - cdf[index]);
+        return index;
+    }
+    static float intervalToTent(float s) {  // warp.cpp:143-155
+        float sign;
+        if (s < 0.5f) {
+            sign = 1;
+            s *= 2;
+        } else {
+            sign = -1;
+            s = 2 * (s - 0.5f);
+        }
+        return sign * (1 - std::sqrt(s));
+    }
+    // internalSampleDirection (envmap.cpp:567-600)
+    V3 sampleLocal(float sx, float sy, V3 &value, float &pdfOut) const {
+        uint32_t row = sampleReuse(cdfRows.data(), (uint32_t)H, sy);
+        uint32_t col = sampleReuse(cdfCols.data() + (size_t)row * (W + 1), (uint32_t)W, sx);
+        float px = (float)col + intervalToTent(sx), py = (float)row + intervalToTent(sy);
+        int xPos = (int)std::floor(px), yPos = (int)std::floor(py);
+        float dx1 = px - xPos, dx2 = 1.0f - dx1, dy1 = py - yPos, dy2 = 1.0f - dy1;
+        V3 v1 = texel(xPos, yPos) * dx2 * dy2 + texel(xPos + 1, yPos) * dx1 * dy2;
+        V3 v2 = texel(xPos, yPos + 1) * dx2 * dy1 + texel(xPos + 1, yPos + 1) * dx1 * dy1;
+        value = (v1 + v2) * scale;
+        pdfOut = (luminance(v1) * rowWeights[std::min(std::max(yPos, 0), H - 1)] +
+                  luminance(v2) * rowWeights[std::min(std::max(yPos + 1, 0), H - 1)]) *
+                 normalization;
+        float sinPhi = std::sin(pixelSize[0] * (px + 0.5f)), cosPhi = std::cos(pixelSize[0] * (px + 0.5f));
+        float sinTheta = std::sin(pixelSize[1] * (py + 0.5f)), cosTheta = std::cos(pixelSize[1] * (py + 0.5f));
+        pdfOut /= std::max(std::fabs(sinTheta), kEpsilon);
+        return V3(sinPhi * sinTheta, cosTheta, -cosPhi * sinTheta);
+    }
+    // sampleDirect (envmap.cpp:516-543): value / pdf; pdf = 0 on failure
+    V3 sampleDirect(V3 ref, float sx, float sy, V3 &d, float &dist, float &pdfOut) const {
+        V3 value;
+        float pdf;
+        d = toWorld(sampleLocal(sx, sy, value, pdf));
+        pdfOut = 0;
+        if (isZero(value) || pdf == 0) return V3(0.f);
+        V3 o = ref - center;
+        float A = dot(d, d), B = 2 * dot(o, d), C = dot(o, o) - radius * radius;
+        float disc = B * B - 4.0f * A * C;
+        if (disc < 0) return V3(0.f);
+        float sq = std::sqrt(disc), temp = (B < 0) ? -0.5f * (B - sq) : -0.5f * (B + sq);
+        float x0 = temp / A, x1 = C / temp;
+        if (x0 > x1) std::swap(x0, x1);
+        if (x0 >= 0 || x1 <= 0) return V3(0.f);
+        dist = x1;
+        pdfOut = pdf;
+        return value / pdf;
+    }
+};
+
 struct Scene {
     std::vector<V3> pos, nrm;
     std::vector<uint32_t> idx;
@@ -140,6 +316,8 @@ struct Scene {
     std::vector<BvhNode> nodes;
     AABB bounds;
     Camera cam;
+    Env env;  // the last emitter of the uniform pick when valid
+    uint32_t numEmitters() const { return (uint32_t)emitters.size() + (env.valid ? 1u : 0u); }
     std::vector<Medium> media;
     int camMedium = -1;
 
@@ -229,6 +407,7 @@ inline void Scene::build(const pg_scene_desc &d) {
         bounds.lo = bounds.lo - ((bounds.hi - bounds.lo) * eps + V3(eps));
         bounds.hi = bounds.hi + ((bounds.hi - bounds.lo) * eps + V3(eps));
     }
+    if (d.envmap) env.build(*d.envmap, bounds);
     std::vector<uint32_t> order(nt);
     for (uint32_t t = 0; t < nt; ++t) order[t] = t;
     nodes.clear();
@@ -477,13 +656,23 @@ struct DirectRec {
 // Scene::sampleEmitterDirect without the visibility test (scene.cpp:871-895 up to the shadow ray):
 // returns radiance / pdf with dr.pdf including the emitter-selection pdf; dr.pdf = 0 on failure
 inline V3 sampleEmitterNoVis(const Scene &S, DirectRec &dr, float sx, float sy) {
-    uint32_t ne = (uint32_t)S.emitters.size();
+    uint32_t ne = S.numEmitters();
     dr.pdf = 0;
     if (ne == 0) return V3(0.f);
     // uniform emitter pdf (every sampling weight is 1): sampleReuse on a uniform CDF
     float emPdf = 1.0f / (float)ne;
     uint32_t ei = std::min((uint32_t)(sx * (float)ne), ne - 1);
     sx = sx * (float)ne - (float)ei;
+    if (S.env.valid && ei == ne - 1) {  // the environment emitter (no refN test: envmap.cpp:516-543)
+        float pdf;
+        V3 value = S.env.sampleDirect(dr.ref, sx, sy, dr.d, dr.dist, pdf);
+        if (pdf == 0) return V3(0.f);
+        dr.p = dr.ref + dr.d * dr.dist;
+        dr.n = -dr.d;
+        dr.emitter = (int)ei;
+        dr.pdf = pdf * emPdf;
+        return value / emPdf;
+    }
     const pg_emitter &em = S.emitters[ei];
     const pg_shape &sh = S.shapes[em.shape];
     // TriMesh::samplePosition: triangle by area on sample.y (reuse), then Triangle::sample(sample)
@@ -532,8 +721,12 @@ inline V3 sampleEmitterDirect(const Scene &S, DirectRec &dr, float sx, float sy)
 inline float pdfEmitterDirect(const Scene &S, int ei, V3 refN, V3 d, V3 n, float dist) {
     if (!(dot(d, refN) >= 0 && dot(d, n) < 0)) return 0.0f;
     float pdfPos = 1.0f / S.emArea[ei];
-    return pdfPos * (dist * dist) / absDot(d, n) * (1.0f / (float)S.emitters.size());
+    return pdfPos * (dist * dist) / absDot(d, n) * (1.0f / (float)S.numEmitters());
 }
+
+// Scene::pdfEmitterDirect for a BSDF-sampled direction that escaped to the environment emitter
+// (fillDirectSamplingRecord: solid-angle measure, envmap.cpp:358-374,545-556)
+inline float pdfEnvDirect(const Scene &S, V3 d) { return S.env.pdf(d) * (1.0f / (float)S.numEmitters()); }
 
 inline V3 emitterLe(const Scene &S, const Its &its, V3 w) {
     int e = S.shapes[its.shape].emitter;

@@ -32,7 +32,7 @@ def test_library_exports_every_symbol(pg):
     out = subprocess.run(["nm", "-D", "--defined-only", pg.capi.LIB_PATH], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}\b", out), name
-    assert lib.pg_abi_version() == 5
+    assert lib.pg_abi_version() == 6
 
 
 def test_struct_layouts_match_header(pg):
@@ -40,7 +40,8 @@ def test_struct_layouts_match_header(pg):
     c = pg.capi
     structs = {"pg_material": c.pg_material, "pg_shape": c.pg_shape, "pg_emitter": c.pg_emitter,
                "pg_camera": c.pg_camera, "pg_scene_desc": c.pg_scene_desc, "pg_config": c.pg_config,
-               "pg_record": c.pg_record, "pg_stats": c.pg_stats, "pg_medium": c.pg_medium}
+               "pg_record": c.pg_record, "pg_stats": c.pg_stats, "pg_medium": c.pg_medium,
+               "pg_envmap": c.pg_envmap}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for s, cls in structs.items():
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
