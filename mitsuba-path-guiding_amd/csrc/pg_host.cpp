@@ -855,7 +855,6 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     g.height = cam.height;
     g.num_emitters = d->num_emitters + (d->envmap ? 1u : 0u);
     g.num_materials = d->num_materials;
-    g.aovs = c->cfg.aovs;
 
     // tile shard of this rank: 32x32 tiles dealt round-robin
     const uint32_t T = c->cfg.tile_size, tx = (cam.width + T - 1) / T, ty = (cam.height + T - 1) / T;
@@ -1103,7 +1102,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         EventPair et = nextEvents(&l);
         HIPC(c, hipEventRecord(et.a, l.stream));
         pg_launch_trace(l.stream, g, sc, pathView(&l), lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb),
-                        l.bound, cls);
+                        l.bound, cls, l.b == 0);
         HIPC(c, hipEventRecord(et.b, l.stream));
         HIPC(c, hipMemcpyAsync(l.h_counts + (size_t)kBounceWords * l.b + kClassCounts, cb + kClassCounts,
                                (PG_NUM_CLASSES + 1) * PG_QSHARDS * 4, hipMemcpyDeviceToHost, l.stream));

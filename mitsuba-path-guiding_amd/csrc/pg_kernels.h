@@ -26,8 +26,8 @@ struct PathDev {
     float4 *vtx;       // [max_vertices][P][3]
     uint32_t *stack_ovf;  // traversal-stack overflow ring, pg_stack_overflow_words(0) words
     uint32_t P;        // capacity (slot stride of vtx)
-    // denoiser features (pg_config.aovs), 1 per slot: the first hit (t, tri | ~0, u, v), written by
-    // k_camera (no hit) and k_shade (depth 1); k_film turns it into albedo + normal sums.  nullptr: off.
+    // denoiser features (pg_config.aovs), 1 per slot: the camera ray's hit record (t, tri | ~0, u, v),
+    // written by the chunk's first k_trace; k_film turns it into albedo + normal sums.  nullptr: off.
     float4 *aov;
 };
 
@@ -86,8 +86,9 @@ void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const u
 // goes to class_queues[c] (shard s -> shard s); escaped paths are only counted, in
 // class_queues[PG_NUM_CLASSES].counts.  max_shard: upper bound of the largest shard count (sizes
 // the grid; the kernels read the counts).
+// first_bounce: the chunk's camera rays (their hit records are kept in p.aov when it is set)
 void pg_launch_trace(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
-                     const Queue *class_queues);
+                     const Queue *class_queues, bool first_bounce);
 void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
                            const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shadow);
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);

@@ -40,7 +40,6 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     p.rad[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.prev[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
     p.pinfo[slot] = make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u);
-    if (p.aov) p.aov[slot] = make_float4(0.f, __uint_as_float(0xFFFFFFFFu), 0.f, 0.f);  // no first hit yet
     q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
 }
 
@@ -116,7 +115,10 @@ __device__ __forceinline__ void classAppend(int cls, uint32_t slot, const ClassQ
 
 // ENV: the scene has an environment emitter (escaped paths pick up its radiance)
 template <bool ENV>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs) {
+// first: the camera rays' bounce with denoiser features on (pg_config.aovs): the hit record of every
+// path also goes to p.aov, which k_film resolves into albedo and normal (nullptr: off)
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
+                                                       float4 *first) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, p.stack_ovf);
     const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
@@ -134,7 +136,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
             bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
-            p.hit[slot] = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+            const float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+            p.hit[slot] = hr;
+            if (first) first[slot] = hr;
             cls = h ? (int)sc.tclass[tri] : PG_NUM_CLASSES;
         }
         classAppend(cls, slot, cqs, s);
@@ -237,7 +241,6 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
             }
             if (depth > g.depth_cap) break;
             const GMat M = sc.mats[h.mat];
-            if (p.aov && depth == 1) p.aov[slot] = hv;  // first hit, resolved into denoiser features by k_film
             if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
                 L = L + T * Le;
                 dirtyL = true;
@@ -634,13 +637,14 @@ static inline dim3 shardGrid(uint32_t max_shard, uint32_t block, uint32_t max_ro
     return dim3(PG_QSHARDS * (rows < max_rows ? rows : max_rows));
 }
 void pg_launch_trace(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
-                     const Queue *class_queues) {
+                     const Queue *class_queues, bool first_bounce) {
     if (!max_shard) return;
     ClassQueues cq;
     for (int c = 0; c <= PG_NUM_CLASSES; ++c) cq.q[c] = class_queues[c];
     const dim3 grid = shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS);
-    if (sc.env) hipLaunchKernelGGL(k_trace<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq);
-    else hipLaunchKernelGGL(k_trace<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq);
+    float4 *first = first_bounce ? p.aov : nullptr;
+    if (sc.env) hipLaunchKernelGGL(k_trace<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq, first);
+    else hipLaunchKernelGGL(k_trace<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq, first);
 }
 template <bool ENV>
 static void launchShade(hipStream_t s, int cls, dim3 grid, const GParams &g, const SceneDev &sc, const SDDev &sd,

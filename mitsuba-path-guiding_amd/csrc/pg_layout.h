@@ -141,5 +141,4 @@ struct GParams {
     int32_t max_depth, rr_depth, use_nee, hide_emitters, strict_normals, guiding, record, max_vertices;
     float max_component_value, bsdf_fraction;
     uint32_t seed, num_emitters, num_materials, depth_cap;  // num_emitters counts the environment emitter
-    int32_t aovs, pad_aov[3];
 };

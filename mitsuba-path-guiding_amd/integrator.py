@@ -310,7 +310,10 @@ class ProgressivePathTracer:
             if self._cancel.is_set():
                 return None
             self.render_progression(self.spp_per_progression)
-        return self.dev.read_film()
+        rgbw, sq = self.dev.read_film()
+        if getattr(self.dev.scene, "mirror_x", False):  # a mirrored sensor (e.g. <scale x="-1"/> in toWorld)
+            rgbw, sq = rgbw[:, ::-1].copy(), sq[:, ::-1].copy()
+        return rgbw, sq
 
     def denoiser_features(self):
         """Per-pixel means of the first-hit albedo and normal (what Denoiser::add averages,

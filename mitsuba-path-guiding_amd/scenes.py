@@ -83,6 +83,7 @@ class Scene:
         self.camera_medium = -1
         self.camera = None
         self.envmap = None  # pg_envmap (set_envmap)
+        self.mirror_x = False  # the sensor's toWorld mirrors x (mitsuba_xml): images are flipped on read-out
         self._env_rgb = None
         self._desc = None
         self.name = "scene"
