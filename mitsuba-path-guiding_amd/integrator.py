@@ -349,6 +349,12 @@ class GuidedPathTracer(ProgressivePathTracer):
     postprogression hook exchanges records (identity on one GPU; RCCL all-gather across ranks via
     `exchange`), splats them into the building SD-tree and refits.  The film is reset before the
     final render, which samples with the last trained tree.
+
+    sampleCombination (after Mueller's practical-path-guiding course notes):
+    "discard" (default) keeps only the final render's samples; "inversevar" keeps every training
+    iteration's image too and returns the inverse-variance weighted combination of all of them,
+    each image weighted by 1 / (its mean per-pixel variance of the mean), since the early, poorly
+    guided iterations are noisier.  All images are unbiased, so the combination is too.
     """
 
     guided = True
@@ -358,6 +364,11 @@ class GuidedPathTracer(ProgressivePathTracer):
         self.training_iterations = int(self.props.get("trainingIterations", 5))
         self.exchange = exchange  # callable(dev) -> None: all-gather + splat into dev (N > 1)
         self.initial_tree = None
+        self.sample_combination = str(self.props.get("sampleCombination", "discard")).lower()
+        if self.sample_combination not in ("discard", "inversevar"):
+            raise ValueError(f"sampleCombination must be discard or inversevar, not {self.sample_combination!r}")
+        self.iteration_films = []
+        self.combination_weights = None
 
     def preprocess(self, scene):
         super().preprocess(scene)
@@ -378,6 +389,9 @@ class GuidedPathTracer(ProgressivePathTracer):
             self.preprogression()
             self.dev.render_pass(2 ** it, self.sample_offset, record=True)
             self.sample_offset += 2 ** it
+            if self.sample_combination == "inversevar":
+                self.iteration_films.append(self.dev.read_film())
+                self.dev.reset_film()
             self.postprogression_train(it)
 
     def postprogression_train(self, it):
@@ -388,9 +402,46 @@ class GuidedPathTracer(ProgressivePathTracer):
         self.dev.refit(it)
 
     def render(self, spp):
+        self.iteration_films = []
         self.train()
         self.dev.reset_film()
-        return super().render(spp)
+        out = super().render(spp)
+        if out is None or self.sample_combination == "discard":
+            return out
+        films = [(f[0][:, ::-1], f[1][:, ::-1]) if getattr(self.dev.scene, "mirror_x", False) else f
+                 for f in self.iteration_films] + [out]
+        return combine_inverse_variance(films, self)
+
+
+def combine_inverse_variance(films, owner=None):
+    """Inverse-variance weighted combination of unbiased images given as film sums (rgbw, sumsq):
+    image i has per-pixel means m_i and variance estimate v_i = mean over pixels and channels of
+    (E[x^2] - m^2) / n.  Returns film-like sums (combined mean x total count, combined second moment
+    x total count) so that callers can keep dividing by the count channel."""
+    means, seconds, weights, counts = [], [], [], []
+    for rgbw, sq in films:
+        n = np.maximum(rgbw[..., 3:4], 1)
+        m = rgbw[..., :3] / n
+        m2 = sq[..., :3] / n
+        v = float(np.mean(np.maximum(m2 - m * m, 0) / n))
+        w = 1.0 / v if v > 0 and np.isfinite(v) else 0.0
+        means.append(m)
+        seconds.append(m2)
+        weights.append(w)
+        counts.append(rgbw[..., 3:4])
+    W = np.asarray(weights, np.float64)
+    if W.sum() <= 0:
+        W = np.zeros_like(W)
+        W[-1] = 1.0
+    W = W / W.sum()
+    if owner is not None:
+        owner.combination_weights = W.tolist()
+    total = np.sum(counts, 0)
+    mean = sum(w * m for w, m in zip(W, means))
+    second = sum(w * m2 for w, m2 in zip(W, seconds))
+    rgbw = np.concatenate([mean * total, total], -1).astype(np.float32)
+    sq = np.concatenate([second * total, np.zeros_like(total)], -1).astype(np.float32)
+    return rgbw, sq
 
 
 class GuidedVolumetricPathTracer(GuidedPathTracer):

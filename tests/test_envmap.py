@@ -130,3 +130,4 @@ def test_envmap_desc_plumbing(pg):
     sc = _env_scene(pg, np.ones((4, 8, 3), np.float32))
     d = sc.desc()
     assert bool(d.envmap) and d.envmap.contents.width == 8 and d.envmap.contents.height == 4
+
