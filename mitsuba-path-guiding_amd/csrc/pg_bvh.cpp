@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <array>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -44,7 +45,16 @@ struct BNode {
 };
 
 constexpr int kBins = 32;
-constexpr uint32_t kLeafTarget = 4;
+// SAH constants: leaves of at most kLeafTarget triangles are never split; a triangle test costs
+// kTriCost node traversals.  PG_BVH_LEAF_TARGET / PG_BVH_TRI_COST override them (A/B measurements).
+uint32_t leafTarget() {
+    const char *e = std::getenv("PG_BVH_LEAF_TARGET");
+    return e ? (uint32_t)std::atoi(e) : 2u;
+}
+float triCost() {
+    const char *e = std::getenv("PG_BVH_TRI_COST");
+    return e ? (float)std::atof(e) : 1.0f;
+}
 
 }  // namespace
 
@@ -63,6 +73,8 @@ static void buildBinary(const float *P, const uint32_t *I, uint32_t nt, uint32_t
     ord.assign(nt, 0);
     for (uint32_t t = 0; t < nt; ++t) ord[t] = t;
     bn.clear();
+    const uint32_t kLeafTarget = std::max(1u, leafTarget());
+    const float kTri = triCost();
     bn.reserve(nt ? 2 * (size_t)nt / kLeafTarget + 8 : 8);
     struct Job { int32_t node; uint32_t first, count, depth; };
     std::vector<Job> st;
@@ -121,8 +133,8 @@ static void buildBinary(const float *P, const uint32_t *I, uint32_t nt, uint32_t
                         }
                     }
                 }
-                float leafCost = box.area() * (float)j.count;
-                float splitCost = box.area() * 1.0f + bestCost;  // traversal cost ~ 1 triangle test
+                float leafCost = box.area() * (float)j.count * kTri;
+                float splitCost = box.area() * 1.0f + bestCost * kTri;  // one node visit + the children's tests
                 if (bestAxis >= 0 && splitCost >= leafCost && j.count <= maxLeaf) leaf = true;
             }
             if (!leaf) {
