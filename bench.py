@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--train", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3)")
+    ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = 2^22)")
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
@@ -83,7 +85,8 @@ def main():
     exchange = D.make_exchange(on_dev, mode=a.exchange) if world > 1 else None
     # one progression for the final render (the device chunks it into waves of <= 4M paths)
     Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
-    integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp}, device=device,
+    integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp, "pathLanes": a.lanes,
+                    "maxPathsInFlight": a.paths_in_flight}, device=device,
                    rank=rank, world_size=world, exchange=exchange)
     integ.preprocess(scene)
     dev = integ.dev

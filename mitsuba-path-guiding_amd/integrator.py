@@ -276,6 +276,7 @@ class ProgressivePathTracer:
             s_tree_threshold=float(props.get("sTreeThreshold", 12000.0)),
             d_tree_threshold=float(props.get("dTreeThreshold", 0.01)),
             max_paths_in_flight=int(props.get("maxPathsInFlight", 0)), integrator=self.integrator,
+            path_lanes=int(props.get("pathLanes", 0)),
             distance_guiding=float(props.get("distanceGuiding", 0.25)),
             aovs=int(bool(props.get("aovs", False))))
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
