@@ -1052,7 +1052,10 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     if (npix == 0 || spp == 0) return PG_OK;
     if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH) return renderVolpath(c, spp, sample_offset, record && c->cfg.guiding);
     const bool rec = record && c->cfg.guiding;
-    uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
+    // 2^25 paths per chunk by default: bigger chunks mean fewer sparse tail bounces (each costs a
+    // class-count readback) per path.  C3 with 3 lanes: 2^22 491, 2^23 552, 2^24 569, 2^25 587
+    // Mpaths/s (DESIGN.md "Lanes"); the lanes then hold ~58 GB each, mostly training vertices.
+    uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
     uint64_t total = (uint64_t)npix * spp;
     // paths per lane: split small passes so that both lanes get work
     uint32_t want = (uint32_t)std::min<uint64_t>((total + c->nlanes - 1) / c->nlanes, cap);
