@@ -935,7 +935,9 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
 // progressive_volpath: chunks of (pixel, sample) items through k_volpath, films in chunk order
 pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) {
     const uint32_t npix = (uint32_t)c->local_pixels.size();
-    const uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 22);
+    // 2^25 items per launch: fewer persistent-kernel tails (C5 guided: 177.8 -> 189.8 Mpaths/s
+    // against 2^22, profiles/r01h_c5_*.log); 50 GB of training vertices when guided
+    const uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
     const uint32_t want = (uint32_t)std::min<uint64_t>((uint64_t)npix * spp, cap);
     if (c->vol_cap < want) {
         HIPC(c, c->vol_rad.alloc((size_t)want * 16));
@@ -1057,8 +1059,18 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     // Mpaths/s (DESIGN.md "Lanes"); the lanes then hold ~58 GB each, mostly training vertices.
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
     uint64_t total = (uint64_t)npix * spp;
-    // paths per lane: split small passes so that both lanes get work
-    uint32_t want = (uint32_t)std::min<uint64_t>((total + c->nlanes - 1) / c->nlanes, cap);
+    // chunk count rounded up to whole rounds of lanes, so that the last round keeps every lane busy
+    // (a rank of an N-GPU job may get only a few chunks of the final render); small passes split
+    // into one chunk per lane
+    uint64_t chunks = std::max<uint64_t>(1, (total + cap - 1) / cap);
+    chunks = (chunks + c->nlanes - 1) / c->nlanes * c->nlanes;
+    uint32_t want;
+    if ((uint64_t)npix * chunks <= total) {  // whole sample layers per chunk
+        const uint64_t layers = (spp + chunks - 1) / chunks;
+        want = (uint32_t)std::min<uint64_t>(layers * npix, cap);
+    } else {
+        want = (uint32_t)std::min<uint64_t>((total + chunks - 1) / chunks, cap);
+    }
     pg_status s;
     if ((s = ensurePaths(c, want))) return s;
     GParams g = c->g;

@@ -320,6 +320,8 @@ class ProgressivePathTracer:
         """Per-pixel means of the first-hit albedo and normal (what Denoiser::add averages,
         denoiser.cpp:138-144), shape (H, W, 3) each; needs props {"aovs": True}."""
         alb, nrm = self.dev.read_aovs()
+        if getattr(self.dev.scene, "mirror_x", False):  # same read-out flip as render()
+            alb, nrm = alb[:, ::-1], nrm[:, ::-1]
         n = np.maximum(alb[..., 3:4], 1)
         return alb[..., :3] / n, nrm[..., :3] / n
 
