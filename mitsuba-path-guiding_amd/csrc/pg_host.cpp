@@ -1058,6 +1058,24 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     // class-count readback) per path.  C3 with 3 lanes: 2^22 491, 2^23 552, 2^24 569, 2^25 587
     // Mpaths/s (DESIGN.md "Lanes"); the lanes then hold ~58 GB each, mostly training vertices.
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
+    if (!c->cfg.max_paths_in_flight) {
+        // ... but at most 70 % of the device memory this context can use for path state (free memory
+        // plus what its lanes already hold), e.g. when several contexts or ranks share one GPU
+        size_t freeB = 0, totalB = 0;
+        if (hipMemGetInfo(&freeB, &totalB) == hipSuccess && freeB > 0) {
+            size_t held = 0;
+            for (int li = 0; li < c->nlanes; ++li) {
+                const Lane &l = c->lanes[li];
+                for (const DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo, &l.sh_o,
+                                        &l.sh_d, &l.sh_c, &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov})
+                    held += b->bytes;
+            }
+            const int vs = c->cfg.guiding ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0;
+            const double perPath = 10.0 * 16 + (3 + PG_NUM_CLASSES) * 4.0 + vs * 48.0 + (c->cfg.aovs ? 16.0 : 0.0);
+            const double fit = 0.7 * (double)(freeB + held) / (perPath * c->nlanes);
+            if (fit < (double)cap) cap = std::max<uint32_t>(1u << 20, (uint32_t)fit & ~4095u);
+        }
+    }
     uint64_t total = (uint64_t)npix * spp;
     // chunk count rounded up to whole rounds of lanes, so that the last round keeps every lane busy
     // (a rank of an N-GPU job may get only a few chunks of the final render); small passes split
