@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 6
+#define PG_ABI_VERSION 7
 
 typedef int32_t pg_status;
 enum {
@@ -209,7 +209,17 @@ typedef struct pg_config {
     int32_t aovs;                 /* 1: accumulate the denoiser feature buffers (Denoiser::Sample albedo + normal,
                                      include/mitsuba/render/denoiser.h:12-16) of every camera sample's first hit;
                                      read with pg_read_aovs.  Path integrator only.  0 */
+    int32_t bsdf_fraction_bound;  /* guided path integrator: how the one-sample-MIS BSDF fraction alpha of a vertex is
+                                     chosen.  PG_FRACTION_FIXED: alpha = bsdf_sampling_fraction everywhere (Mueller et
+                                     al. 2017).  PG_FRACTION_ALBEDO: alpha = max(bsdf_sampling_fraction, min(a, 0.95))
+                                     with a = the max channel of BSDF::getAlbedo, which bounds the mixture weight
+                                     f / (alpha p_bsdf + (1 - alpha) p_guide) <= (f / p_bsdf) / alpha by 1 for albedo
+                                     bounded BSDF weights.  PG_FRACTION_THROUGHPUT: as ALBEDO with a scaled by the path
+                                     throughput max(T), so a path may regain throughput it lost, but not grow past 1.
+                                     Any per-vertex choice independent of the sampled direction is unbiased.
+                                     Default PG_FRACTION_ALBEDO (C3 quality). */
 } pg_config;
+enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2 };
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
 enum { PG_MAJORANT_GRID = 0, PG_MAJORANT_GLOBAL = 1 };
 

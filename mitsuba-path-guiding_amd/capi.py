@@ -16,6 +16,7 @@ PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, P
 PG_MEDIUM_HETEROGENEOUS = 0
 PG_INTEGRATOR_PATH, PG_INTEGRATOR_VOLPATH = 0, 1
 PG_MAJORANT_GRID, PG_MAJORANT_GLOBAL = 0, 1
+PG_FRACTION_FIXED, PG_FRACTION_ALBEDO, PG_FRACTION_THROUGHPUT = 0, 1, 2
 MAJORANT_CELL = 8  # voxels per majorant-grid cell edge (pg_host.cpp / oracle/orc_medium.h)
 PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
 PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
@@ -84,7 +85,7 @@ class pg_config(C.Structure):
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
                 ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
-                ("distance_guiding", C.c_float), ("aovs", C.c_int32)]
+                ("distance_guiding", C.c_float), ("aovs", C.c_int32), ("bsdf_fraction_bound", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -126,6 +127,7 @@ def default_config(**overrides):
     c.integrator = PG_INTEGRATOR_PATH
     c.distance_guiding = 0.25
     c.aovs = 0
+    c.bsdf_fraction_bound = PG_FRACTION_ALBEDO
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")
@@ -169,7 +171,7 @@ SIGNATURES = [
 ]
 
 
-PG_ABI_VERSION = 6  # include/pg_capi.h
+PG_ABI_VERSION = 7  # include/pg_capi.h
 
 
 def load_library(path=None):

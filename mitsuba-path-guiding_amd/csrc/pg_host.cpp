@@ -258,6 +258,23 @@ GMat makeGMat(const pg_material &m) {
     }
     if (m.flags & PG_MAT_TWOSIDED) sides |= 0x10000u;
     g.type |= sides;
+    {  // BSDF::getAlbedo (as bsdfAlbedo in pg_kernels.hip), max channel: the guide-fraction bound
+        float a[3];
+        for (int i = 0; i < 3; ++i) {
+            const float d = g.diff[i], s = g.spec[i], t = g.trans[i];
+            switch (m.type) {
+                case PG_BSDF_DIFFUSE: a[i] = d; break;
+                case PG_BSDF_CONDUCTOR:
+                case PG_BSDF_ROUGHCONDUCTOR: a[i] = s; break;
+                case PG_BSDF_DIELECTRIC: a[i] = t * 0.5f + s * 0.5f; break;
+                case PG_BSDF_ROUGHDIELECTRIC: a[i] = s * 0.5f + t * 0.5f; break;
+                case PG_BSDF_PLASTIC: a[i] = d * 0.5f + s * 0.5f; break;
+                case PG_BSDF_ROUGHPLASTIC: a[i] = s * 0.5f + d * 0.5f; break;
+                default: a[i] = 0.0f;
+            }
+        }
+        g.wbound = std::max(std::max(a[0], a[1]), a[2]);
+    }
     return g;
 }
 
@@ -544,6 +561,7 @@ pg_status pg_config_default(pg_config *c) {
     c->path_lanes = 0;
     c->integrator = PG_INTEGRATOR_PATH;
     c->distance_guiding = 0.25f;
+    c->bsdf_fraction_bound = PG_FRACTION_ALBEDO;
     return PG_OK;
 }
 
@@ -578,6 +596,10 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     if (c->cfg.integrator != PG_INTEGRATOR_PATH && c->cfg.integrator != PG_INTEGRATOR_VOLPATH) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown integrator");
+    }
+    if (c->cfg.bsdf_fraction_bound < PG_FRACTION_FIXED || c->cfg.bsdf_fraction_bound > PG_FRACTION_THROUGHPUT) {
+        delete c;
+        return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown bsdf_fraction_bound");
     }
     if (c->cfg.volume_majorant != PG_MAJORANT_GRID && c->cfg.volume_majorant != PG_MAJORANT_GLOBAL) {
         delete c;
@@ -962,6 +984,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
     g.guiding = c->cfg.guiding;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
+    g.fraction_bound = c->cfg.bsdf_fraction_bound;
     g.record = rec && maxV > 0;
     g.max_vertices = maxV;
     const SceneDev sc = sceneView(c);
@@ -1102,6 +1125,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     g.max_vertices = rec ? std::min(c->cfg.record_max_vertices, c->lanes[0].vtx_slots) : 0;
     g.max_component_value = c->cfg.max_component_value;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
+    g.fraction_bound = c->cfg.bsdf_fraction_bound;
     g.seed = c->cfg.seed;
     g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
     const SceneDev sc = sceneView(c);

@@ -253,7 +253,8 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
             const SDView sv = sdv(sd);
             uint4 meta = make_uint4(0, 0, 0, 0);
             if (guide) meta = sd.meta[sdLookup(sv, h.p)];
-            const float alpha = g.bsdf_fraction;
+            // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction)
+            const float alpha = guideFraction(g.fraction_bound, g.bsdf_fraction, M.wbound, maxc(T));
 
             // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow.  With
             // guiding, the D-tree pdf of the light direction is resolved below, in one lockstep walk

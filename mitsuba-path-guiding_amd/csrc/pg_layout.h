@@ -9,7 +9,7 @@
 struct GMat {
     uint32_t model, dist, flags, type;  // pg BSDF model, microfacet distribution, PG_MAT_* flags, EBSDFType bits
     float alpha_u, alpha_v, eta, invEta;
-    float invEta2, fdrInt, specWeight, pad0;
+    float invEta2, fdrInt, specWeight, wbound;  // wbound: max channel of BSDF::getAlbedo (guide-fraction bound)
     float diff[4];
     float spec[4];
     float trans[4];
@@ -141,4 +141,5 @@ struct GParams {
     int32_t max_depth, rr_depth, use_nee, hide_emitters, strict_normals, guiding, record, max_vertices;
     float max_component_value, bsdf_fraction;
     uint32_t seed, num_emitters, num_materials, depth_cap;  // num_emitters counts the environment emitter
+    int32_t fraction_bound;  // pg_config.bsdf_fraction_bound (PG_FRACTION_*)
 };

@@ -282,6 +282,16 @@ __device__ __forceinline__ float miWeight(float a, float b) {
     return a / (a + b);
 }
 
+// BSDF fraction alpha of one guided vertex's one-sample MIS (pg_config.bsdf_fraction_bound).  The
+// mixture weight f / (alpha p_bsdf + (1 - alpha) p_guide) is at most (f / p_bsdf) / alpha, so
+// raising alpha to the BSDF's albedo keeps it <= 1 and the path throughput cannot compound upward
+// over bounces where the D-tree has no density.  Oracle: guideFraction (oracle/oracle.cpp).
+__device__ __forceinline__ float guideFraction(int mode, float alpha, float wbound, float maxT) {
+    if (mode == PG_FRACTION_ALBEDO) return fmaxf(alpha, fminf(wbound, 0.95f));
+    if (mode == PG_FRACTION_THROUGHPUT) return fmaxf(alpha, fminf(wbound * maxT, 0.95f));
+    return alpha;
+}
+
 // wave-aggregated append of `pred` lanes' values into q (one atomic per wave)
 __device__ __forceinline__ void waveAppend(bool pred, uint32_t value, uint32_t *q, uint32_t *count) {
     unsigned long long m = __ballot(pred);

@@ -43,6 +43,10 @@ def _p(a):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
 
+_FRACTION_BOUNDS = {"fixed": capi.PG_FRACTION_FIXED, "albedo": capi.PG_FRACTION_ALBEDO,
+                    "throughput": capi.PG_FRACTION_THROUGHPUT}
+
+
 class PGError(RuntimeError):
     def __init__(self, status, msg):
         super().__init__(f"pg status {status}: {msg}")
@@ -278,7 +282,8 @@ class ProgressivePathTracer:
             max_paths_in_flight=int(props.get("maxPathsInFlight", 0)), integrator=self.integrator,
             path_lanes=int(props.get("pathLanes", 0)),
             distance_guiding=float(props.get("distanceGuiding", 0.25)),
-            aovs=int(bool(props.get("aovs", False))))
+            aovs=int(bool(props.get("aovs", False))),
+            bsdf_fraction_bound=_FRACTION_BOUNDS[str(props.get("bsdfSamplingFractionBound", "albedo")).lower()])
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         self.dev = None
         self.progression = 0

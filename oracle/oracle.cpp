@@ -32,6 +32,15 @@ inline float miWeight(float a, float b) {
     return a / (a + b);
 }
 
+// BSDF fraction of a guided vertex (pg_config.bsdf_fraction_bound; kernels: guideFraction, pg_trace.h)
+inline float guideFraction(int mode, float alpha, const Material &M, float maxT) {
+    const V3 a = M.albedoOf();
+    const float wb = std::max(std::max(a.x, a.y), a.z);
+    if (mode == PG_FRACTION_ALBEDO) return std::max(alpha, std::min(wb, 0.95f));
+    if (mode == PG_FRACTION_THROUGHPUT) return std::max(alpha, std::min(wb * maxT, 0.95f));
+    return alpha;
+}
+
 struct Vtx {
     V3 p, dir, T, Lat;
     float woPdf;
@@ -45,7 +54,6 @@ struct Counters {
 V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, Ray ray, std::vector<pg_record> *recs,
       Counters &cnt) {
     const bool guiding = cfg.guiding && tree && tree->built;
-    const float alpha = cfg.bsdf_sampling_fraction;
     const int maxDepth = cfg.max_depth;
     const int maxV = std::min(cfg.record_max_vertices, 64);
     Vtx vtx[64];
@@ -75,6 +83,7 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
         V3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? its.sh.n : V3(0.f);
         const bool guidable = guiding && (M.type & ESmooth) && !(M.type & EDelta);
         const DTreeW *dt = guidable ? &tree->dtrees[tree->lookup(its.p)] : nullptr;
+        const float alpha = guideFraction(cfg.bsdf_fraction_bound, cfg.bsdf_sampling_fraction, M, maxc(T));
 
         // ---- direct illumination (NEE)
         if (cfg.use_nee && (M.type & ESmooth)) {

@@ -60,7 +60,8 @@ def main():
     O.build()
     sc = pg.scenes.cornell(32, 32)
     osc = O.OracleScene(pg.capi, sc)
-    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=400.0)
+    # Mueller et al.'s fixed BSDF fraction (the fixture predates pg_config.bsdf_fraction_bound)
+    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=400.0, bsdf_fraction_bound=pg.capi.PG_FRACTION_FIXED)
     tree = O.OracleSDTree(osc)
     for it in range(3):
         O.render(osc, cfg, 2 ** it, 2 ** it - 1, record=True, sdtree=tree, nthreads=1)

@@ -12,7 +12,7 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 def _trained(pg, O, iters=3, res=32, thr=400.0):
     sc = pg.scenes.cornell(res, res)
     osc = O.OracleScene(pg.capi, sc)
-    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=thr)
+    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=thr, bsdf_fraction_bound=pg.capi.PG_FRACTION_FIXED)
     tree = O.OracleSDTree(osc)
     for it in range(iters):
         O.render(osc, cfg, 2 ** it, 2 ** it - 1, record=True, sdtree=tree, nthreads=1)
@@ -101,3 +101,19 @@ def test_refinement_rules(pg, O):
     t3.splat_bytes(recs)
     t3.refit(0, cfg2)
     assert t3.serialize()[:64].view(np.uint32)[12] > 1
+
+
+def test_fraction_bound_modes_unbiased(pg, O):
+    """Every pg_config.bsdf_fraction_bound mode picks alpha per vertex independently of the sampled
+    direction, so the guided image keeps the unguided expectation (per-pixel means pooled over the
+    image; independent of the tree's quality)."""
+    sc, osc, tree = _trained(pg, O)
+    ref, rsq, _ = O.render(osc, pg.capi.default_config(), 512, 1 << 20, nthreads=8)
+    n = ref[..., 3:4]
+    m_ref = ref[..., :3].sum() / n.sum()
+    var_ref = (rsq[..., :3].sum() / n.sum() - (ref[..., :3] / n) ** 2).clip(0).mean()
+    for mode in (pg.capi.PG_FRACTION_FIXED, pg.capi.PG_FRACTION_ALBEDO, pg.capi.PG_FRACTION_THROUGHPUT):
+        cfg = pg.capi.default_config(guiding=1, bsdf_fraction_bound=mode)
+        g, gsq, _ = O.render(osc, cfg, 256, 7, sdtree=tree, nthreads=8)
+        m = g[..., :3].sum() / g[..., 3].sum()
+        assert abs(m - m_ref) / m_ref < 0.01, (mode, m, m_ref)
