@@ -1,19 +1,28 @@
-"""Benchmark: Mpaths/s of the SD-tree guided integrator on the Veach ajar-door-class scene (C3).
+"""Benchmark: Mpaths/s + equal-spp RMSE of the SD-tree guided integrator on the Veach ajar-door-class
+scene (C3).
 
 A step is one complete guided render job of C3 (BASELINE.json configs[2]): 1280x720, five training
-progressions of 1, 2, 4, 8, 16 spp (training-record write, RCCL all-gather of records across ranks,
-fixed-point splat, SD-tree refit) followed by the 1024-spp final render with the trained tree —
-(31 + 1024) x 921,600 = 972.3 M camera paths per step.  Inputs (scene, BVH, path buffers) are
-resident in HBM before timing starts.  With N ranks the image tiles are sharded (total work fixed:
-"strong" scaling); value = all paths of the job / max-over-ranks wall time.
+progressions of 1, 2, 4, 8, 16 spp (training-record write, fixed-point splat, all-reduce of the
+SD-tree building statistics across ranks, refit) followed by the 1024-spp final render with the
+trained tree -- (31 + 1024) x 921,600 = 972.3 M camera paths per step.  Inputs (scene, BVH, path
+buffers) are resident in HBM before timing starts.  With N ranks the image tiles are sharded (total
+work fixed: "strong" scaling) and the film tiles are reduced to rank 0 inside the timed job;
+value = all paths of the job / max-over-ranks wall time.
 
-Also reported: the dominant kernel's roofline (algorithmic bytes per launch, SURVEY.md §8d /
-DESIGN.md §"Measurement", over its HIP-event-measured average duration on a one-lane context, since
-the timed job overlaps three lanes), the timed-region pipeline figure, and on rank 0 at N=1 the
-CPU oracle timed on a bounded sample of the same job (kind "port"), plus the equal-spp relative RMSE
-between GPU and CPU on that sample.
+Also reported:
+  roofline   the dominant kernel's algorithmic bytes per launch (SURVEY.md §8d's 420 B per segment,
+             split per kernel) over its HIP-event-measured average launch, on a
+             one-lane context (the timed job overlaps three lanes); `traffic` from the committed
+             rocprofv3 PMC summary named in `traffic_source` (with its code revision);
+  pipeline   §8d's pipeline figure: segments/s x 420 B over the timed wall clock;
+  quality    (N = 1, C3 at 1280x720) relative errors of the timed job's guided image against the
+             65,536-spp unguided ground truth tests/golden/c3_gt.npz, next to the unguided path
+             tracer at equal spp and at equal time (tools/quality_c3.py has the definitions);
+  cpu_baseline  (rank 0, N = 1) the CPU oracle running the same guided job on a bounded sample: the
+             full 31-spp training (its own records, splat and refit) and the 1024-spp final render
+             of a block of tiles; with the GPU/CPU relative-RMSE ratio on those tiles.
 
-  python bench.py [--gpus N --steps K --warmup W] [--spp 1024] [--no-cpu] [--quick]
+  python bench.py [--gpus N --steps K --warmup W] [--spp 1024] [--no-cpu] [--no-quality] [--quick]
   python bench.py --scene smoke      # C5: the guided volumetric job on the 256^3 smoke cloud at 1024^2
 """
 import argparse
@@ -28,12 +37,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# algorithmic bytes per unit (DESIGN.md §"Measurement"; SURVEY.md §8d decomposition of B_seg)
-BYTES_TRACE_PER_RAY = 52      # queue id 4 + ray o/tmin 16 + ray d/tmax 16 + hit write 16
-BYTES_SHADOW_PER_RAY = 84     # queue id 4 + shadow ray 32 + contribution 16 + radiance RMW 32
-BYTES_SHADE_PER_VERTEX = 488  # path state read 96 + write 96 + tri gather 80 + material 32 + shadow write 48
-#                               + emitter-tri gather 80 + training vertex 48 + queue writes 8
-BYTES_DENSITY_LOOKUP = 32     # k_volpath (C5): one trilinear lookup gathers 8 f32 voxels
+# B_seg = 420 B per path segment (state read 72 + write 68, hit record write + read
+# 32, hit-triangle gather 76, material 32, shadow-queue write + read 64, emitter-triangle gather 36,
+# training record 40), split over the three path kernels:
+BYTES_SEGMENT = 420
+BYTES_TRACE_PER_RAY = 48       # ray o/d read 32 + hit write 16
+BYTES_SHADE_PER_VERTEX = 300   # state read 40 + write 68 + hit read 16 + triangle 76 + material 32
+#                                + shadow-queue write 32 + emitter triangle 36
+BYTES_SHADE_RECORD = 40        # + training record (recording passes only)
+BYTES_SHADOW_PER_RAY = 32      # shadow-queue read 32
+assert BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX + BYTES_SHADE_RECORD + BYTES_SHADOW_PER_RAY == BYTES_SEGMENT
+BYTES_DENSITY_LOOKUP = 32      # k_volpath (C5): one trilinear lookup gathers 8 f32 voxels
+GT_C3 = os.path.join(ROOT, "tests", "golden", "c3_gt.npz")
 
 
 def parse():
@@ -47,10 +62,11 @@ def parse():
     ap.add_argument("--spp", type=int, default=1024)
     ap.add_argument("--train", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-quality", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3)")
-    ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = 2^22)")
+    ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = auto: 2^25)")
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather"])
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU budget of the final-render sample")
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
     return ap.parse_args()
 
@@ -83,7 +99,7 @@ def main():
     scene = pg.scenes.SCENES[a.scene](a.width, a.height)
     # postprogression exchange: all-reduce of the SD-tree building statistics
     exchange = D.make_exchange(on_dev, mode=a.exchange) if world > 1 else None
-    # one progression for the final render (the device chunks it into waves of <= 4M paths)
+    # one progression for the final render (the device chunks it into 2^25-path chunks, 3 in flight)
     Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
     integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp, "pathLanes": a.lanes,
                     "maxPathsInFlight": a.paths_in_flight}, device=device,
@@ -99,7 +115,10 @@ def main():
 
     def job():
         integ.reset()
-        integ.render(a.spp)
+        rgbw, sq = integ.render(a.spp)
+        if world > 1:  # gather the disjoint film tiles on rank 0
+            rgbw, sq = D.reduce_film(rgbw, sq, on_dev)
+        return rgbw
 
     for _ in range(a.warmup):
         job()
@@ -107,7 +126,7 @@ def main():
     s0 = dev.stats()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        job()
+        final = job()
     barrier()
     elapsed = time.perf_counter() - t0
     s1 = dev.stats()
@@ -117,28 +136,34 @@ def main():
     total_paths = paths_per_job * a.steps
     value = total_paths / elapsed / 1e6
 
-    # ---- timed-region pipeline figure: algorithmic bytes of trace + shade + shadow per wall second
+    # ---- §8d pipeline figure over the timed wall clock
     d = {k: s1[k] - s0[k] for k in s1}
+    if world > 1:
+        for k in ("segments", "density_lookups"):
+            d[k] = int(D.sum_over_ranks(d[k], on_dev))
     if vol:
         pipe_bytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
         pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
                     "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
                     "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
-                    "note": "density-grid gathers of k_volpath over the timed wall clock"}
+                    "note": "density-grid gathers of k_volpath over the timed wall clock, all ranks"}
         roofline = volume_roofline(d)
     else:
-        pipe_bytes = d["segments"] * (BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX) + d["shadow_rays"] * BYTES_SHADOW_PER_RAY
+        pipe_bytes = d["segments"] * BYTES_SEGMENT
         pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
                     "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
-                    "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
-                    "note": "all path kernels over the timed wall clock (3 path lanes run concurrently)"}
+                    "bytes_per_segment": BYTES_SEGMENT, "segments_per_step": int(d["segments"] / a.steps),
+                    "note": "SURVEY.md §8d: segments/s x 420 B over the timed wall clock, all ranks"}
         roofline = kernel_roofline(pg, scene, integ, device, a)
 
-    # ---- CPU baseline (oracle, rank 0, N = 1, bounded sample) + equal-spp RMSE on the sample
+    quality = None
+    if rank == 0 and world == 1 and not vol and not a.no_quality:
+        quality = quality_block(pg, scene, final, elapsed / a.steps, a)
+    # ---- CPU baseline (oracle, rank 0, N = 1, bounded sample of the same guided job)
     cpu = None
     rmse = None
     if rank == 0 and world == 1 and not a.no_cpu:
-        cpu, rmse = cpu_baseline(pg, scene, integ, a)
+        cpu, rmse = cpu_baseline(pg, scene, integ, final, a)
 
     if rank == 0:
         line = {
@@ -151,14 +176,14 @@ def main():
                                    f"iterations (1..{2 ** (a.train - 1)} spp) + {a.spp} spp render",
                        "scene": a.scene, "triangles": scene.num_triangles, "width": a.width, "height": a.height,
                        "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
-                       "parallelism": f"tile-shard x{world}, RCCL {a.exchange} per training iteration"},
+                       "parallelism": f"tile-shard x{world}, RCCL {a.exchange} per training iteration"
+                                      + (", film reduce to rank 0" if world > 1 else "")},
             "roofline": roofline,
             "pipeline": pipeline,
+            "quality": quality,
             "cpu_baseline": cpu,
             "rmse_vs_cpu": rmse,
-            "segments_per_path": round(d["segments"] / max(d["paths"], 1), 3),
-            "kernel_event_ms_per_step": {k: round(d[k] / a.steps, 2)
-                                         for k in (("volume_ms",) if vol else ("trace_ms", "shade_ms", "shadow_ms"))},
+            "segments_per_path": round(d["segments"] / max(total_paths, 1), 3),
         }
         print(json.dumps(line), flush=True)
     integ.postprocess()
@@ -170,10 +195,11 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
     """Roofline of the dominant kernel.  The timed job runs three path lanes concurrently, so a HIP
     event pair around one launch also covers the other lanes' kernels; per-kernel durations are
     therefore measured on a one-lane context (same scene, same trained SD-tree, guided final-render
-    passes, launches serialized on one stream) right after the timed region."""
+    passes without records, launches serialized on one stream) right after the timed region."""
     from mitsuba_path_guiding_amd.integrator import Device
     cfg = pg.capi.default_config(guiding=1, device=local, path_lanes=1, rank=integ.dev.cfg.rank,
-                                 world_size=integ.dev.cfg.world_size)
+                                 world_size=integ.dev.cfg.world_size,
+                                 bsdf_fraction_bound=integ.cfg.bsdf_fraction_bound)
     dev = Device(cfg)
     dev.upload(scene)
     dev.put_sdtree(integ.dev.get_sdtree())
@@ -184,28 +210,35 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
     dev.render_pass(spp, off)
     s1 = dev.stats()
     d = {k: s1[k] - s0[k] for k in s1}
-    kernels = {  # name: (total ms, algorithmic bytes, launches)
+    shaded = d["segments"] - d["escaped"]
+    kernels = {  # name: (total ms, algorithmic bytes, launches); record=False: no training-record bytes
         "k_trace": (d["trace_ms"], d["segments"] * BYTES_TRACE_PER_RAY, d["trace_launches"]),
-        "k_shade": (d["shade_ms"], d["segments"] * BYTES_SHADE_PER_VERTEX, d["shade_launches"]),
+        "k_shade": (d["shade_ms"], shaded * BYTES_SHADE_PER_VERTEX, d["shade_launches"]),
         "k_shadow": (d["shadow_ms"], d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["trace_launches"]),
     }
     dev.close()
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms, nbytes, launches = kernels[dom]
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic = None
+    traffic, source = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
             traffic = pj.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            source = {"file": "profiles/pmc_latest.json", "profiled": pj.get("source"),
+                      "revision": pj.get("revision")}
         except (OSError, ValueError):
             traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": dom,
-            "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
+            "kernel": dom, "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
             "avg_launch_ms": round(ms / max(launches, 1), 4),
-            "measured": f"1-lane context, guided {scene.width}x{scene.height} x {spp} spp with the trained tree",
+            "bytes_model": {"k_trace": f"{BYTES_TRACE_PER_RAY} B/ray", "k_shade": f"{BYTES_SHADE_PER_VERTEX} B/vertex "
+                            f"(+{BYTES_SHADE_RECORD} B when recording)", "k_shadow": f"{BYTES_SHADOW_PER_RAY} B/ray",
+                            "sum": f"{BYTES_SEGMENT} B/segment (SURVEY.md §8d)"},
+            "measured": f"1-lane context, guided {scene.width}x{scene.height} x {spp} spp with the trained tree, "
+                        f"no records",
             "kernels": {k: {"ms": round(v[0], 2), "launches": int(v[2]),
                             "achieved_gbs": round(v[1] / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else 0.0}
                         for k, v in kernels.items()}}
@@ -219,74 +252,143 @@ def volume_roofline(d):
     ms, launches = d["volume_ms"], max(d["volume_launches"], 1)
     nbytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic = None
+    traffic, source = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_volpath_latest.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("kernels", {}).get("k_volpath", {}).get("hbm_bytes_per_launch")
+            pj = json.load(open(pmc))
+            traffic = pj.get("kernels", {}).get("k_volpath", {}).get("hbm_bytes_per_launch")
+            source = {"file": "profiles/pmc_volpath_latest.json", "profiled": pj.get("source"),
+                      "revision": pj.get("revision")}
         except (OSError, ValueError):
             traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "kernel": "k_volpath",
-            "algorithmic_bytes_per_launch": int(nbytes / launches), "avg_launch_ms": round(ms / launches, 4),
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
+            "kernel": "k_volpath", "algorithmic_bytes_per_launch": int(nbytes / launches),
+            "avg_launch_ms": round(ms / launches, 4),
             "density_lookups_per_launch": int(d["density_lookups"] / launches),
             "measured": "timed job, HIP events around every k_volpath launch (one stream)"}
 
 
-def cpu_baseline(pg, scene, integ, a):
-    """Time the oracle (CPU restatement, all host cores) on a bounded sample of the same job: the
-    guided final render of the first tiles with the GPU-trained SD-tree, then compare GPU vs CPU at
-    equal spp on those pixels."""
+def load_gt(path=GT_C3):
+    z = np.load(path)
+    return z["mean_x256"].astype(np.float32) / np.float32(z["scale"]), int(z["spp"])
+
+
+def errors(x, gt):
+    """rel_rmse = sqrt(mean((x - gt)^2)) / mean(gt); relmse = mean((x - gt)^2 / (gt^2 + 1e-2 mean(gt)^2))
+    (relMSE on the image exposed to mean 1; C3's mean is 0.0018); _trim999 without the worst 0.1 %
+    of pixels; _dark = median over pixels darker than the mean (the room lit through the door)."""
+    d2 = (x.astype(np.float64) - gt) ** 2
+    rel = (d2 / (gt.astype(np.float64) ** 2 + 1e-2 * float(gt.mean()) ** 2)).mean(-1).ravel()
+    trim = np.sort(rel)[: max(1, int(len(rel) * 0.999))]
+    dark = (gt.mean(-1) < gt.mean()).ravel()
+    return {"rel_rmse": round(float(np.sqrt(d2.mean()) / gt.mean()), 5), "relmse": round(float(rel.mean()), 5),
+            "relmse_trim999": round(float(trim.mean()), 5),
+            "relmse_dark_median": round(float(np.median(rel[dark])), 5) if dark.any() else None}
+
+
+def image(rgbw):
+    return rgbw[..., :3] / np.maximum(rgbw[..., 3:4], 1)
+
+
+def quality_block(pg, scene, final, job_s, a):
+    """Equal-spp / equal-time relative errors against the committed 65,536-spp ground truth."""
+    if a.scene != "ajar_door" or (a.width, a.height) != (1280, 720) or not os.path.exists(GT_C3):
+        return None
+    from mitsuba_path_guiding_amd.integrator import Device
+    gt, gt_spp = load_gt()
+    out = {"ground_truth": f"tests/golden/c3_gt.npz: unguided GPU path tracer, {gt_spp} spp, seed 4242",
+           "guided": errors(image(final), gt)}
+    dev = Device(pg.capi.default_config())
+    dev.upload(scene)
+    dev.render_pass(a.spp, 0)  # warm-up + equal-spp image (independent of the guided streams' offsets)
+    ug = image(dev.read_film()[0])
+    dev.reset_film()
+    t = time.perf_counter()
+    dev.render_pass(a.spp, 0)
+    dev.read_film()
+    rate = a.spp / (time.perf_counter() - t)
+    out["unguided_equal_spp"] = dict(errors(ug, gt), spp=a.spp)
+    spp_eq = max(1, int(round(job_s * rate)))
+    dev.reset_film()
+    done = 0
+    while done < spp_eq:
+        k = min(1024, spp_eq - done)
+        dev.render_pass(k, done)
+        done += k
+    out["unguided_equal_time"] = dict(errors(image(dev.read_film()[0]), gt), spp=spp_eq)
+    dev.close()
+    g = out["guided"]
+    out["guided_over_unguided"] = {
+        f"{m}_{w}": round(g[m] / out[f"unguided_{w}"][m], 4)
+        for m in ("relmse", "relmse_trim999", "relmse_dark_median") for w in ("equal_spp", "equal_time")}
+    return out
+
+
+def cpu_baseline(pg, scene, integ, final, a):
+    """The oracle (CPU restatement, up to 16 host threads = the GPU box's CPU share) runs the same
+    guided job on a bounded sample: the full training (every pixel, 1..16 spp, its own records,
+    splat and refit) and the final render of a block of tiles from the image centre.  Returns the
+    CPU throughput over both, and the equal-spp RMSE of the GPU and the CPU images on those tiles
+    against the ground truth (RMSE_gpu / RMSE_cpu <= 1.01)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O  # checker / CPU baseline only
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16 threads
-    osc = O.OracleScene(pg.capi, scene)
-    tree = O.OracleSDTree(osc)
-    tree.deserialize(integ.dev.get_sdtree())
-    cfg = pg.capi.default_config(guiding=1)
+    host_cpus = os.cpu_count()
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host_cpus
+    cores = max(1, min(cores, 16))  # gpurun: size pools to the box's CPU share of 16
     vol = a.scene == "smoke"
-    if vol:
-        cfg = integ.cfg  # guided volpath, same parameters as the GPU job
-    W = scene.width
-    T = 32
-    tiles = []
-    for ty in range(0, scene.height, T):
-        for tx in range(0, W, T):
-            tiles.append([(y * W + x) for y in range(ty, min(ty + T, scene.height)) for x in range(tx, min(tx + T, W))])
-    spp = 64
+    osc = O.OracleScene(pg.capi, scene)
+    cfg = integ.cfg  # same integrator parameters as the GPU job
+    tree = O.OracleSDTree(osc)
+    t0 = time.perf_counter()
+    paths = 0
+    for it in range(a.train):
+        st = O.render(osc, cfg, 2 ** it, 2 ** it - 1, record=True, sdtree=tree, nthreads=cores)[2]
+        paths += int(st[0])
+        tree.splat_pending()
+        tree.refit(it, cfg)
+    t_train = time.perf_counter() - t0
+    same_tree = bool(np.array_equal(tree.serialize(), integ.dev.get_sdtree()))
+    W, T = scene.width, 32
+    tiles = [[y * W + x for y in range(ty, min(ty + T, scene.height)) for x in range(tx, min(tx + T, W))]
+             for ty in range(0, scene.height, T) for tx in range(0, W, T)]
     off = 2 ** a.train - 1
-    # warm up on one tile, calibrate on 16 tiles from the image centre, then size the sample to
-    # ~cpu_seconds of work
     mid = len(tiles) // 2
-    O.render(osc, cfg, 4, off, sdtree=tree, pixels=np.array(tiles[mid], np.uint32), nthreads=cores)
-    cal = np.array([p for i in range(16) for p in tiles[(mid + i) % len(tiles)]], np.uint32)
+    # calibrate on `cores` tiles (the oracle's threads take whole tiles) at 1/16 of the spp, then size
+    # the sample to ~cpu_seconds
+    cal = np.array([p for i in range(cores) for p in tiles[(mid + i) % len(tiles)]], np.uint32)
     t = time.perf_counter()
-    O.render(osc, cfg, spp, off, sdtree=tree, pixels=cal, nthreads=cores)
-    per_tile = (time.perf_counter() - t) / 16
-    ntiles = int(max(1, min(len(tiles), a.cpu_seconds / max(per_tile, 1e-4))))
-    sel = [tiles[(mid + i) % len(tiles)] for i in range(ntiles)]
-    pix = np.array([p for tl in sel for p in tl], np.uint32)
+    O.render(osc, cfg, max(1, a.spp // 16), off, sdtree=tree, pixels=cal, nthreads=cores)
+    per_tile = (time.perf_counter() - t) / cores * a.spp / max(1, a.spp // 16)
+    ntiles = int(max(cores, min(len(tiles), a.cpu_seconds / max(per_tile, 1e-4))))
+    ntiles = ntiles // cores * cores  # whole rounds of the oracle's tile workers
+    pix = np.array([p for i in range(ntiles) for p in tiles[(mid + i) % len(tiles)]], np.uint32)
     t = time.perf_counter()
-    c_rgbw, _, st = O.render(osc, cfg, spp, off, sdtree=tree, pixels=pix, nthreads=cores)
-    dt = time.perf_counter() - t
-    cpu = {"value": round(float(st[0]) / dt / 1e6, 4), "unit": "Mpaths/s", "cores": cores, "kind": "port",
-           "sample": f"{ntiles} tiles of 32x32 ({len(pix)} px) x {spp} spp of the guided {'C5' if vol else 'C3'} final render "
-                     f"with the GPU-trained SD-tree ({int(st[0])} paths, {dt:.1f} s)"}
-    # equal-spp GPU render of the same sample indices (fresh film; timed region is over)
-    integ.dev.reset_film()
-    integ.dev.render_pass(spp, off, False)
-    g_rgbw, _ = integ.dev.read_film()
-    g = g_rgbw.reshape(-1, 4)[pix]
-    c = c_rgbw.reshape(-1, 4)[pix]
-    gm = g[:, :3] / np.maximum(g[:, 3:4], 1)
-    cm = c[:, :3] / np.maximum(c[:, 3:4], 1)
-    rmse = float(np.sqrt(np.mean((gm - cm) ** 2)) / max(float(np.sqrt(np.mean(cm ** 2))), 1e-12))
-    rel = np.abs(gm - cm).max(-1) / np.maximum(cm.max(-1), 1e-3)
-    return cpu, {"relative_rmse": round(rmse, 6), "pixels_diverged_frac": round(float((rel > 1e-3).mean()), 6),
-                 "spp": spp, "pixels": int(len(pix)),
-                 "note": "same RNG streams on both sides; a path whose fp32 libm/FMA rounding flips one "
-                         "branch diverges, so the RMSE is dominated by the few diverged firefly pixels"}
+    c_rgbw, _, st = O.render(osc, cfg, a.spp, off, sdtree=tree, pixels=pix, nthreads=cores)
+    t_render = time.perf_counter() - t
+    paths += int(st[0])
+    cpu = {"value": round(paths / (t_train + t_render) / 1e6, 4), "unit": "Mpaths/s", "cores": cores,
+           "host_cpus": host_cpus, "kind": "port",
+           "sample": f"the guided {'C5' if vol else 'C3'} job on the CPU oracle: full training "
+                     f"({a.train} iterations, every pixel, {t_train:.1f} s) + the {a.spp}-spp final render of "
+                     f"{ntiles} tiles of 32x32 ({len(pix)} px, {t_render:.1f} s); {paths} paths"}
+    g = image(final).reshape(-1, 3)[pix]
+    c = image(c_rgbw).reshape(-1, 3)[pix]
+    rel = np.abs(g - c).max(-1) / np.maximum(c.max(-1), 1e-3)
+    rmse = {"gpu_vs_cpu_relative_rmse": round(float(np.sqrt(np.mean((g - c) ** 2)) /
+                                                    max(float(np.sqrt(np.mean(c ** 2))), 1e-12)), 6),
+            "pixels_diverged_frac": round(float((rel > 1e-3).mean()), 6), "same_sdtree": same_tree,
+            "spp": a.spp, "pixels": int(len(pix)),
+            "note": "CPU and GPU guided jobs on the same RNG streams; a path whose fp32 libm/FMA rounding "
+                    "flips one branch diverges"}
+    if not vol and os.path.exists(GT_C3) and (a.width, a.height) == (1280, 720):
+        gt = load_gt()[0].reshape(-1, 3)[pix]
+        eg, ec = np.sqrt(np.mean((g - gt) ** 2)), np.sqrt(np.mean((c - gt) ** 2))
+        rmse.update({"rmse_gpu_vs_gt": float(eg), "rmse_cpu_vs_gt": float(ec),
+                     "rmse_ratio_gpu_over_cpu": round(float(eg / ec), 5) if ec > 0 else None,
+                     "target": "<= 1.01 (SURVEY.md §8c(3))"})
+    return cpu, rmse
 
 
 if __name__ == "__main__":

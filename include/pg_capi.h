@@ -249,6 +249,7 @@ typedef struct pg_stats {
     double volume_ms;         /* device time of the volumetric path kernel (integrator = volpath) */
     uint64_t volume_launches;
     uint64_t density_lookups; /* volpath: trilinear density-grid lookups (tentative collisions) */
+    uint64_t escaped;         /* path integrator: segments whose ray left the scene (not shaded) */
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

@@ -98,7 +98,7 @@ class pg_stats(C.Structure):
                 ("trace_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double), ("other_ms", C.c_double),
                 ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
                 ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64),
-                ("density_lookups", C.c_uint64)]
+                ("density_lookups", C.c_uint64), ("escaped", C.c_uint64)]
 
 
 def default_config(**overrides):

@@ -1264,7 +1264,10 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             for (int sh = 0; sh < PG_QSHARDS; ++sh) {
                 const uint32_t v = hc[k * PG_QSHARDS + sh];
                 c->stats.segments += v;
-                if (k == PG_NUM_CLASSES) continue;
+                if (k == PG_NUM_CLASSES) {
+                    c->stats.escaped += v;
+                    continue;
+                }
                 m = std::max(m, v);
                 shardLive[sh] += v;
                 nlive += v;

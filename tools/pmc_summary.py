@@ -14,6 +14,7 @@ usage: python tools/pmc_summary.py gpurun_out/prof_rNN profiles/rNN
 import csv
 import json
 import os
+import subprocess
 import sys
 from collections import defaultdict
 
@@ -44,6 +45,19 @@ def load_counter(path, name):
     return {k: [v for _, v in sorted(l)] for k, l in acc.items()}
 
 
+def revision():
+    """git HEAD of the tree that was uploaded for the profile (run this right after the profile call)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    try:
+        head = subprocess.run(["git", "-C", root, "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                              text=True, timeout=10).stdout.strip()
+        dirty = subprocess.run(["git", "-C", root, "status", "--porcelain", "--untracked-files=no", "--", "*.hip",
+                                "*.cpp", "*.h", "*.py"], capture_output=True, text=True, timeout=10).stdout.strip()
+        return head + ("+dirty" if dirty else "") if head else None
+    except (OSError, subprocess.SubprocessError):
+        return None
+
+
 def mean(v):
     return sum(v) / len(v) if v else 0.0
 
@@ -65,7 +79,7 @@ def main(src, dst_prefix):
     # the run, so its launches are the last `calibration_calls` dispatches of each path kernel
     fetch = load_counter(os.path.join(src, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = load_counter(os.path.join(src, "write", "run_counter_collection.csv"), "WRITE_SIZE")
-    out = {"source": src, "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
+    out = {"source": src, "revision": revision(), "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 per launch",
            "calibration_stream": cal, "kernels": {}}
     for k, s in sorted(stats.items(), key=lambda kv: -kv[1]["total_ns"]):
         e = {"calls": s["calls"], "avg_ns": s["total_ns"] / s["calls"], "total_ns": s["total_ns"]}

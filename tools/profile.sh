@@ -10,9 +10,9 @@ cd "$ROOT"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T -d "$OUT/trace" -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu "$@" > "$OUT/trace.log" 2>&1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-quality "$@" > "$OUT/trace.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -T -d "$OUT/fetch" -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu "$@" > "$OUT/fetch.log" 2>&1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-quality "$@" > "$OUT/fetch.log" 2>&1
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -T -d "$OUT/write" -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --no-cpu "$@" > "$OUT/write.log" 2>&1
+    python3 bench.py --steps 1 --warmup 0 --no-cpu --no-quality "$@" > "$OUT/write.log" 2>&1
 echo "profile done"
