@@ -105,6 +105,7 @@ struct Lane {
     hipStream_t stream = nullptr;
     uint32_t P = 0;
     int vtx_slots = 0;
+    uint32_t vtxP = 0;  // slot stride of vtx (recording passes only allocate it)
     DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
     DevBuf aov;  // denoiser features per slot (pg_config.aovs), 2 x float4
     uint32_t *h_counts = nullptr;  // pinned: per-bounce class counts of the running chunk
@@ -339,7 +340,7 @@ PathDev pathView(const Lane *c) {
     return PathDev{c->ray_o.as<float4>(), c->ray_d.as<float4>(), c->hit.as<float4>(), c->thr.as<float4>(),
                    c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(), c->sh_o.as<float4>(),
                    c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->stack_ovf.as<uint32_t>(),
-                   c->P,                  c->aov.as<float4>()};
+                   c->P,                  c->vtxP,               c->aov.as<float4>()};
 }
 
 pg_status uploadSd(Ctx *c) {
@@ -402,9 +403,27 @@ EventPair nextEvents(Lane *l) {
     return pool[l->evused[l->evcur]++];
 }
 
-// path-state capacity of every lane for chunks of up to `want` paths
-pg_status ensurePaths(Ctx *c, uint32_t want) {
-    int vslots = (c->cfg.guiding ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0);
+// training-vertex slots per path of a pass (only recording passes write training vertices)
+int vertexSlots(const Ctx *c, bool rec) { return rec ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0; }
+
+// release every lane's path state (streams, events and counters stay)
+void releasePaths(Ctx *c) {
+    for (int li = 0; li < c->nlanes; ++li) {
+        Lane &l = c->lanes[li];
+        for (DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo, &l.sh_o, &l.sh_d, &l.sh_c,
+                          &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov})
+            b->release();
+        l.P = 0;
+        l.vtx_slots = 0;
+        l.vtxP = 0;
+    }
+}
+
+// path-state capacity of every lane for chunks of up to `want` paths; recording passes also need
+// vertex slots for `want` paths (a non-recording pass never allocates them: the 2^25-path chunks of
+// a final render would need ~51 GB per lane)
+pg_status ensurePaths(Ctx *c, uint32_t want, bool rec) {
+    const int vslots = vertexSlots(c, rec);
     for (int li = 0; li < c->nlanes; ++li) {
         Lane &l = c->lanes[li];
         if (!l.stream) {
@@ -417,9 +436,15 @@ pg_status ensurePaths(Ctx *c, uint32_t want) {
             HIPC(c, l.stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
         }
         const bool aovMissing = c->cfg.aovs && !l.aov.p;
-        if (want <= l.P && vslots <= l.vtx_slots && !aovMissing) continue;
+        if (vslots > 0 && (vslots > l.vtx_slots || want > l.vtxP)) {
+            const int vs = std::max(vslots, l.vtx_slots);
+            const uint32_t vp = std::max(want, l.vtxP);
+            HIPC(c, l.vtx.alloc((size_t)vs * vp * 48));
+            l.vtx_slots = vs;
+            l.vtxP = vp;
+        }
+        if (want <= l.P && !aovMissing) continue;
         const uint32_t P = std::max(want, l.P);
-        const int vs = std::max(vslots, l.vtx_slots);
         size_t f4 = (size_t)P * 16;
         HIPC(c, l.ray_o.alloc(f4));
         HIPC(c, l.ray_d.alloc(f4));
@@ -436,10 +461,8 @@ pg_status ensurePaths(Ctx *c, uint32_t want) {
         HIPC(c, l.q1.alloc(qbytes));
         HIPC(c, l.qs.alloc(qbytes));
         HIPC(c, l.class_q.alloc((size_t)PG_NUM_CLASSES * qbytes));
-        if (vs > 0) HIPC(c, l.vtx.alloc((size_t)vs * P * 48));
         if (c->cfg.aovs) HIPC(c, l.aov.alloc((size_t)P * 16));
         l.P = P;
-        l.vtx_slots = vs;
     }
     return PG_OK;
 }
@@ -1006,6 +1029,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     pv.rad = v.rad;
     pv.vtx = v.vtx;
     pv.P = want;
+    pv.vtxP = want;
     pv.pinfo = nullptr;  // k_commit reads the vertex count from rad[item].w
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix), pixPer = std::min(npix, want);
     std::vector<EventPair> evs;
@@ -1093,27 +1117,36 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
                                         &l.sh_d, &l.sh_c, &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov})
                     held += b->bytes;
             }
-            const int vs = c->cfg.guiding ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0;
+            const int vs = vertexSlots(c, rec);
             const double perPath = 10.0 * 16 + (3 + PG_NUM_CLASSES) * 4.0 + vs * 48.0 + (c->cfg.aovs ? 16.0 : 0.0);
             const double fit = 0.7 * (double)(freeB + held) / (perPath * c->nlanes);
             if (fit < (double)cap) cap = std::max<uint32_t>(1u << 20, (uint32_t)fit & ~4095u);
         }
     }
     uint64_t total = (uint64_t)npix * spp;
-    // chunk count rounded up to whole rounds of lanes, so that the last round keeps every lane busy
-    // (a rank of an N-GPU job may get only a few chunks of the final render); small passes split
-    // into one chunk per lane
-    uint64_t chunks = std::max<uint64_t>(1, (total + cap - 1) / cap);
-    chunks = (chunks + c->nlanes - 1) / c->nlanes * c->nlanes;
     uint32_t want;
-    if ((uint64_t)npix * chunks <= total) {  // whole sample layers per chunk
-        const uint64_t layers = (spp + chunks - 1) / chunks;
-        want = (uint32_t)std::min<uint64_t>(layers * npix, cap);
-    } else {
-        want = (uint32_t)std::min<uint64_t>((total + chunks - 1) / chunks, cap);
-    }
     pg_status s;
-    if ((s = ensurePaths(c, want))) return s;
+    for (;;) {
+        // chunk count rounded up to whole rounds of lanes, so that the last round keeps every lane busy
+        // (a rank of an N-GPU job may get only a few chunks of the final render); small passes split
+        // into one chunk per lane
+        uint64_t chunks = std::max<uint64_t>(1, (total + cap - 1) / cap);
+        chunks = (chunks + c->nlanes - 1) / c->nlanes * c->nlanes;
+        if ((uint64_t)npix * chunks <= total) {  // whole sample layers per chunk
+            const uint64_t layers = (spp + chunks - 1) / chunks;
+            want = (uint32_t)std::min<uint64_t>(layers * npix, cap);
+        } else {
+            want = (uint32_t)std::min<uint64_t>((total + chunks - 1) / chunks, cap);
+        }
+        s = ensurePaths(c, want, rec);
+        if (s != PG_ERR_OOM || cap <= (1u << 20)) break;
+        // out of device memory (e.g. contexts sharing a GPU sized their chunks from the same free
+        // memory): release the lanes and retry with half the chunk size, down to 2^20 paths
+        releasePaths(c);
+        (void)hipGetLastError();
+        cap = std::max<uint32_t>(1u << 20, (cap / 2) & ~4095u);
+    }
+    if (s) return s;
     GParams g = c->g;
     g.max_depth = c->cfg.max_depth;
     g.rr_depth = c->cfg.rr_depth;
@@ -1122,7 +1155,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     g.strict_normals = c->cfg.strict_normals;
     g.guiding = c->cfg.guiding;
     g.record = rec ? 1 : 0;
-    g.max_vertices = rec ? std::min(c->cfg.record_max_vertices, c->lanes[0].vtx_slots) : 0;
+    g.max_vertices = rec ? std::min(vertexSlots(c, rec), c->lanes[0].vtx_slots) : 0;
     g.max_component_value = c->cfg.max_component_value;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
     g.fraction_bound = c->cfg.bsdf_fraction_bound;

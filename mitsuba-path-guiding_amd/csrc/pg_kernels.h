@@ -25,7 +25,8 @@ struct PathDev {
     float4 *sh_o, *sh_d, *sh_c;
     float4 *vtx;       // [max_vertices][P][3]
     uint32_t *stack_ovf;  // traversal-stack overflow ring, pg_stack_overflow_words(0) words
-    uint32_t P;        // capacity (slot stride of vtx)
+    uint32_t P;        // path-state capacity
+    uint32_t vtxP;     // slot stride of vtx (recording passes)
     // denoiser features (pg_config.aovs), 1 per slot: the camera ray's hit record (t, tri | ~0, u, v),
     // written by the chunk's first k_trace; k_film turns it into albedo + normal sums.  nullptr: off.
     float4 *aov;

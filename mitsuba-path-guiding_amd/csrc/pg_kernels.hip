@@ -167,7 +167,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
             p.rad[slot] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
             uint32_t vi = __float_as_uint(c.w);
             if (vi != 0xFFFFFFFFu) {
-                float4 *vl = p.vtx + ((size_t)vi * p.P + slot) * 3 + 2;
+                float4 *vl = p.vtx + ((size_t)vi * p.vtxP + slot) * 3 + 2;
                 float4 a = *vl;
                 *vl = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w);
             }
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                     if (g.record && !(bs.type & EDelta) && nv < (uint32_t)g.max_vertices) {
                         float cu, cv;
                         dirToCanonical(wo, cu, cv);
-                        float4 *vb = p.vtx + ((size_t)nv * p.P + slot) * 3;
+                        float4 *vb = p.vtx + ((size_t)nv * p.vtxP + slot) * 3;
                         vb[0] = f4(h.p, woPdf);
                         vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
                         vb[2] = f4(L, 0.0f);
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int 
     float4 L = p.rad[slot];
     for (uint32_t k = 0; k < nv; ++k, ++o) {
         if (o >= capacity) return;
-        const float4 *vb = p.vtx + ((size_t)k * p.P + slot) * 3;
+        const float4 *vb = p.vtx + ((size_t)k * p.vtxP + slot) * 3;
         float4 a = vb[0], b = vb[1], c = vb[2];
         float woPdf = a.w;
         float lr = (b.x * woPdf > 1e-4f) ? (L.x - c.x) / b.x : 0.0f;
@@ -511,7 +511,9 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
         valid = woPdf > 0 && val >= 0 && val < 1e30f;
         if (valid) {
             float s = val * 16777216.0f;
-            if (s >= 4.0e18f) s = 4.0e18f;
+            // cap 2^48 (value <= 2^24): 2^16 records at the cap still fit one u64 quadrant sum, so the
+            // sums over records and ranks cannot wrap (oracle kSplatCap)
+            if (s >= 281474976710656.0f) s = 281474976710656.0f;
             fx = (unsigned long long)s;
             const SDView sv = sdv(sd);
             dt = sdLookup(sv, mk(a.x, a.y, a.z));

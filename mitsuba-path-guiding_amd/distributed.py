@@ -126,6 +126,20 @@ def reduce_film(rgbw, sumsq, on_device):
     return out[0], out[1]
 
 
+def make_reduce_sum(on_device):
+    """callable(np.ndarray float64) -> its element-wise sum over ranks (all-reduce)."""
+    import torch
+    import torch.distributed as dist
+
+    def reduce_sum(x):
+        tdev = torch.device("cuda", torch.cuda.current_device()) if on_device else torch.device("cpu")
+        t = torch.from_numpy(np.ascontiguousarray(x, np.float64)).to(tdev)
+        dist.all_reduce(t)
+        return t.cpu().numpy()
+
+    return reduce_sum
+
+
 def max_over_ranks(value, on_device):
     import torch
     import torch.distributed as dist

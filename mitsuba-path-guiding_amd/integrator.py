@@ -367,10 +367,13 @@ class GuidedPathTracer(ProgressivePathTracer):
 
     guided = True
 
-    def __init__(self, props=None, device=0, rank=0, world_size=1, exchange=None):
+    def __init__(self, props=None, device=0, rank=0, world_size=1, exchange=None, reduce_sum=None):
         super().__init__(props, device, rank, world_size)
         self.training_iterations = int(self.props.get("trainingIterations", 5))
-        self.exchange = exchange  # callable(dev) -> None: all-gather + splat into dev (N > 1)
+        self.exchange = exchange  # callable(dev): the postprogression statistics exchange (N > 1)
+        # callable(np.float64 array) -> its sum over ranks (N > 1): inverse-variance weights from the
+        # whole image, not this rank's tiles
+        self.reduce_sum = reduce_sum
         self.initial_tree = None
         self.sample_combination = str(self.props.get("sampleCombination", "discard")).lower()
         if self.sample_combination not in ("discard", "inversevar"):
@@ -418,25 +421,36 @@ class GuidedPathTracer(ProgressivePathTracer):
             return out
         films = [(f[0][:, ::-1], f[1][:, ::-1]) if getattr(self.dev.scene, "mirror_x", False) else f
                  for f in self.iteration_films] + [out]
-        return combine_inverse_variance(films, self)
+        return combine_inverse_variance(films, self, self.reduce_sum)
 
 
-def combine_inverse_variance(films, owner=None):
+def combine_inverse_variance(films, owner=None, reduce_sum=None):
     """Inverse-variance weighted combination of unbiased images given as film sums (rgbw, sumsq):
-    image i has per-pixel means m_i and variance estimate v_i = mean over pixels and channels of
-    (E[x^2] - m^2) / n.  Returns film-like sums (combined mean x total count, combined second moment
-    x total count) so that callers can keep dividing by the count channel."""
-    means, seconds, weights, counts = [], [], [], []
-    for rgbw, sq in films:
-        n = np.maximum(rgbw[..., 3:4], 1)
+    image i has per-pixel means m_i and variance estimate v_i = mean over the rendered pixels and
+    channels of (E[x^2] - m^2) / n.  With a tile shard, each rank holds only its tiles: reduce_sum
+    (a sum over ranks) turns the local sums and pixel counts into the whole image's, so every rank
+    uses the same weights and the result does not depend on the rank count.  Returns film-like sums
+    (combined mean x total count, combined second moment x total count) so that callers can keep
+    dividing by the count channel."""
+    means, seconds, counts = [], [], []
+    stats = np.zeros(2 * len(films), np.float64)  # per image: variance sum, channel count
+    for i, (rgbw, sq) in enumerate(films):
+        cnt = rgbw[..., 3:4]
+        n = np.maximum(cnt, 1)
         m = rgbw[..., :3] / n
         m2 = sq[..., :3] / n
-        v = float(np.mean(np.maximum(m2 - m * m, 0) / n))
-        w = 1.0 / v if v > 0 and np.isfinite(v) else 0.0
+        mask = np.broadcast_to(cnt > 0, m.shape)
+        stats[2 * i] = float(np.sum((np.maximum(m2 - m * m, 0) / n)[mask], dtype=np.float64))
+        stats[2 * i + 1] = float(mask.sum())
         means.append(m)
         seconds.append(m2)
-        weights.append(w)
-        counts.append(rgbw[..., 3:4])
+        counts.append(cnt)
+    if reduce_sum is not None:
+        stats = np.asarray(reduce_sum(stats), np.float64)
+    weights = []
+    for i in range(len(films)):
+        v = stats[2 * i] / stats[2 * i + 1] if stats[2 * i + 1] > 0 else 0.0
+        weights.append(1.0 / v if v > 0 and np.isfinite(v) else 0.0)
     W = np.asarray(weights, np.float64)
     if W.sum() <= 0:
         W = np.zeros_like(W)

@@ -25,6 +25,9 @@
 namespace orc {
 
 constexpr float kFixedScale = 16777216.0f;  // 2^24
+// per-record cap of the fixed-point value, 2^48 (radiance / woPdf <= 2^24): 2^16 records at the cap
+// still fit a u64 quadrant sum, so sums across records and ranks cannot wrap
+constexpr float kSplatCap = 281474976710656.0f;
 constexpr uint32_t kSdMagic = 0x44534750u;    // 'PGSD'
 
 struct SNode {
@@ -217,7 +220,7 @@ struct SDTree {
         float val = r.radiance / r.wo_pdf;
         if (!(val >= 0) || !(val < 1e30f)) return false;
         float s = val * kFixedScale;
-        if (s >= 4.0e18f) s = 4.0e18f;
+        if (s >= kSplatCap) s = kSplatCap;  // kernels: k_splat
         fixed = (uint64_t)s;
         return true;
     }

@@ -1,0 +1,173 @@
+"""GPU parity at the workloads the headline metric is quoted on:
+the HIP path through the C-ABI against the CPU oracle, with one SD-tree on both sides and the same
+counter-RNG streams, so that per-pixel agreement is far tighter than a Monte-Carlo tolerance.
+
+  C3  guided ajar door at the full 1280x720: the GPU trains the whole job (5 iterations), the
+      oracle renders a block of tiles of the final pass with the GPU's tree
+      (progressive_path.cpp:133-314, progressiveintegrator.cpp:222-282);
+  C4  guided kitchen class (~1 M triangles, 5 emitters) on a 4-rank tile shard: four shard contexts
+      train with the pg_get/put_tree_stats all-reduce and must hold the single-rank tree bit for
+      bit; the union of their final renders against the oracle with that tree;
+  C5  guided volumetric path tracer on the 256^3 smoke grid.
+Plus the chunk scheduler: tiny max_paths_in_flight (pixel-range chunks, many rounds of lanes) gives
+the default chunking's film and SD-tree bit for bit.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16  # the GPU box's CPU share
+
+
+def make_dev(pg, scene, **cfg):
+    from mitsuba_path_guiding_amd.integrator import Device
+    d = Device(pg.capi.default_config(**cfg))
+    d.upload(scene)
+    return d
+
+
+def tiles_of(scene, ntiles, T=32):
+    W, H = scene.width, scene.height
+    tiles = [[y * W + x for y in range(ty, min(ty + T, H)) for x in range(tx, min(tx + T, W))]
+             for ty in range(0, H, T) for tx in range(0, W, T)]
+    mid = len(tiles) // 2
+    return np.array([p for i in range(ntiles) for p in tiles[(mid + i) % len(tiles)]], np.uint32)
+
+
+def means(film):
+    rgbw, sq = film
+    n = np.maximum(rgbw[..., 3:4], 1)
+    m = rgbw[..., :3] / n
+    v = np.maximum(sq[..., :3] / n - m * m, 0) / n
+    return m, v
+
+
+def pixel_parity(g, c, pix):
+    """(z over the pixels, fraction of pixels whose means differ by more than 1e-3 relative)"""
+    mg, vg = means(g)
+    mc, vc = means(c)
+    mg, vg, mc, vc = (a.reshape(-1, 3)[pix] for a in (mg, vg, mc, vc))
+    z = (mg - mc) / np.sqrt(vg + vc + 1e-12)
+    rel = np.abs(mg - mc).max(-1) / np.maximum(mc.max(-1), 1e-3)
+    return z, float((rel > 1e-3).mean())
+
+
+def test_c3_guided_full_resolution(pg, O):
+    from mitsuba_path_guiding_amd.integrator import GuidedPathTracer
+    sc = pg.scenes.ajar_door(1280, 720)
+    integ = GuidedPathTracer({"trainingIterations": 5})
+    integ.preprocess(sc)
+    integ.train()
+    blob = integ.dev.get_sdtree()
+    st = integ.dev.stats()
+    assert st["stree_nodes"] > 1000 and st["records"] > 10_000_000
+    spp, off = 64, 31
+    integ.dev.reset_film()
+    integ.dev.render_pass(spp, off)
+    g = integ.dev.read_film()
+    cfg = integ.cfg
+    integ.postprocess()
+    osc = O.OracleScene(pg.capi, sc)
+    tree = O.OracleSDTree(osc)
+    tree.deserialize(blob)
+    pix = tiles_of(sc, 32)
+    c = O.render(osc, cfg, spp, off, sdtree=tree, pixels=pix, nthreads=THREADS)[:2]
+    assert np.array_equal(g[0].reshape(-1, 4)[pix, 3], c[0].reshape(-1, 4)[pix, 3])
+    z, diverged = pixel_parity(g, c, pix)
+    assert (np.abs(z) < 5).mean() > 0.999
+    assert diverged < 1e-3, diverged
+
+
+def test_c4_guided_four_rank_shard(pg, O):
+    sc = pg.scenes.kitchen(192, 108)
+    cfg = dict(guiding=1, s_tree_threshold=2000.0)
+    full = make_dev(pg, sc, **cfg)
+    shards = [make_dev(pg, sc, rank=r, world_size=4, **cfg) for r in range(4)]
+    off = 0
+    for it in range(4):
+        full.render_pass(2 ** it, off, True)
+        full.splat_local()
+        full.refit(it)
+        for d in shards:
+            d.render_pass(2 ** it, off, True)
+            d.splat_local()
+        total = sum(d.get_tree_stats() for d in shards)  # the all-reduce of the postprogression exchange
+        for d in shards:
+            d.put_tree_stats(total)
+            d.refit(it)
+        off += 2 ** it
+    blob = full.get_sdtree()
+    assert all(np.array_equal(d.get_sdtree(), blob) for d in shards)
+    assert full.stats()["stree_nodes"] > 1
+    spp = 16
+    films = []
+    for d in shards:
+        d.reset_film()
+        d.render_pass(spp, off)
+        films.append(d.read_film())
+    g = (sum(f[0] for f in films), sum(f[1] for f in films))
+    assert (g[0][..., 3] > 0).all() and g[0][..., 3].max() <= spp  # the shards tile the image exactly once
+    ocfg = pg.capi.default_config(**cfg)
+    osc = O.OracleScene(pg.capi, sc)
+    tree = O.OracleSDTree(osc)
+    tree.deserialize(blob)
+    c = O.render(osc, ocfg, spp, off, sdtree=tree, nthreads=THREADS)[:2]
+    assert (g[0][..., 3] == c[0][..., 3]).mean() > 0.999
+    z, diverged = pixel_parity(g, c, np.arange(sc.width * sc.height))
+    assert (np.abs(z) < 5).mean() > 0.999
+    assert diverged < 5e-3, diverged
+    for d in shards + [full]:
+        d.close()
+
+
+def test_c5_guided_volpath_256_grid(pg, O):
+    from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer
+    sc = pg.scenes.smoke(64, 64, res=256)
+    integ = GuidedVolumetricPathTracer({"trainingIterations": 3, "sTreeThreshold": 400.0})
+    integ.preprocess(sc)
+    integ.train()
+    blob = integ.dev.get_sdtree()
+    spp, off = 32, 7
+    integ.dev.reset_film()
+    integ.dev.render_pass(spp, off, True)
+    g = integ.dev.read_film()
+    nrec_gpu = integ.dev.record_count()
+    cfg = integ.cfg
+    integ.postprocess()
+    osc = O.OracleScene(pg.capi, sc)
+    tree = O.OracleSDTree(osc)
+    tree.deserialize(blob)
+    c = O.render(osc, cfg, spp, off, record=True, sdtree=tree, nthreads=THREADS)
+    nrec_cpu = int(c[2][3])
+    mg, _ = means(g)
+    mc, _ = means(c[:2])
+    z, _ = pixel_parity(g, c[:2], np.arange(64 * 64))
+    assert (np.abs(z) < 5).mean() > 0.999
+    close = np.abs(mg - mc).max(-1) <= 1e-3 * np.maximum(mc.max(-1), 1e-3)
+    assert close.mean() > 0.5, close.mean()
+    assert abs(nrec_gpu - nrec_cpu) <= 0.01 * nrec_cpu, (nrec_gpu, nrec_cpu)
+
+
+@pytest.mark.parametrize("paths", [1024, 4096])
+def test_small_chunks_bitexact(pg, paths):
+    """max_paths_in_flight far below the pass: pixel-range chunks (1024) or one layer per chunk
+    (4096), many rounds of three lanes, record-buffer growth with lanes in flight.  Films are
+    committed in chunk order and splats are integer, so film and SD-tree equal the default's."""
+    sc = pg.scenes.cornell(64, 64)
+    out = []
+    for cap in (0, paths):
+        d = make_dev(pg, sc, guiding=1, s_tree_threshold=300.0, max_paths_in_flight=cap)
+        off = 0
+        for it in range(3):
+            d.render_pass(2 ** it, off, True)
+            d.splat_local()
+            d.refit(it)
+            off += 2 ** it
+        d.reset_film()
+        d.render_pass(8, off, True)
+        out.append((d.read_film()[0], d.get_sdtree(), d.record_count(), d.stats()["paths"]))
+        d.close()
+    assert np.array_equal(out[0][0], out[1][0])
+    assert np.array_equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2] and out[0][3] == out[1][3]
