@@ -267,6 +267,13 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *scene);
  *      sample indices [sample_offset, sample_offset + spp).  record != 0 writes training
  *      records (only meaningful with guiding).  Accumulates into the film. ------------ */
 pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_t record);
+/* Time-budget rendering (maxRenderTime; ProgressiveMonteCarloIntegrator::renderTime,
+ * src/librender/progressiveintegrator.cpp:117-168,185,207-208): whole progressions of
+ * spp_per_progression samples, sample indices from sample_offset on, until `seconds` of wall clock
+ * have passed (checked after each batch of progressions) or max_spp samples are done (0 = no cap).
+ * *spp_done = samples per pixel rendered (the reference's m_spp after renderTime).  No records. */
+pg_status pg_render_time(void *ctx, double seconds, uint32_t spp_per_progression, uint32_t sample_offset,
+                         uint32_t max_spp, uint32_t *spp_done);
 
 /* ---- training records / SD-tree refit (the postprogression slot) ------------------------ */
 pg_status pg_get_record_count(void *ctx, uint64_t *count);

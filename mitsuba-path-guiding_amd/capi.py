@@ -146,6 +146,7 @@ SIGNATURES = [
     ("pg_cancel", C.c_int32, [VP]),
     ("pg_upload_scene", C.c_int32, [VP, C.POINTER(pg_scene_desc)]),
     ("pg_render_pass", C.c_int32, [VP, C.c_uint32, C.c_uint32, C.c_int32]),
+    ("pg_render_time", C.c_int32, [VP, C.c_double, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("pg_get_record_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
     ("pg_get_records", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, C.POINTER(C.c_uint64)]),
     ("pg_splat_records", C.c_int32, [VP, VP, C.c_uint64, C.c_int32]),

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -1375,6 +1376,41 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         c->rec_host_count = c->rec_bound = rc;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+// ProgressiveMonteCarloIntegrator::renderTime (progressiveintegrator.cpp:117-168): whole
+// progressions until the wall-clock budget is spent.  The reference checks the timer after every
+// progression of a 128-progression batch and cancels the rest; here consecutive progressions are
+// merged into one pg_render_pass (the film adds samples in sample order, so a merged pass equals
+// its progressions bit for bit), each merge covering at most half the remaining budget at the
+// measured rate, so the overshoot stays below one progression plus one readback.  Only whole
+// progressions reach the film: every pixel holds the same sample count (the reference may cancel
+// a progression midway, leaving some blocks with one progression more).
+pg_status pg_render_time(void *ctx, double seconds, uint32_t spp_per_progression, uint32_t sample_offset,
+                         uint32_t max_spp, uint32_t *spp_done) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !spp_done) return fail(c, PG_ERR_INVALID, "pg_render_time: null argument");
+    *spp_done = 0;
+    if (!(seconds > 0) || spp_per_progression == 0)
+        return fail(c, PG_ERR_INVALID, "pg_render_time: need seconds > 0 and spp_per_progression > 0");
+    const uint32_t limit = max_spp ? max_spp : 0x7FFFFFFFu;
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t done = 0, batch = std::min(spp_per_progression, limit);
+    while (done < limit) {
+        pg_status s = pg_render_pass(ctx, batch, sample_offset + done, 0);
+        if (s) return s;
+        done += batch;
+        *spp_done = done;
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el >= seconds) break;
+        const double perProg = el / (done / spp_per_progression);
+        const double progs = std::floor(0.5 * (seconds - el) / std::max(perProg, 1e-9));
+        const uint64_t want = (uint64_t)std::max(1.0, std::min(progs, 1e6)) * spp_per_progression;
+        batch = (uint32_t)std::min<uint64_t>(want, limit - done);
+        batch -= batch % spp_per_progression;  // whole progressions
+        if (batch == 0) break;
+    }
     return PG_OK;
 }
 

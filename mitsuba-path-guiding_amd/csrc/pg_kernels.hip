@@ -158,7 +158,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
         uint32_t slot = items[i];
         float4 o = p.sh_o[slot], d = p.sh_d[slot];
         float tmax = d.w;
-        uint32_t tri;
+        uint32_t tri = 0xFFFFFFFFu;
         float u, v;
         bool occ = traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
         if (!occ) {

@@ -169,7 +169,7 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
             const uint32_t tr = T.x + (uint32_t)(__ffs(T.y) - 1);
             T.y &= T.y - 1u;
             float tt, bu, bv;
-            if (woopHit(woop, tr, o, d, tmin, tmax, tt, bu, bv)) {
+            if (woopHit(woop, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {  // ties: lower index
                 found = true;
                 if (ANY) return true;
                 tmax = tt;
@@ -257,7 +257,10 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
                     if (a >= 0.0f && a <= 1.0f) {
                         const float4 w2 = woop[3 * tr + 2];
                         float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
-                        if (b >= 0.0f && a + b <= 1.0f) {
+                        // equal distances (shared edges, coplanar triangles) go to the lower triangle
+                        // index, so the closest hit does not depend on the order in which the wave's
+                        // postponed leaves are visited (and thus on which paths share the wave)
+                        if (b >= 0.0f && a + b <= 1.0f && (tt < tmax || tr < hitTri)) {
                             found = true;
                             if (ANY) return true;
                             tmax = tt;

@@ -101,6 +101,13 @@ class Device:
     def render_pass(self, spp, sample_offset=0, record=False):
         self._chk(self.lib.pg_render_pass(self.h, spp, sample_offset, int(bool(record))))
 
+    def render_time(self, seconds, spp_per_progression=1, sample_offset=0, max_spp=0):
+        """pg_render_time: whole progressions until `seconds` of wall clock; returns the spp rendered."""
+        n = C.c_uint32()
+        self._chk(self.lib.pg_render_time(self.h, float(seconds), int(spp_per_progression), int(sample_offset),
+                                          int(max_spp), C.byref(n)))
+        return n.value
+
     def cancel(self):
         self._chk(self.lib.pg_cancel(self.h))
 
@@ -285,6 +292,12 @@ class ProgressivePathTracer:
             aovs=int(bool(props.get("aovs", False))),
             bsdf_fraction_bound=_FRACTION_BOUNDS[str(props.get("bsdfSamplingFractionBound", "albedo")).lower()])
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
+        # maxRenderTime (progressiveintegrator.cpp:296-300): > 0 renders whole progressions until this
+        # many seconds have passed (renderTime, :117-168); rendered_spp / render_seconds report the
+        # outcome (the reference's m_spp and m_renderTime, :207-208)
+        self.max_render_time = float(props.get("maxRenderTime", -1.0))
+        self.rendered_spp = 0
+        self.render_seconds = 0.0
         self.dev = None
         self.progression = 0
         self.sample_offset = 0
@@ -309,13 +322,28 @@ class ProgressivePathTracer:
         self.sample_offset += spp
         self.postprogression()
 
-    def render(self, spp):
-        """renderSamples: spp / samplesPerProgression progressions; returns (rgbw, sumsq)."""
-        passes = max(1, spp // self.spp_per_progression)
-        for _ in range(passes):
-            if self._cancel.is_set():
-                return None
-            self.render_progression(self.spp_per_progression)
+    def render(self, spp, budget_start=None):
+        """renderSamples: spp / samplesPerProgression progressions, or with maxRenderTime > 0 renderTime
+        (whole progressions until the budget, counted from budget_start, is spent); returns (rgbw, sumsq)."""
+        import time
+        t0 = time.perf_counter() if budget_start is None else budget_start
+        if self.max_render_time > 0:
+            left = self.max_render_time - (time.perf_counter() - t0)
+            done = 0
+            if left > 0 and not self._cancel.is_set():
+                self.preprogression()
+                done = self.dev.render_time(left, self.spp_per_progression, self.sample_offset)
+                self.sample_offset += done
+                self.postprogression()
+            self.rendered_spp = done
+        else:
+            passes = max(1, spp // self.spp_per_progression)
+            for _ in range(passes):
+                if self._cancel.is_set():
+                    return None
+                self.render_progression(self.spp_per_progression)
+            self.rendered_spp = passes * self.spp_per_progression
+        self.render_seconds = time.perf_counter() - t0
         rgbw, sq = self.dev.read_film()
         if getattr(self.dev.scene, "mirror_x", False):  # a mirrored sensor (e.g. <scale x="-1"/> in toWorld)
             rgbw, sq = rgbw[:, ::-1].copy(), sq[:, ::-1].copy()
@@ -413,10 +441,14 @@ class GuidedPathTracer(ProgressivePathTracer):
         self.dev.refit(it)
 
     def render(self, spp):
+        """Training iterations, then the final render (spp, or with maxRenderTime > 0 whole
+        progressions until the budget, which includes the training time, is spent)."""
+        import time
+        t0 = time.perf_counter()
         self.iteration_films = []
         self.train()
         self.dev.reset_film()
-        out = super().render(spp)
+        out = super().render(spp, budget_start=t0)
         if out is None or self.sample_combination == "discard":
             return out
         films = [(f[0][:, ::-1], f[1][:, ::-1]) if getattr(self.dev.scene, "mirror_x", False) else f
