@@ -68,6 +68,7 @@ def parse():
     ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather"])
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU budget of the final-render sample")
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
+    ap.add_argument("--props", default="{}", help="extra integrator properties (JSON), for A/B runs")
     return ap.parse_args()
 
 
@@ -102,7 +103,7 @@ def main():
     # one progression for the final render (the device chunks it into 2^25-path chunks, 3 in flight)
     Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
     integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp, "pathLanes": a.lanes,
-                    "maxPathsInFlight": a.paths_in_flight}, device=device,
+                    "maxPathsInFlight": a.paths_in_flight, **json.loads(a.props)}, device=device,
                    rank=rank, world_size=world, exchange=exchange,
                    reduce_sum=D.make_reduce_sum(on_dev) if world > 1 else None)
     integ.preprocess(scene)

@@ -8,7 +8,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "build", "libpgamd.so")
+LIB_PATH = os.environ.get("PG_LIB") or os.path.join(_HERE, "build", "libpgamd.so")  # PG_LIB: A/B builds (tools)
 
 PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, PG_ERR_NO_DEVICE = range(7)
 (PG_BSDF_DIFFUSE, PG_BSDF_CONDUCTOR, PG_BSDF_ROUGHCONDUCTOR, PG_BSDF_DIELECTRIC, PG_BSDF_ROUGHDIELECTRIC,
