@@ -65,7 +65,9 @@ def parse():
     ap.add_argument("--no-quality", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3)")
     ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = auto: 2^25)")
-    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather"])
+    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather", "capi"],
+                    help="postprogression exchange: torch.distributed all-reduce of the tree statistics (default), "
+                         "record all-gather, or the library's own RCCL communicator (pg_comm_*, the C++ adapter's path)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU budget of the final-render sample")
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
     ap.add_argument("--props", default="{}", help="extra integrator properties (JSON), for A/B runs")
@@ -99,7 +101,11 @@ def main():
     device = local % max(1, torch.cuda.device_count())
     scene = pg.scenes.SCENES[a.scene](a.width, a.height)
     # postprogression exchange: all-reduce of the SD-tree building statistics
-    exchange = D.make_exchange(on_dev, mode=a.exchange) if world > 1 else None
+    capi_comm = world > 1 and a.exchange == "capi"
+    if world > 1:
+        exchange = D.make_capi_exchange() if capi_comm else D.make_exchange(on_dev, mode=a.exchange)
+    else:
+        exchange = None
     # one progression for the final render (the device chunks it into 2^25-path chunks, 3 in flight)
     Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
     integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp, "pathLanes": a.lanes,
@@ -108,6 +114,8 @@ def main():
                    reduce_sum=D.make_reduce_sum(on_dev) if world > 1 else None)
     integ.preprocess(scene)
     dev = integ.dev
+    if capi_comm:
+        D.init_capi_comm(dev)
 
     def barrier():
         if world > 1:
@@ -118,7 +126,10 @@ def main():
     def job():
         integ.reset()
         rgbw, sq = integ.render(a.spp)
-        if world > 1:  # gather the disjoint film tiles on rank 0
+        if capi_comm:  # RCCL reduce of the device films inside the library, then rank 0 reads it
+            dev.comm_reduce_film(0)
+            rgbw = dev.read_film()[0]
+        elif world > 1:  # gather the disjoint film tiles on rank 0
             rgbw, sq = D.reduce_film(rgbw, sq, on_dev)
         return rgbw
 

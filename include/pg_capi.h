@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 7
+#define PG_ABI_VERSION 8
 
 typedef int32_t pg_status;
 enum {
@@ -354,6 +354,27 @@ pg_status pg_get_tree_stats(void *ctx, void *dst, uint64_t capacity_words, int32
 pg_status pg_put_tree_stats(void *ctx, const void *src, uint64_t words, int32_t src_is_device);
 
 pg_status pg_rough_transmittance(uint32_t distribution, float alpha, float eta, float *table, float *fdr_int);
+
+/* ---- multi-GPU inside the library: one RCCL communicator per context (RCCL over xGMI) --------
+ * Replaces the reference's distributed rendering (the remote scheduler that ships work units and
+ * merges image blocks, include/mitsuba/core/sched_remote.h:50-236) for one render job: one
+ * process (or thread) per GPU, each with a context created with its rank / world_size (its tile
+ * shard).  Rank 0 calls pg_comm_unique_id and hands the PG_COMM_ID_BYTES bytes to every rank by
+ * any out-of-band channel (MPI_Bcast, a file, torch.distributed); then every rank calls
+ * pg_comm_init.  The pg_comm_* calls below are collective: every rank makes them, in the same
+ * order.  Postprogression slot: pg_splat_local_records; pg_comm_allreduce_tree_stats; pg_refit
+ * (every rank then holds the tree one GPU builds from all records, bit for bit).  End of the
+ * job: pg_comm_reduce_film(root), then the root's pg_read_film returns the whole image. */
+#define PG_COMM_ID_BYTES 128
+pg_status pg_comm_unique_id(void *id_out);
+pg_status pg_comm_init(void *ctx, const void *id);
+/* In-place sum over ranks of the building statistics (the pg_get_tree_stats vector) on the device. */
+pg_status pg_comm_allreduce_tree_stats(void *ctx);
+/* Sum of every rank's film (+ sums of squares, + feature buffers) into rank `root`'s film; the
+ * shards are disjoint, so the root's film equals the single-GPU film bit for bit. */
+pg_status pg_comm_reduce_film(void *ctx, int32_t root);
+/* In-place sum over ranks of n host doubles (e.g. inverse-variance combination statistics). */
+pg_status pg_comm_allreduce_f64(void *ctx, double *values, uint64_t n);
 
 #ifdef __cplusplus
 }

@@ -169,10 +169,16 @@ SIGNATURES = [
     ("pg_rough_transmittance", C.c_int32, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
     ("pg_get_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
     ("pg_put_tree_stats", C.c_int32, [VP, VP, C.c_uint64, C.c_int32]),
+    ("pg_comm_unique_id", C.c_int32, [VP]),
+    ("pg_comm_init", C.c_int32, [VP, VP]),
+    ("pg_comm_allreduce_tree_stats", C.c_int32, [VP]),
+    ("pg_comm_reduce_film", C.c_int32, [VP, C.c_int32]),
+    ("pg_comm_allreduce_f64", C.c_int32, [VP, VP, C.c_uint64]),
 ]
 
 
-PG_ABI_VERSION = 7  # include/pg_capi.h
+PG_ABI_VERSION = 8  # include/pg_capi.h
+PG_COMM_ID_BYTES = 128
 
 
 def load_library(path=None):

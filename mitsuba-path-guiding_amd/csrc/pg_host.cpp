@@ -3,6 +3,7 @@
 // src/librender/progressiveintegrator.cpp:65-114,222-282, re-expressed as a GPU wavefront loop),
 // training-record management and the SD-tree refit hook (postprogression, :314-317).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -171,6 +172,8 @@ struct Ctx {
     int sd_jump_bits = 0;
     PinnedBuf sd_stage;
     bool sd_dirty = true;
+    // multi-GPU: RCCL communicator over the job's ranks (pg_comm_init), one per context/device
+    ncclComm_t comm = nullptr;
     // stats
     pg_stats stats{};
 };
@@ -669,6 +672,7 @@ pg_status pg_destroy(void *ctx) {
     if (c->timing.b) (void)hipEventDestroy(c->timing.b);
     if (c->film_order) (void)hipEventDestroy(c->film_order);
     if (c->pass_start) (void)hipEventDestroy(c->pass_start);
+    if (c->comm) (void)ncclCommDestroy(c->comm);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return PG_OK;
@@ -1518,6 +1522,93 @@ pg_status pg_put_tree_stats(void *ctx, const void *src, uint64_t words, int32_t 
     const hipMemcpyKind k = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     HIPC(c, hipMemcpyAsync(c->sd_bsum.p, src, 32 * nb, k, c->stream));
     HIPC(c, hipMemcpyAsync(c->sd_count.p, (const uint64_t *)src + 4 * nb, 8 * nl, k, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+// ---- multi-GPU inside the library (RCCL over xGMI).  Replaces what the reference's remote
+// scheduler does for a distributed render (include/mitsuba/core/sched_remote.h:50-236: ship work
+// units to other machines, merge their image blocks): here every rank renders its tile shard, and
+// the only exchanges are the postprogression statistics all-reduce and the final film reduce.
+#define NCCLC(c, expr)                                                                            \
+    do {                                                                                          \
+        ncclResult_t _r = (expr);                                                                 \
+        if (_r != ncclSuccess) return fail(c, PG_ERR_HIP, std::string("RCCL: ") + #expr + ": " + \
+                                                              ncclGetErrorString(_r));              \
+    } while (0)
+
+static_assert(PG_COMM_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "pg_comm id size");
+
+pg_status pg_comm_unique_id(void *id_out) {
+    if (!id_out) return fail(nullptr, PG_ERR_INVALID, "pg_comm_unique_id: null argument");
+    ncclUniqueId id;
+    NCCLC(nullptr, ncclGetUniqueId(&id));
+    std::memcpy(id_out, &id, sizeof(id));
+    return PG_OK;
+}
+
+pg_status pg_comm_init(void *ctx, const void *id) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || !id) return fail(c, PG_ERR_INVALID, "pg_comm_init: null argument");
+    if (c->comm) return fail(c, PG_ERR_STATE, "pg_comm_init: communicator already initialised");
+    if (c->cfg.world_size < 1 || c->cfg.rank < 0 || c->cfg.rank >= c->cfg.world_size)
+        return fail(c, PG_ERR_INVALID, "pg_comm_init: rank / world_size of the config are inconsistent");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    NCCLC(c, ncclCommInitRank(&c->comm, c->cfg.world_size, uid, c->cfg.rank));
+    return PG_OK;
+}
+
+pg_status pg_comm_allreduce_tree_stats(void *ctx) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_comm_allreduce_tree_stats: null context");
+    if (!c->comm) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_tree_stats: no communicator (pg_comm_init)");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_tree_stats: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
+    // in place on the device building state: the u64 quadrant sums and per-D-tree record counts
+    // (the pg_get_tree_stats vector); integer sums, so every rank ends with identical statistics
+    NCCLC(c, ncclGroupStart());
+    NCCLC(c, ncclAllReduce(c->sd_bsum.p, c->sd_bsum.p, 4 * nb, ncclUint64, ncclSum, c->comm, c->stream));
+    NCCLC(c, ncclAllReduce(c->sd_count.p, c->sd_count.p, nl, ncclUint64, ncclSum, c->comm, c->stream));
+    NCCLC(c, ncclGroupEnd());
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_comm_reduce_film(void *ctx, int32_t root) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_comm_reduce_film: null context");
+    if (!c->comm) return fail(c, PG_ERR_STATE, "pg_comm_reduce_film: no communicator (pg_comm_init)");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_comm_reduce_film: no scene");
+    if (root < 0 || root >= c->cfg.world_size) return fail(c, PG_ERR_INVALID, "pg_comm_reduce_film: bad root");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const size_t nf = (size_t)c->g.width * c->g.height * 4;
+    // disjoint tile shards: every pixel has one non-zero contributor, so the f32 sum is exact
+    NCCLC(c, ncclGroupStart());
+    NCCLC(c, ncclReduce(c->film.p, c->film.p, nf, ncclFloat32, ncclSum, root, c->comm, c->stream));
+    NCCLC(c, ncclReduce(c->film_sq.p, c->film_sq.p, nf, ncclFloat32, ncclSum, root, c->comm, c->stream));
+    if (c->aov_albedo.p) {
+        NCCLC(c, ncclReduce(c->aov_albedo.p, c->aov_albedo.p, nf, ncclFloat32, ncclSum, root, c->comm, c->stream));
+        NCCLC(c, ncclReduce(c->aov_normal.p, c->aov_normal.p, nf, ncclFloat32, ncclSum, root, c->comm, c->stream));
+    }
+    NCCLC(c, ncclGroupEnd());
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_comm_allreduce_f64(void *ctx, double *values, uint64_t n) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!values && n)) return fail(c, PG_ERR_INVALID, "pg_comm_allreduce_f64: null argument");
+    if (!c->comm) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_f64: no communicator (pg_comm_init)");
+    if (!n) return PG_OK;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    DevBuf b;
+    HIPC(c, b.alloc(n * 8));
+    HIPC(c, hipMemcpyAsync(b.p, values, n * 8, hipMemcpyHostToDevice, c->stream));
+    NCCLC(c, ncclAllReduce(b.p, b.p, n, ncclFloat64, ncclSum, c->comm, c->stream));
+    HIPC(c, hipMemcpyAsync(values, b.p, n * 8, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }

@@ -115,6 +115,30 @@ def make_exchange(on_device, mode="allreduce"):
     return exchange_allreduce if mode == "allreduce" else exchange
 
 
+def init_capi_comm(dev):
+    """The library's own RCCL communicator (pg_comm_init), the multi-GPU path of the C++ adapter:
+    rank 0 draws the unique id (pg_comm_unique_id), torch.distributed broadcasts its bytes."""
+    import torch.distributed as dist
+    obj = [bytes(dev.comm_unique_id().tobytes()) if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    dev.comm_init(np.frombuffer(obj[0], np.uint8))
+
+
+def make_capi_exchange():
+    """exchange(dev) through the library's communicator (after init_capi_comm): splat the local
+    records, then pg_comm_allreduce_tree_stats (in-place RCCL all-reduce of the device building
+    statistics).  Returns every rank's record count."""
+    def exchange(dev):
+        import torch.distributed as dist
+        counts = np.zeros(dist.get_world_size(), np.float64)
+        counts[dist.get_rank()] = dev.record_count()
+        dev.splat_local()
+        dev.comm_allreduce_tree_stats()
+        return [int(x) for x in dev.comm_allreduce_f64(counts)]
+
+    return exchange
+
+
 def reduce_film(rgbw, sumsq, on_device):
     """Sum-reduce the (disjoint-tile) films of all ranks to rank 0; returns numpy arrays on rank 0."""
     import torch

@@ -163,6 +163,27 @@ class Device:
     def refit(self, iteration):
         self._chk(self.lib.pg_refit(self.h, iteration))
 
+    # -- multi-GPU inside the library (RCCL): the C++ adapter's exchange path
+    def comm_unique_id(self):
+        buf = np.zeros(capi.PG_COMM_ID_BYTES, np.uint8)
+        self._chk(self.lib.pg_comm_unique_id(_p(buf)))
+        return buf
+
+    def comm_init(self, uid):
+        uid = np.ascontiguousarray(uid, np.uint8)
+        self._chk(self.lib.pg_comm_init(self.h, _p(uid)))
+
+    def comm_allreduce_tree_stats(self):
+        self._chk(self.lib.pg_comm_allreduce_tree_stats(self.h))
+
+    def comm_reduce_film(self, root=0):
+        self._chk(self.lib.pg_comm_reduce_film(self.h, int(root)))
+
+    def comm_allreduce_f64(self, values):
+        v = np.ascontiguousarray(values, np.float64).copy()
+        self._chk(self.lib.pg_comm_allreduce_f64(self.h, _p(v), len(v)))
+        return v
+
     def get_sdtree(self):
         n = C.c_uint64()
         self._chk(self.lib.pg_get_sdtree(self.h, None, 0, C.byref(n)))

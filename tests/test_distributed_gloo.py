@@ -1,4 +1,4 @@
-"""World-size-2 gloo test of the multi-rank training path (CPU): tile sharding + the exchange of
+"""World-size-2 and -4 (C4's rank count) gloo tests of the multi-rank training path (CPU): tile sharding + the exchange of
 mitsuba_path_guiding_amd.distributed (both the building-statistics all-reduce and the record
 all-gather) + refit must leave every rank with the same SD-tree, bit for bit, and that tree must
 equal a single-rank training on the whole image (splats are exact fixed-point arithmetic, so
@@ -117,6 +117,11 @@ def _worker(rank, world, port, outdir, mode):
         assert len(counts) == world
         dev.refit(it)
     np.save(os.path.join(outdir, f"tree{rank}.npy"), dev.tree.serialize())
+    # final render of the shard with the trained tree, films summed to rank 0 (distributed.reduce_film)
+    rgbw, sq = O.render(dev.osc, cfg, 4, off, sdtree=dev.tree, pixels=dev.pixels, nthreads=1)[:2]
+    rgbw, sq = D.reduce_film(rgbw, sq, on_device=False)
+    if rank == 0:
+        np.save(os.path.join(outdir, "film.npy"), np.stack([rgbw, sq]))
     import torch.distributed as dist
     dist.barrier()
     dist.destroy_process_group()
@@ -130,14 +135,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("mode", ["allreduce", "allgather"])
-def test_two_rank_exchange_gives_identical_trees(pg, O, tmp_path, mode):
+@pytest.mark.parametrize("mode,world", [("allreduce", 2), ("allgather", 2), ("allreduce", 4)])
+def test_multi_rank_exchange_gives_identical_trees(pg, O, tmp_path, mode, world):
     import torch.multiprocessing as mp
-    world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     t0 = np.load(tmp_path / "tree0.npy")
-    t1 = np.load(tmp_path / "tree1.npy")
-    assert np.array_equal(t0, t1)
+    for r in range(1, world):
+        assert np.array_equal(t0, np.load(tmp_path / f"tree{r}.npy"))
     # single rank over the whole image, same sample indices -> same record multiset -> same tree
     sc = pg.scenes.cornell(RES, RES)
     cfg = pg.capi.default_config(guiding=1, s_tree_threshold=THR)
@@ -150,6 +154,10 @@ def test_two_rank_exchange_gives_identical_trees(pg, O, tmp_path, mode):
         tree.splat_pending()
         tree.refit(it, cfg)
     assert np.array_equal(tree.serialize(), t0)
+    # the reduced film equals the single-rank film bit for bit (disjoint tiles, one contributor each)
+    film = np.load(tmp_path / "film.npy")
+    rgbw, sq = O.render(osc, cfg, 4, off, sdtree=tree, nthreads=2)[:2]
+    assert np.array_equal(film[0], rgbw) and np.array_equal(film[1], sq)
 
 
 def test_shard_covers_image_once():
