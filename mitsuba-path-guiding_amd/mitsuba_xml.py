@@ -213,8 +213,7 @@ class _Loader:
             elif name in scenes.CONDUCTORS:
                 kw.update(conductor=name)
             else:
-                raise NotImplementedError(f"conductor material '{name}' (Cu, Al, Au, none or explicit eta/k; other "
-                                          "presets need Mitsuba's spectral data/ior/*.spd conversion)")
+                raise ValueError(f"conductor material '{name}' is not one of the reference's data/ior presets")
             m = scenes.material(typ, specular_reflectance=rgb("specularReflectance", 1.0), **kw)
             if "extEta" in P:  # roughconductor.cpp:173-188: eta and k are relative to the exterior
                 ext = ior("extEta", "air")

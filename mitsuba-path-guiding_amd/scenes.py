@@ -21,11 +21,18 @@ from . import capi
 
 # RGB conductor optical constants as produced by Mitsuba's spectral->RGB conversion of
 # data/ior/{Cu,Al,Au}.{eta,k}.spd (roughconductor.cpp:173-188, extEta = 1 for air).
-CONDUCTORS = {
-    "Cu": ((0.200438, 0.924033, 1.10221), (3.91295, 2.45285, 2.14219)),
-    "Al": ((1.65746, 0.880369, 0.521229), (9.22387, 6.26952, 4.83700)),
-    "Au": ((0.143119, 0.374957, 1.44248), (3.98316, 2.38572, 1.60322)),
-}
+def _load_conductors():
+    """RGB eta / k of the reference's conductor presets (data/ior/<name>.{eta,k}.spd through
+    Spectrum::fromContinuousSpectrum, roughconductor.cpp:173-188), derived by
+    tests/golden/make_conductor_fixture.py into conductors.json."""
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "conductors.json")) as f:
+        mats = json.load(f)["materials"]
+    return {name: (tuple(m["eta"]), tuple(m["k"])) for name, m in mats.items()}
+
+
+CONDUCTORS = _load_conductors()
 
 
 def _f4(v):
