@@ -583,4 +583,30 @@ void oracle_hg_query(float g, const float *in, const float *wog, uint64_t n, flo
     }
 }
 
+// MicrofacetDistribution queries (microfacet.h; the test_microfacet.cpp:47-90 adapter): per query
+// wi (n x 3; all zero = sampleAll / pdfAll, else sampleVisible / pdfVisible for that wi), a 2D sample
+// u (n x 2) and an optional normal mg (n x 3).  out n x 5: m.xyz, the density of m (sampleAll's own
+// pdf, or pdfVisible(wi, m)), the density of mg (0 without mg).
+void oracle_microfacet_query(int32_t type, float au, float av, const float *wi, const float *u, const float *mg,
+                             uint64_t n, float *out) {
+    const Microfacet all(type, au, av, false);
+    for (uint64_t i = 0; i < n; ++i) {
+        const V3 w(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]);
+        const bool vis = w.x != 0 || w.y != 0 || w.z != 0;
+        float pdf = 0;
+        V3 m = vis ? all.sampleVisible(w, u[2 * i], u[2 * i + 1]) : all.sampleAll(u[2 * i], u[2 * i + 1], pdf);
+        if (vis) pdf = all.pdfVisible(w, m);
+        float *o = out + 5 * i;
+        o[0] = m.x;
+        o[1] = m.y;
+        o[2] = m.z;
+        o[3] = pdf;
+        o[4] = 0.0f;
+        if (mg) {
+            const V3 g(mg[3 * i], mg[3 * i + 1], mg[3 * i + 2]);
+            o[4] = vis ? all.pdfVisible(w, g) : all.pdfAll(g);
+        }
+    }
+}
+
 }  // extern "C"

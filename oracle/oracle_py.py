@@ -52,6 +52,7 @@ def lib(capi):
             "oracle_set_volpath_eager": (None, [C.c_int32]),
             "oracle_medium_query": (None, [VP, C.c_int32, C.c_int32, VP, VP, C.c_uint64, VP]),
             "oracle_hg_query": (None, [C.c_float, VP, VP, C.c_uint64, VP]),
+            "oracle_microfacet_query": (None, [C.c_int32, C.c_float, C.c_float, VP, VP, VP, C.c_uint64, VP]),
             "oracle_render_aovs": (None, [VP, C.c_uint32, C.c_uint32, C.c_uint32, VP, VP]),
             "oracle_envmap_query": (C.c_int, [VP, C.c_int32, VP, C.c_uint64, VP]),
         }
@@ -218,6 +219,16 @@ def hg_query(capi, g, wi, u, wo_given=None):
     wg = None if wo_given is None else np.ascontiguousarray(wo_given, np.float32)
     out = np.zeros((len(a), 5), np.float32)
     lib(capi).oracle_hg_query(float(g), _p(a), _p(wg), len(a), _p(out))
+    return out
+
+
+def microfacet_query(capi, dist, au, av, wi, u, m_given=None):
+    """(m.xyz, density of m, density of m_given) per query; wi all zero = sampleAll / pdfAll."""
+    wi = np.ascontiguousarray(wi, np.float32)
+    u = np.ascontiguousarray(u, np.float32)
+    mg = None if m_given is None else np.ascontiguousarray(m_given, np.float32)
+    out = np.zeros((len(wi), 5), np.float32)
+    lib(capi).oracle_microfacet_query(int(dist), float(au), float(av), _p(wi), _p(u), _p(mg), len(wi), _p(out))
     return out
 
 
