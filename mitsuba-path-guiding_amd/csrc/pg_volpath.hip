@@ -624,7 +624,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         }
         if (P.depth >= maxDepth && maxDepth != -1) return false;
         if (g.strict_normals && -dot(h.geoN, P.d) * h.wi.z < 0) return false;
-        const GMat M = sc.mats[h.mat];
+        const GMat &M = sc.mats[h.mat];
         const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
         const uint32_t tm = v.tmed[P.its.tri];
         const bool guide = guiding && (M.type & ESmooth) && !(M.type & EDelta);
