@@ -291,13 +291,16 @@ def load_gt(path=GT_C3):
 def errors(x, gt):
     """rel_rmse = sqrt(mean((x - gt)^2)) / mean(gt); relmse = mean((x - gt)^2 / (gt^2 + 1e-2 mean(gt)^2))
     (relMSE on the image exposed to mean 1; C3's mean is 0.0018); _trim999 without the worst 0.1 %
-    of pixels; _dark = median over pixels darker than the mean (the room lit through the door)."""
+    of pixels; _dark = median over pixels darker than the mean (the room lit through the door, 96 % of
+    the image); _top100_share = the 100 worst pixels' share of relmse (single-sample glints)."""
     d2 = (x.astype(np.float64) - gt) ** 2
     rel = (d2 / (gt.astype(np.float64) ** 2 + 1e-2 * float(gt.mean()) ** 2)).mean(-1).ravel()
     trim = np.sort(rel)[: max(1, int(len(rel) * 0.999))]
     dark = (gt.mean(-1) < gt.mean()).ravel()
+    top = np.sort(rel)[::-1][:100]
     return {"rel_rmse": round(float(np.sqrt(d2.mean()) / gt.mean()), 5), "relmse": round(float(rel.mean()), 5),
             "relmse_trim999": round(float(trim.mean()), 5),
+            "relmse_top100_share": round(float(top.sum() / max(rel.sum(), 1e-30)), 4),
             "relmse_dark_median": round(float(np.median(rel[dark])), 5) if dark.any() else None}
 
 

@@ -403,8 +403,9 @@ class GuidedPathTracer(ProgressivePathTracer):
     """SD-tree guided progressive path tracer (Mueller et al. 2017 on the fork's scaffolding).
 
     Training: iteration k renders 2^k progressions' worth of spp with training records, then the
-    postprogression hook exchanges records (identity on one GPU; RCCL all-gather across ranks via
-    `exchange`), splats them into the building SD-tree and refits.  The film is reset before the
+    postprogression hook splats them into the building SD-tree (one GPU), or runs `exchange` (several
+    ranks: by default distributed.make_exchange's all-reduce of the building statistics over RCCL;
+    distributed.make_capi_exchange uses the library's own communicator), and refits.  The film is reset before the
     final render, which samples with the last trained tree.
 
     sampleCombination (after Mueller's practical-path-guiding course notes):
