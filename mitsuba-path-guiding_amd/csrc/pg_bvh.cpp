@@ -462,11 +462,27 @@ static bool buildBinaryBvh(const float *P, const uint32_t *I, uint32_t nt, uint3
     out.order = ord;
     out.woop.assign(12 * (size_t)nt, 0.0f);
     for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, ord[k], &out.woop[12 * (size_t)k]);
-    // ---- pack: inner nodes get GPU indices in DFS order; a leaf root gets a synthetic parent
+    // ---- pack: the inner nodes of the top PG_BVH_TOP_LEVELS levels first, breadth first (k_trace
+    // stages them in LDS), then the rest depth first; a leaf root gets a synthetic parent
     std::vector<int32_t> gpuIndex(bn.size(), -1);
     std::vector<int32_t> innerOrder;
     {
-        std::vector<int32_t> s{0};
+        std::vector<std::pair<int32_t, int>> level{{0, 0}};
+        std::vector<int32_t> frontier;  // children below the top levels, left to right
+        for (size_t k = 0; k < level.size(); ++k) {
+            const auto [n, d] = level[k];
+            if (bn[n].leaf) continue;
+            if (d >= PG_BVH_TOP_LEVELS) {
+                frontier.push_back(n);
+                continue;
+            }
+            gpuIndex[n] = (int32_t)innerOrder.size();
+            innerOrder.push_back(n);
+            level.push_back({bn[n].child[0], d + 1});
+            level.push_back({bn[n].child[1], d + 1});
+        }
+        out.top_nodes = (uint32_t)innerOrder.size();
+        std::vector<int32_t> s(frontier.rbegin(), frontier.rend());
         while (!s.empty()) {
             int32_t n = s.back();
             s.pop_back();
@@ -497,6 +513,7 @@ static bool buildBinaryBvh(const float *P, const uint32_t *I, uint32_t nt, uint3
         int32_t empty = (int32_t)(~0u << 4);  // ~((0 << 4) | 0) with count 0
         empty = ~(int32_t)0;                  // first 0, count 0
         putNode(&out.nodes[0], bn[0].box, ref(0), far, empty);
+        out.top_nodes = 1;
         return true;
     }
     out.nodes.assign(16 * innerOrder.size(), 0.0f);
@@ -520,6 +537,7 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         out.woop.clear();
         out.wwoop.clear();
         out.max_depth = out.wide_depth = 1;
+        out.top_nodes = 1;
         for (int a = 0; a < 3; ++a) out.lo[a] = out.hi[a] = 0.0f;
         return true;
     }

@@ -16,6 +16,7 @@ struct BvhOut {
     std::vector<float> woop;      // 12 floats per triangle (BVH order)
     std::vector<uint32_t> order;  // BVH-order -> original triangle id
     uint32_t max_depth = 0;
+    uint32_t top_nodes = 0;       // nodes [0, top_nodes): the top PG_BVH_TOP_LEVELS levels, breadth first
     // any-hit structure: 8-wide BVH, 4 * PG_WIDE_NODE_F4 floats per node (root = node 0), with its
     // own triangle order (shadow rays need no triangle id)
     std::vector<float> wnodes;

@@ -146,6 +146,7 @@ struct Ctx {
     uint64_t vol_vtx_cap = 0;
     uint32_t vol_cap = 0;
     uint32_t num_tris = 0, num_mats = 0;
+    uint32_t bvh_top_nodes = 0;  // breadth-first top levels of the binary BVH (staged in LDS by k_trace)
     std::vector<GMat> host_mats;
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};
     // shard
@@ -322,7 +323,7 @@ SceneDev sceneView(const Ctx *c) {
                     c->tshade.as<float4>(), c->tclass.as<uint8_t>(),
                     c->mats.as<GMat>(),
                     c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>(),
-                    c->has_env ? c->env.as<GEnv>() : nullptr};
+                    c->has_env ? c->env.as<GEnv>() : nullptr, c->bvh_top_nodes};
 }
 SDDev sdView(const Ctx *c) {
     SDDev s{};
@@ -825,6 +826,7 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     pg_status s;
     if ((s = upload(c, c->rtab, rtab))) return s;
     for (auto &mo : rtabOf) c->host_mats[mo.first].rtrans = c->rtab.as<float>() + mo.second;
+    c->bvh_top_nodes = std::min<uint32_t>(bvh.top_nodes, PG_BVH_TOP_NODES);
     if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) ||
         (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->wwoop, bvh.wwoop)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||

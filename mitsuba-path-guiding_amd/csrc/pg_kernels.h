@@ -17,6 +17,7 @@ struct SceneDev {
     const float4 *emtri;    // PG_TRI_SHADE_F4 float4 per emitter triangle
     const float *emcdf;
     const GEnv *env;        // environment emitter (the last emitter), or nullptr
+    uint32_t top_nodes;     // binary-BVH nodes [0, top_nodes) are the top levels (k_trace stages them in LDS)
 };
 
 struct PathDev {

@@ -10,6 +10,16 @@
 
 #include "pg_trace.h"
 
+// LDS staging of node and material tiles (measured, off by default: profiles/r02k_lds_ab/ -- C3
+// within noise to -1 %: the top BVH levels and the few materials already hit in L1, and the block
+// fill + barrier is paid by every short-lived shading block)
+#ifndef SHADE_LDS_MATS
+#define SHADE_LDS_MATS 0   // > 0: k_shade stages up to this many materials in LDS (64 = 8 KiB)
+#endif
+#ifndef PG_TRACE_LDS_TOP
+#define PG_TRACE_LDS_TOP 0  // 1: k_trace stages the BVH's top PG_BVH_TOP_LEVELS levels in LDS (2 KiB)
+#endif
+
 // =============================================================================================
 // camera rays: PerspectiveCamera::sampleRay (perspective.cpp:271-298) for (pixel, sample) slots
 __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint32_t *__restrict__ local_pixels,
@@ -120,10 +130,17 @@ template <bool ENV>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                        float4 *first) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    // the BVH's top levels (breadth first, pg_layout.h PG_BVH_TOP_NODES), staged in LDS once per block
+    __shared__ float4 top[(PG_TRACE_LDS_TOP ? PG_BVH_TOP_NODES : 1) * PG_BVH_NODE_F4];
     const TStack stk = threadStack(stack, p.stack_ovf);
     const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
     const uint32_t n = q.counts[s];
     const uint32_t *items = q.items + (size_t)s * q.stride;
+    const int ntop = PG_TRACE_LDS_TOP ? (int)sc.top_nodes : 0;
+    if (PG_TRACE_LDS_TOP) {
+        for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_BVH_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
+        __syncthreads();
+    }
     // block-uniform loop bound, so whole waves reach the class ballots together
     for (uint32_t base = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK; base < n; base += gridDim.x / PG_QSHARDS * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
@@ -135,7 +152,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
             float tmax = d.w;
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
-            bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+            bool h = traverse<false, PG_TRACE_LDS_TOP != 0>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk,
+                                                           top, ntop);
             const float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
             p.hit[slot] = hr;
             if (first) first[slot] = hr;
@@ -194,8 +212,17 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
     bool alive = false, shadow = false, dirtyL = false;
     uint32_t slot = 0;
     f3 L = mk1(0.f);
+    if (i < n) slot = in.items[(size_t)s * in.stride + i];
+    // the material table, staged in LDS once per block (the material read sits on the dependent chain
+    // hit -> triangle -> material of every shaded vertex); larger tables stay in global memory
+    __shared__ float4 smat[(SHADE_LDS_MATS > 0 ? SHADE_LDS_MATS : 1) * (sizeof(GMat) / 16)];
+    const bool ldsMats = SHADE_LDS_MATS > 0 && g.num_materials <= SHADE_LDS_MATS;
+    if (ldsMats) {
+        const float4 *src = reinterpret_cast<const float4 *>(sc.mats);
+        for (uint32_t k = threadIdx.x; k < g.num_materials * (uint32_t)(sizeof(GMat) / 16); k += SHADE_BLOCK) smat[k] = src[k];
+        __syncthreads();
+    }
     if (i < n) {
-        slot = in.items[(size_t)s * in.stride + i];
         do {
             uint4 pi = p.pinfo[slot];
             const uint32_t pix = pi.x, sample = pi.y;
@@ -240,7 +267,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                 }
             }
             if (depth > g.depth_cap) break;
-            const GMat M = sc.mats[h.mat];
+            const GMat M = ldsMats ? reinterpret_cast<const GMat *>(smat)[h.mat] : sc.mats[h.mat];
             if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
                 L = L + T * Le;
                 dirtyL = true;

@@ -104,6 +104,10 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 // child >= 0: inner node index; child < 0: leaf, ~child = (first_tri << 4) | count (count <= 15).
 #define PG_BVH_NODE_F4 4
 #define PG_LEAF_MAX 8
+// The inner nodes of the top PG_BVH_TOP_LEVELS levels come first, in breadth-first order (the rest
+// in depth-first order): k_trace stages nodes [0, SceneDev.top_nodes) in LDS once per block.
+#define PG_BVH_TOP_LEVELS 5
+#define PG_BVH_TOP_NODES 31
 
 // 8-wide BVH node for shadow rays, with quantised child boxes (5 x float4 = 80 B; after Ylitie et al. 2017):
 //   [0] p.xyz (quantisation origin = node box min), bits(ex | ey << 8 | ez << 16 | imask << 24)

@@ -190,10 +190,11 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
 // nodes until every lane of the wave holds a leaf, then all lanes test triangles together.  This
 // keeps the 64-wide wave in one code path most of the time (if-if traversal measured 23 % lane
 // utilisation on gfx950).
-template <bool ANY>
+// LTOP: nodes [0, ntop) are read from `lnodes` (the top levels, staged in LDS by the caller).
+template <bool ANY, bool LTOP = false>
 __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
                                          float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                         const TStack &stk) {
+                                         const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
     const int DONE = 0x7fffffff;
     const float eps = 1e-30f;
     const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
@@ -206,10 +207,18 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
     bool found = false;
     while (node != DONE) {
         while (node >= 0 && node != DONE) {
-            const float4 n0 = nodes[4 * node + 0];
-            const float4 n1 = nodes[4 * node + 1];
-            const float4 n2 = nodes[4 * node + 2];
-            const float4 n3 = nodes[4 * node + 3];
+            float4 n0, n1, n2, n3;
+            if (LTOP && node < ntop) {
+                n0 = lnodes[4 * node + 0];
+                n1 = lnodes[4 * node + 1];
+                n2 = lnodes[4 * node + 2];
+                n3 = lnodes[4 * node + 3];
+            } else {
+                n0 = nodes[4 * node + 0];
+                n1 = nodes[4 * node + 1];
+                n2 = nodes[4 * node + 2];
+                n3 = nodes[4 * node + 3];
+            }
             float a0 = fmaf(n0.x, idir.x, -ood.x), a1 = fmaf(n0.y, idir.x, -ood.x);
             float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
             float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
