@@ -7,7 +7,8 @@ pg = pgload.load()
 from mitsuba_path_guiding_amd.integrator import GuidedPathTracer
 
 sc = pg.scenes.ajar_door(1280, 720)
-integ = GuidedPathTracer({"trainingIterations": 5, "samplesPerProgression": 1024})
+world = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # emulate rank 0 of `world` (its tile shard)
+integ = GuidedPathTracer({"trainingIterations": 5, "samplesPerProgression": 1024}, rank=0, world_size=world)
 integ.preprocess(sc)
 d = integ.dev
 for rep in range(2):
@@ -24,6 +25,6 @@ for rep in range(2):
         tm(f"refit{it}", d.refit, it)
     tm("reset_film", d.reset_film)
     tm("final", d.render_pass, 1024, off, False)
-    print(f"rep {rep}: total {time.perf_counter()-t0:.3f} s  " + "  ".join(f"{k} {v*1e3:.1f}" for k, v in T.items()), flush=True)
+    print(f"world {world} rep {rep}: total {time.perf_counter()-t0:.3f} s  " + "  ".join(f"{k} {v*1e3:.1f}" for k, v in T.items()), flush=True)
     st = d.stats()
     print("  stree", st["stree_nodes"], "dtree", st["dtree_nodes"], flush=True)
