@@ -44,12 +44,12 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     f3 up = mk(g.cam_up[0], g.cam_up[1], g.cam_up[2]);
     f3 dir = mk(g.cam_dir[0], g.cam_dir[1], g.cam_dir[2]);
     f3 wd = left * d.x + up * d.y + dir * d.z;
-    p.ray_o[slot] = make_float4(g.cam_o[0], g.cam_o[1], g.cam_o[2], g.near_clip * invZ);
-    p.ray_d[slot] = f4(wd, g.far_clip * invZ);
-    p.thr[slot] = make_float4(1.f, 1.f, 1.f, 1.f);
-    p.rad[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-    p.prev[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
-    p.pinfo[slot] = make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u);
+    stS(&p.ray_o[slot], make_float4(g.cam_o[0], g.cam_o[1], g.cam_o[2], g.near_clip * invZ));
+    stS(&p.ray_d[slot], f4(wd, g.far_clip * invZ));
+    stS(&p.thr[slot], make_float4(1.f, 1.f, 1.f, 1.f));
+    stS(&p.rad[slot], make_float4(0.f, 0.f, 0.f, 0.f));
+    stS(&p.prev[slot], make_float4(0.f, 0.f, 0.f, 0.f));
+    stS(&p.pinfo[slot], make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u));
     q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
 }
 
@@ -148,19 +148,19 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
         uint32_t slot = 0;
         if (i < n) {
             slot = items[i];
-            float4 o = p.ray_o[slot], d = p.ray_d[slot];
+            float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.ray_d[slot]);
             float tmax = d.w;
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
             bool h = traverse<false, PG_TRACE_LDS_TOP != 0>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk,
                                                            top, ntop);
             const float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
-            p.hit[slot] = hr;
+            stS(&p.hit[slot], hr);
             if (first) first[slot] = hr;
             cls = h ? (int)sc.tclass[tri] : PG_NUM_CLASSES;
         }
         classAppend(cls, slot, cqs, s);
-        if (ENV && cls == PG_NUM_CLASSES) envEscape(g, sc, p, slot, xyz(p.ray_d[slot]));
+        if (ENV && cls == PG_NUM_CLASSES) envEscape(g, sc, p, slot, xyz(ldS(&p.ray_d[slot])));
     }
 }
 
@@ -174,15 +174,15 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
     const uint32_t *items = q.items + (size_t)s * q.stride;
     for (uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x / PG_QSHARDS * TRACE_BLOCK) {
         uint32_t slot = items[i];
-        float4 o = p.sh_o[slot], d = p.sh_d[slot];
+        float4 o = ldS(&p.sh_o[slot]), d = ldS(&p.sh_d[slot]);
         float tmax = d.w;
         uint32_t tri = 0xFFFFFFFFu;
         float u, v;
         bool occ = traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
         if (!occ) {
-            float4 c = p.sh_c[slot];
-            float4 L = p.rad[slot];
-            p.rad[slot] = make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w);
+            float4 c = ldS(&p.sh_c[slot]);
+            float4 L = ldS(&p.rad[slot]);
+            stS(&p.rad[slot], make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w));
             uint32_t vi = __float_as_uint(c.w);
             if (vi != 0xFFFFFFFFu) {
                 float4 *vl = p.vtx + ((size_t)vi * p.vtxP + slot) * 3 + 2;
@@ -224,19 +224,19 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
     }
     if (i < n) {
         do {
-            uint4 pi = p.pinfo[slot];
+            uint4 pi = ldS(&p.pinfo[slot]);
             const uint32_t pix = pi.x, sample = pi.y;
             uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16, nv = pi.w;
-            float4 hv = p.hit[slot];
-            float4 T4 = p.thr[slot];
-            float4 L4 = p.rad[slot];
+            float4 hv = ldS(&p.hit[slot]);
+            float4 T4 = ldS(&p.thr[slot]);
+            float4 L4 = ldS(&p.rad[slot]);
             f3 T = xyz(T4);
             L = xyz(L4);
             float eta = T4.w;
             uint32_t tri = __float_as_uint(hv.y);
             if (tri == 0xFFFFFFFFu) break;  // escaped: no environment emitter
             const uint32_t key = rngKey(pix, g.seed);
-            f3 rd = xyz(p.ray_d[slot]);
+            f3 rd = xyz(ldS(&p.ray_d[slot]));
             Hit h;
             fetchHit(sc, tri, hv.z, hv.w, rd, h);
             f3 Le = mk1(0.f);
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
             // ---- finish the previous bounce: emitter hit by the sampled direction (MIS), then RR
             if (depth > 1) {
                 if (h.emitter >= 0) {
-                    float4 pv = p.prev[slot];
+                    float4 pv = ldS(&p.prev[slot]);
                     float lumPdf = 0.0f;
                     if (g.use_nee && !(flags & PF_PREV_DELTA)) {
                         f3 prevRefN = xyz(pv);
@@ -373,31 +373,31 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
                         float cu, cv;
                         dirToCanonical(wo, cu, cv);
                         float4 *vb = p.vtx + ((size_t)nv * p.vtxP + slot) * 3;
-                        vb[0] = f4(h.p, woPdf);
-                        vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
-                        vb[2] = f4(L, 0.0f);
+                        stS(vb + 0, f4(h.p, woPdf));
+                        stS(vb + 1, f4(Tn, __uint_as_float(packCanonical(cu, cv))));
+                        stS(vb + 2, f4(L, 0.0f));
                         vtxIndex = nv;
                         nv++;
                     }
                     float tmin = kEpsilon * fmaxf(fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z)), kEpsilon);
-                    p.ray_o[slot] = f4(h.p, tmin);
-                    p.ray_d[slot] = f4(wo, __int_as_float(0x7f800000));
-                    p.thr[slot] = f4(Tn, eta * bs.eta);
-                    p.prev[slot] = f4(refN, woPdf);
+                    stS(&p.ray_o[slot], f4(h.p, tmin));
+                    stS(&p.ray_d[slot], f4(wo, __int_as_float(0x7f800000)));
+                    stS(&p.thr[slot], f4(Tn, eta * bs.eta));
+                    stS(&p.prev[slot], f4(refN, woPdf));
                     flags = (flags & ~(PF_EMITTED_QUERY | PF_PREV_DELTA)) | ((bs.type & EDelta) ? PF_PREV_DELTA : 0u);
-                    p.pinfo[slot] = make_uint4(pix, sample, (depth + 1) | (flags << 16), nv);
+                    stS(&p.pinfo[slot], make_uint4(pix, sample, (depth + 1) | (flags << 16), nv));
                     alive = true;
                 }
             }
             if (shadow) {
                 float tmin = kEpsilon * fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z));
-                p.sh_o[slot] = f4(h.p, tmin);
-                p.sh_d[slot] = f4(neeD, neeDist * (1 - kShadowEpsilon));
-                p.sh_c[slot] = f4(neeC, __uint_as_float(vtxIndex));
+                stS(&p.sh_o[slot], f4(h.p, tmin));
+                stS(&p.sh_d[slot], f4(neeD, neeDist * (1 - kShadowEpsilon)));
+                stS(&p.sh_c[slot], f4(neeC, __uint_as_float(vtxIndex)));
             }
-            if (!alive && nv != pi.w) p.pinfo[slot] = make_uint4(pix, sample, pi.z, nv);
+            if (!alive && nv != pi.w) stS(&p.pinfo[slot], make_uint4(pix, sample, pi.z, nv));
         } while (false);
-        if (dirtyL) p.rad[slot] = f4(L, 0.0f);
+        if (dirtyL) stS(&p.rad[slot], f4(L, 0.0f));
     }
     waveAppend(alive, slot, out.items + (size_t)s * out.stride, out.counts + s);
     waveAppend(shadow, slot, shq.items + (size_t)s * shq.stride, shq.counts + s);

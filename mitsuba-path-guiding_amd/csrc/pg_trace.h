@@ -16,6 +16,47 @@ using namespace pgd;
 
 namespace {
 
+// Path state is streamed: every SoA record is read once and written once per bounce, and a chunk's
+// state (hundreds of MB) never fits the 4 MiB L2 of an XCD.  Non-temporal accesses (PG_NT_STATE) keep
+// it from evicting what does get reused there: BVH nodes, triangles, materials, D-tree nodes.
+#ifndef PG_NT_STATE
+#define PG_NT_STATE 1
+#endif
+typedef float pg_v4f __attribute__((ext_vector_type(4)));
+typedef uint32_t pg_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldS(const float4 *p) {
+#if PG_NT_STATE
+    const pg_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pg_v4f *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ uint4 ldS(const uint4 *p) {
+#if PG_NT_STATE
+    const pg_v4u v = __builtin_nontemporal_load(reinterpret_cast<const pg_v4u *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void stS(float4 *p, float4 a) {
+#if PG_NT_STATE
+    const pg_v4f v = {a.x, a.y, a.z, a.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<pg_v4f *>(p));
+#else
+    *p = a;
+#endif
+}
+__device__ __forceinline__ void stS(uint4 *p, uint4 a) {
+#if PG_NT_STATE
+    const pg_v4u v = {a.x, a.y, a.z, a.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<pg_v4u *>(p));
+#else
+    *p = a;
+#endif
+}
+
 // ---------------------------------------------------------------------------------------------
 // BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,
 // sahkdtree3.h:178-308) with the same contract: closest t in [tmin, tmax] (any hit for shadow
