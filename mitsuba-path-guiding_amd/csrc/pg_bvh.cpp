@@ -267,13 +267,11 @@ int quantExponent(float extent) {
 
 }  // namespace
 
-// 8-wide BVH (for any-hit queries) with its own triangle order: wnodes + wwoop
-static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
-    std::vector<BNode> bn;
-    std::vector<uint32_t> ord;
-    uint32_t maxDepth = 0;
-    Box all;
-    buildBinary(P, I, nt, PG_WIDE_LEAF_MAX, bn, ord, maxDepth, all);
+// 8-wide BVH (for any-hit queries), collapsed from the binary tree (bn, ord); its leaf slots copy the
+// binary leaves' triangle ranges contiguously, and that copy order (out.order) is the one triangle
+// order of both BVHs: posOf[i] = the position of ord[i] in it.
+static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, const std::vector<BNode> &bn,
+                      const std::vector<uint32_t> &ord, BvhOut &out, std::vector<uint32_t> &posOf) {
     // ---- collapse to 8-wide nodes, SAH-optimal over the binary tree (dynamic programming after
     // Ylitie et al. 2017): dist[n][j] = cheapest way to spread subtree n over at most j slots of
     // one wide node; a slot is a leaf (subtree of <= PG_WIDE_LEAF_MAX triangles, one contiguous
@@ -362,6 +360,7 @@ static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t s
     std::vector<WTask> work{{0, 0, 1}};
     std::vector<float> nodes(PG_WIDE_NODE_F4 * 4, 0.0f);
     std::vector<uint32_t> order;
+    posOf.assign(nt, 0);
     order.reserve(nt);
     uint32_t wideDepth = 0;
     for (size_t w = 0; w < work.size(); ++w) {
@@ -411,7 +410,10 @@ static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t s
             }
             if (isLeafSlot(cn)) {
                 const uint32_t off = (uint32_t)order.size() - triBase;
-                for (uint32_t k = 0; k < rCount[cn]; ++k) order.push_back(ord[rFirst[cn] + k]);
+                for (uint32_t k = 0; k < rCount[cn]; ++k) {
+                    posOf[rFirst[cn] + k] = (uint32_t)order.size();
+                    order.push_back(ord[rFirst[cn] + k]);
+                }
                 meta[sl] = (uint8_t)(off | (rCount[cn] << 5));  // count 1..3 in bits 5-6 (0 = empty slot)
             } else {
                 imask |= 1u << sl;
@@ -441,27 +443,19 @@ static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t s
     out.wnodes.swap(nodes);
     out.wide_depth = wideDepth;
     if (wideDepth + 1 > stack_limit || order.size() != nt) return false;
-    out.wwoop.assign(12 * (size_t)nt, 0.0f);
-    for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, order[k], &out.wwoop[12 * (size_t)k]);
+    out.order.swap(order);
+    out.woop.assign(12 * (size_t)nt, 0.0f);
+    for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, out.order[k], &out.woop[12 * (size_t)k]);
     return true;
 }
 
-// binary BVH (for closest-hit queries): nodes + woop in `order`
-static bool buildBinaryBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
-    std::vector<BNode> bn;
-    std::vector<uint32_t> ord;
-    uint32_t maxDepth = 0;
-    Box all;
-    buildBinary(P, I, nt, PG_LEAF_MAX, bn, ord, maxDepth, all);
-    for (int a = 0; a < 3; ++a) {
-        out.lo[a] = all.lo[a];
-        out.hi[a] = all.hi[a];
-    }
+// binary BVH (for closest-hit queries) over the same tree: nodes whose leaves index the shared
+// triangle order (posOf: a binary leaf's triangles lie inside one wide leaf slot, so they stay
+// contiguous)
+static bool buildBinaryBvh(const std::vector<BNode> &bn, uint32_t maxDepth, const std::vector<uint32_t> &posOf,
+                           uint32_t stack_limit, BvhOut &out) {
     out.max_depth = maxDepth;
     if (maxDepth + 1 > stack_limit) return false;
-    out.order = ord;
-    out.woop.assign(12 * (size_t)nt, 0.0f);
-    for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, ord[k], &out.woop[12 * (size_t)k]);
     // ---- pack: the inner nodes of the top PG_BVH_TOP_LEVELS levels first, breadth first (k_trace
     // stages them in LDS), then the rest depth first; a leaf root gets a synthetic parent
     std::vector<int32_t> gpuIndex(bn.size(), -1);
@@ -494,7 +488,7 @@ static bool buildBinaryBvh(const float *P, const uint32_t *I, uint32_t nt, uint3
         }
     }
     auto ref = [&](int32_t n) -> int32_t {
-        if (bn[n].leaf) return (int32_t)(~((bn[n].first << 4) | bn[n].count));
+        if (bn[n].leaf) return (int32_t)(~((posOf[bn[n].first] << 4) | bn[n].count));
         return gpuIndex[n];
     };
     auto putNode = [&](float *o, const Box &b0, int32_t r0, const Box &b1, int32_t r1) {
@@ -535,13 +529,23 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         out.wnodes.assign(PG_WIDE_NODE_F4 * 4, 0.0f);
         out.order.clear();
         out.woop.clear();
-        out.wwoop.clear();
         out.max_depth = out.wide_depth = 1;
         out.top_nodes = 1;
         for (int a = 0; a < 3; ++a) out.lo[a] = out.hi[a] = 0.0f;
         return true;
     }
-    return buildBinaryBvh(P, I, nt, stack_limit, out) && buildWide(P, I, nt, stack_limit, out);
+    // one binary build (leaves <= PG_WIDE_LEAF_MAX triangles) serves both BVHs, and both walk one
+    // Woop triangle array in one order (the L2 of an XCD then holds one copy of the triangles)
+    std::vector<BNode> bn;
+    std::vector<uint32_t> ord, posOf;
+    uint32_t maxDepth = 0;
+    Box all;
+    buildBinary(P, I, nt, PG_WIDE_LEAF_MAX, bn, ord, maxDepth, all);
+    for (int a = 0; a < 3; ++a) {
+        out.lo[a] = all.lo[a];
+        out.hi[a] = all.hi[a];
+    }
+    return buildWide(P, I, nt, stack_limit, bn, ord, out, posOf) && buildBinaryBvh(bn, maxDepth, posOf, stack_limit, out);
 }
 
 }  // namespace pgh

@@ -1,7 +1,7 @@
-// Host-side BVH builders producing the GPU layouts of pg_layout.h from binned-SAH binary builds:
-// a binary BVH (64-B nodes, leaves <= 8 triangles) for closest-hit rays, and an 8-wide BVH with
-// quantised child boxes (80-B nodes, leaves <= 3 triangles, collapsed SAH-optimally) for shadow
-// rays, which it traverses with 28 % less time; 48-B Woop unit-triangle records for each.  Replaces the reference's SAH kd-tree build
+// Host-side BVH builders producing the GPU layouts of pg_layout.h from one binned-SAH binary build
+// (leaves <= 3 triangles): a binary BVH (64-B nodes) for closest-hit rays, and an 8-wide BVH with
+// quantised child boxes (80-B nodes, collapsed SAH-optimally from the same tree) for shadow rays,
+// which it traverses with 28 % less time.  Both index one array of 48-B Woop unit-triangle records.  Replaces the reference's SAH kd-tree build
 // (include/mitsuba/render/sahkdtree3.h, gkdtree.h) — only the closest-hit contract is kept.
 #pragma once
 #include <stdint.h>
@@ -13,14 +13,13 @@ namespace pgh {
 struct BvhOut {
     // closest-hit structure: binary BVH, 16 floats per node, leaves index `order`
     std::vector<float> nodes;
-    std::vector<float> woop;      // 12 floats per triangle (BVH order)
+    std::vector<float> woop;      // 12 floats per triangle (BVH order), shared by both BVHs
     std::vector<uint32_t> order;  // BVH-order -> original triangle id
     uint32_t max_depth = 0;
     uint32_t top_nodes = 0;       // nodes [0, top_nodes): the top PG_BVH_TOP_LEVELS levels, breadth first
-    // any-hit structure: 8-wide BVH, 4 * PG_WIDE_NODE_F4 floats per node (root = node 0), with its
-    // own triangle order (shadow rays need no triangle id)
+    // any-hit structure: 8-wide BVH, 4 * PG_WIDE_NODE_F4 floats per node (root = node 0), over the
+    // same triangle order
     std::vector<float> wnodes;
-    std::vector<float> wwoop;
     uint32_t wide_depth = 0;
     float lo[3], hi[3];
 };

@@ -103,7 +103,7 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 //   [2] c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z   [3] bits(child0), bits(child1), 0, 0
 // child >= 0: inner node index; child < 0: leaf, ~child = (first_tri << 4) | count (count <= 15).
 #define PG_BVH_NODE_F4 4
-#define PG_LEAF_MAX 8
+#define PG_LEAF_MAX 3  // the binary tree is the one the 8-wide BVH collapses (PG_WIDE_LEAF_MAX)
 // The inner nodes of the top PG_BVH_TOP_LEVELS levels come first, in breadth-first order (the rest
 // in depth-first order): k_trace stages nodes [0, SceneDev.top_nodes) in LDS once per block.
 #define PG_BVH_TOP_LEVELS 5
