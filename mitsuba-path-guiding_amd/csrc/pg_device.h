@@ -729,8 +729,8 @@ PGD uint32_t c4(uint4 c, int q) { return q == 0 ? c.x : (q == 1 ? c.y : (q == 2 
 struct SDView {
     const uint2 *snodes;
     const uint4 *meta;      // per D-tree: sampling root, building root, count, bits(samplingTotal)
-    const float4 *qsum;     // sampling nodes
-    const uint4 *qchild;
+    const float4 *qsum;     // sampling nodes, interleaved: node n = {qsum[2n] energies, qchild[2n] children}
+    const uint4 *qchild;    // = (const uint4 *)(qsum + 1)
     const uint32_t *jump;   // S-tree jump grid: (2^jumpBits)^3 cells -> node at depth <= 3*jumpBits
     float3 lo;
     float extent;           // cube edge; lookups divide by it (bit-identical with the host spec)
@@ -785,8 +785,8 @@ PGD float sdPdfCanon(const SDView &v, uint4 meta, float u, float w) {
     int depth = 1;
     for (int guard = 0; guard < 64; ++guard, ++depth) {
         int q = childIndex(u, w);
-        uint32_t c = c4(v.qchild[n], q);
-        if (c == 0) return telescopedPdf(q4(v.qsum[n], q), total, depth);
+        uint32_t c = c4(v.qchild[2 * (n)], q);
+        if (c == 0) return telescopedPdf(q4(v.qsum[2 * (n)], q), total, depth);
         n = c;
     }
     return 0.0f;
@@ -810,7 +810,7 @@ PGD void sdSampleCanon(const SDView &v, uint4 meta, float px, float py, float &c
     int depth = 0;
     float parentEnergy = total0;
     for (int guard = 0; guard < 64; ++guard) {
-        float4 s = v.qsum[n];
+        float4 s = v.qsum[2 * (n)];
         float total = quadTotal(s);
         if (!(total > 0)) {
             cu = ox + scale * px;
@@ -845,7 +845,7 @@ PGD void sdSampleCanon(const SDView &v, uint4 meta, float px, float py, float &c
         oy = oy + scale * qy;
         scale = scale * 0.5f;
         ++depth;
-        uint32_t c = c4(v.qchild[n], q);
+        uint32_t c = c4(v.qchild[2 * (n)], q);
         if (c == 0) {
             cu = ox + scale * px;
             cv = oy + scale * py;
@@ -882,9 +882,9 @@ PGD void sdDual(const SDView &v, uint4 meta, bool aOn, float au, float aw, float
     bool bEmpty = false;
     for (int guard = 0; guard < 64 && (aAct || bAct); ++guard) {
         // issue every load of this level before using any of them
-        const uint4 ach = v.qchild[an];
-        const uint4 bch = v.qchild[bn];
-        const float4 s = v.qsum[bn];
+        const uint4 ach = v.qchild[2 * (an)];
+        const uint4 bch = v.qchild[2 * (bn)];
+        const float4 s = v.qsum[2 * (bn)];
         if (aAct) {
             aq = childIndex(au, aw);
             const uint32_t c = c4(ach, aq);
@@ -954,10 +954,10 @@ PGD void sdDual(const SDView &v, uint4 meta, bool aOn, float au, float aw, float
             }
         }
     }
-    if (aOn) aPdf = aLeaf ? telescopedPdf(q4(v.qsum[an], aq), total0, ad) : 0.0f;
+    if (aOn) aPdf = aLeaf ? telescopedPdf(q4(v.qsum[2 * (an)], aq), total0, ad) : 0.0f;
     if (bOn) {
         if (!bSample) {
-            bPdf = bLeaf ? telescopedPdf(q4(v.qsum[bn], bq), total0, bd) : 0.0f;
+            bPdf = bLeaf ? telescopedPdf(q4(v.qsum[2 * (bn)], bq), total0, bd) : 0.0f;
         } else {
             cu = ox + scale * bu;
             cv = oy + scale * bw;

@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -119,6 +120,9 @@ struct Lane {
     hipEvent_t done = nullptr;     // last finished chunk's statistics copy
     bool stats_pending = false;
     uint32_t stats_bounces = 0;
+    // PG_DEBUG_COUNTS: per-bounce segment totals the host read (running chunk / last finished chunk),
+    // checked against the device counters of the finished chunk
+    std::vector<uint64_t> used_cur, used_prev;
     // running chunk
     bool active = false;
     bool traced = false;  // every path of the chunk terminated; film waits for its turn
@@ -169,7 +173,7 @@ struct Ctx {
     DevBuf ext_records;
     // sd-tree
     pgh::SdTree sd;
-    DevBuf sd_snodes, sd_meta, sd_qsum, sd_qchild, sd_bchild, sd_bsum, sd_count, sd_jump;
+    DevBuf sd_snodes, sd_meta, sd_qnode, sd_bchild, sd_bsum, sd_count, sd_jump;  // sd_qnode: {energies, children}
     int sd_jump_bits = 0;
     PinnedBuf sd_stage;
     bool sd_dirty = true;
@@ -329,8 +333,8 @@ SDDev sdView(const Ctx *c) {
     SDDev s{};
     s.snodes = c->sd_snodes.as<uint2>();
     s.meta = c->sd_meta.as<uint4>();
-    s.qsum = c->sd_qsum.as<float4>();
-    s.qchild = c->sd_qchild.as<uint4>();
+    s.qsum = c->sd_qnode.as<float4>();
+    s.qchild = reinterpret_cast<const uint4 *>(c->sd_qnode.as<float4>() + 1);
     s.bchild = c->sd_bchild.as<uint4>();
     s.bsum = c->sd_bsum.as<unsigned long long>();
     s.count = c->sd_count.as<unsigned long long>();
@@ -352,12 +356,18 @@ pg_status uploadSd(Ctx *c) {
     pgh::SdTree::Flat f;
     c->sd.flatten(f);
     const std::vector<uint64_t> count64(f.count.begin(), f.count.end());
+    // sampling nodes interleaved, 32 B each ({energies, children}): a walk reads one line per level
+    std::vector<uint32_t> qnode(2 * f.qsum.size());
+    for (size_t n = 0; n < f.qsum.size() / 4; ++n) {
+        std::memcpy(&qnode[8 * n], &f.qsum[4 * n], 16);
+        std::memcpy(&qnode[8 * n + 4], &f.qchild[4 * n], 16);
+    }
     struct Part {
         DevBuf *dst;
         const void *src;
         size_t bytes;
     } parts[] = {{&c->sd_snodes, f.snodes.data(), f.snodes.size() * 4}, {&c->sd_meta, f.meta.data(), f.meta.size() * 4},
-                 {&c->sd_qsum, f.qsum.data(), f.qsum.size() * 4},       {&c->sd_qchild, f.qchild.data(), f.qchild.size() * 4},
+                 {&c->sd_qnode, qnode.data(), qnode.size() * 4},
                  {&c->sd_bchild, f.bchild.data(), f.bchild.size() * 4}, {&c->sd_bsum, f.bsum.data(), f.bsum.size() * 8},
                  {&c->sd_count, count64.data(), count64.size() * 8},    {&c->sd_jump, f.jump.data(), f.jump.size() * 4}};
     size_t total = 0;
@@ -1213,6 +1223,16 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         for (uint32_t k = 0; k < l.stats_bounces; ++k)
             for (int sh = 0; sh < PG_QSHARDS; ++sh)
                 c->stats.shadow_rays += l.h_stats[(size_t)kBounceWords * k + kShadowCounts + sh];
+        if (std::getenv("PG_DEBUG_COUNTS")) {
+            for (uint32_t k = 0; k < l.stats_bounces && k < l.used_prev.size(); ++k) {
+                uint64_t t = 0;
+                for (int w = 0; w < (PG_NUM_CLASSES + 1) * PG_QSHARDS; ++w)
+                    t += l.h_stats[(size_t)kBounceWords * k + kClassCounts + w];
+                if (t != l.used_prev[k])
+                    std::fprintf(stderr, "PG_DEBUG_COUNTS: chunk bounce %u: host read %llu segments, device %llu\n", k,
+                                 (unsigned long long)l.used_prev[k], (unsigned long long)t);
+            }
+        }
         const int prev = l.evcur ^ 1;
         std::vector<EventPair> &pool = l.ev[prev];
         for (size_t e = 0; e + 2 < l.evused[prev]; e += 3) {
@@ -1288,6 +1308,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         HIPC(c, hipGetLastError());
         l.stats_pending = true;
         l.stats_bounces = l.b;
+        l.used_prev.swap(l.used_cur);
+        l.used_cur.clear();
         l.evcur ^= 1;
         c->stats.paths += l.n;
         return startChunk(l);
@@ -1313,6 +1335,11 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
                 nlive += v;
             }
             if (k < PG_NUM_CLASSES) clsMax[k] = m;
+        }
+        {
+            uint64_t t = 0;
+            for (int w = 0; w < (PG_NUM_CLASSES + 1) * PG_QSHARDS; ++w) t += hc[w];
+            l.used_cur.push_back(t);
         }
         ++l.b;
         if (nlive == 0 || l.b >= maxBounces) {

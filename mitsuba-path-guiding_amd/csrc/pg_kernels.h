@@ -36,8 +36,8 @@ struct PathDev {
 struct SDDev {
     const uint2 *snodes;
     const uint4 *meta;
-    const float4 *qsum;
-    const uint4 *qchild;
+    const float4 *qsum;        // sampling D-tree nodes, 32 B each: {float4 energies, uint4 children}
+    const uint4 *qchild;       // (const uint4 *)(qsum + 1); node n at index 2n of both
     const uint4 *bchild;
     unsigned long long *bsum;  // 4 per building node
     unsigned long long *count;  // records per D-tree (u64, so the building statistics are one u64 vector)

@@ -16,46 +16,13 @@ using namespace pgd;
 
 namespace {
 
-// Path state is streamed: every SoA record is read once and written once per bounce, and a chunk's
-// state (hundreds of MB) never fits the 4 MiB L2 of an XCD.  Non-temporal accesses (PG_NT_STATE) keep
-// it from evicting what does get reused there: BVH nodes, triangles, materials, D-tree nodes.
-#ifndef PG_NT_STATE
-#define PG_NT_STATE 1
-#endif
-typedef float pg_v4f __attribute__((ext_vector_type(4)));
-typedef uint32_t pg_v4u __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ float4 ldS(const float4 *p) {
-#if PG_NT_STATE
-    const pg_v4f v = __builtin_nontemporal_load(reinterpret_cast<const pg_v4f *>(p));
-    return make_float4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ uint4 ldS(const uint4 *p) {
-#if PG_NT_STATE
-    const pg_v4u v = __builtin_nontemporal_load(reinterpret_cast<const pg_v4u *>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-#else
-    return *p;
-#endif
-}
-__device__ __forceinline__ void stS(float4 *p, float4 a) {
-#if PG_NT_STATE
-    const pg_v4f v = {a.x, a.y, a.z, a.w};
-    __builtin_nontemporal_store(v, reinterpret_cast<pg_v4f *>(p));
-#else
-    *p = a;
-#endif
-}
-__device__ __forceinline__ void stS(uint4 *p, uint4 a) {
-#if PG_NT_STATE
-    const pg_v4u v = {a.x, a.y, a.z, a.w};
-    __builtin_nontemporal_store(v, reinterpret_cast<pg_v4u *>(p));
-#else
-    *p = a;
-#endif
-}
+// Path-state accesses (every SoA record is read once and written once per bounce).  Non-temporal
+// loads/stores here measured +1 % on C3 but made results timing-dependent with three lanes in flight
+// (2 outcomes in 12 runs of tools/det_kitchen.py, 1 in 20 without), so they are plain.
+__device__ __forceinline__ float4 ldS(const float4 *p) { return *p; }
+__device__ __forceinline__ uint4 ldS(const uint4 *p) { return *p; }
+__device__ __forceinline__ void stS(float4 *p, float4 a) { *p = a; }
+__device__ __forceinline__ void stS(uint4 *p, uint4 a) { *p = a; }
 
 // ---------------------------------------------------------------------------------------------
 // BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,
@@ -242,11 +209,18 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
                        1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
                        1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
     const f3 ood = o * idir;
+    // rounding of the slab distances fma(plane, idir, -o * idir) is bounded by a few ulps of |o * idir|
+    const float tslack = 1e-6f * fmaxf(fmaxf(fabsf(ood.x), fabsf(ood.y)), fabsf(ood.z));
     int sp = 0;
     int node = 0;   // >= 0 inner node, < 0 leaf ref, DONE
     int leaf = 0;   // postponed leaf ref (< 0) or none (>= 0)
     bool found = false;
     while (node != DONE) {
+        // boxes are culled against tmax widened by the slab-distance rounding: a triangle that ties
+        // with the current hit (shared edge, coplanar) can sit in a box whose rounded entry distance
+        // lands just past tmax, and skipping it would make the tie-break (lower index) depend on
+        // traversal order, i.e. on which paths share the wave
+        const float tcull = tmax * 1.000001f + tslack;
         while (node >= 0 && node != DONE) {
             float4 n0, n1, n2, n3;
             if (LTOP && node < ntop) {
@@ -264,12 +238,12 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
             float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
             float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
             float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), tmin));
-            float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), tmax));
+            float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), tcull));
             float b0 = fmaf(n1.x, idir.x, -ood.x), b1 = fmaf(n1.y, idir.x, -ood.x);
             float b2 = fmaf(n1.z, idir.y, -ood.y), b3 = fmaf(n1.w, idir.y, -ood.y);
             float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
             float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), tmin));
-            float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tmax));
+            float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tcull));
             const bool h0 = c0min <= c0max, h1 = c1min <= c1max;
             const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
             if (!h0 && !h1) {
