@@ -216,3 +216,28 @@ def test_max_render_time(pg):
     assert g.rendered_spp > 0 and g.render_seconds < budget + 0.25
     assert (rgbw[..., 3] == g.rendered_spp).mean() > 0.999
     g.postprocess()
+
+
+def test_training_independent_of_lanes_and_runs(pg):
+    """Paths are pure functions of (pixel, sample): guided kitchen training gives the same sorted
+    records, films and trees for 1 and 3 lanes in flight, and again on a fresh context (closest-hit
+    ties resolved independently of traversal order; DESIGN.md §4 Determinism)."""
+    sc = pg.scenes.kitchen(128, 72)
+
+    def train(lanes):
+        d = make_dev(pg, sc, guiding=1, s_tree_threshold=1500.0, path_lanes=lanes)
+        off, out = 0, []
+        for it in range(4):
+            d.render_pass(2 ** it, off, True)
+            rec = d.get_records().reshape(-1, 32)
+            out.append((_md5(rec[np.lexsort(rec.T[::-1])]), _md5(d.read_film()[0])))
+            d.splat_local()
+            d.refit(it)
+            off += 2 ** it
+        out.append(_md5(d.get_sdtree()))
+        d.close()
+        return out
+
+    a = train(3)
+    assert train(1) == a
+    assert train(3) == a
