@@ -210,7 +210,7 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
     therefore measured on a one-lane context (same scene, same trained SD-tree, guided final-render
     passes without records, launches serialized on one stream) right after the timed region."""
     from mitsuba_path_guiding_amd.integrator import Device
-    cfg = pg.capi.default_config(guiding=1, device=local, path_lanes=1, rank=integ.dev.cfg.rank,
+    cfg = pg.capi.default_config(guiding=1, device=local, path_lanes=1, kernel_timing=1, rank=integ.dev.cfg.rank,
                                  world_size=integ.dev.cfg.world_size,
                                  bsdf_fraction_bound=integ.cfg.bsdf_fraction_bound)
     dev = Device(cfg)

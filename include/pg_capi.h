@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 8
+#define PG_ABI_VERSION 9
 
 typedef int32_t pg_status;
 enum {
@@ -218,6 +218,10 @@ typedef struct pg_config {
                                      throughput max(T), so a path may regain throughput it lost, but not grow past 1.
                                      Any per-vertex choice independent of the sampled direction is unbiased.
                                      Default PG_FRACTION_ALBEDO (C3 quality). */
+    int32_t kernel_timing;        /* 1: bracket every closest-hit, shading and shadow launch with HIP events and sum
+                                     their device times into pg_stats trace_ms / shade_ms / shadow_ms.  Six event
+                                     records per bounce cost ~2 % on C3, so 0 (the default) leaves
+                                     those three statistics at 0. */
 } pg_config;
 enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2 };
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
@@ -238,7 +242,8 @@ typedef struct pg_stats {
     uint64_t segments;        /* path segments (extension rays) */
     uint64_t shadow_rays;
     uint64_t records;         /* training records written */
-    double trace_ms;          /* device time of the closest-hit kernel (HIP events; lanes overlap) */
+    double trace_ms;          /* device time of the closest-hit kernel (HIP events; lanes overlap; needs
+                                 pg_config.kernel_timing) */
     double shade_ms;          /* device time of the shading kernels (all material classes) */
     double shadow_ms;
     double other_ms;

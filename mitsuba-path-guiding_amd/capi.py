@@ -85,7 +85,8 @@ class pg_config(C.Structure):
                 ("record_max_vertices", C.c_int32), ("rank", C.c_int32), ("world_size", C.c_int32),
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
                 ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
-                ("distance_guiding", C.c_float), ("aovs", C.c_int32), ("bsdf_fraction_bound", C.c_int32)]
+                ("distance_guiding", C.c_float), ("aovs", C.c_int32), ("bsdf_fraction_bound", C.c_int32),
+                ("kernel_timing", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -128,6 +129,7 @@ def default_config(**overrides):
     c.distance_guiding = 0.25
     c.aovs = 0
     c.bsdf_fraction_bound = PG_FRACTION_ALBEDO
+    c.kernel_timing = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")
@@ -177,7 +179,7 @@ SIGNATURES = [
 ]
 
 
-PG_ABI_VERSION = 8  # include/pg_capi.h
+PG_ABI_VERSION = 9  # include/pg_capi.h
 PG_COMM_ID_BYTES = 128
 
 

@@ -600,6 +600,7 @@ pg_status pg_config_default(pg_config *c) {
     c->integrator = PG_INTEGRATOR_PATH;
     c->distance_guiding = 0.25f;
     c->bsdf_fraction_bound = PG_FRACTION_ALBEDO;
+    c->kernel_timing = 0;
     return PG_OK;
 }
 
@@ -1181,6 +1182,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const SceneDev sc = sceneView(c);
     const SDDev sd = sdView(c);
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
+    const bool evt = c->cfg.kernel_timing != 0;  // per-launch HIP events (pg_stats trace/shade/shadow_ms)
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
     const uint32_t pixPer = std::min(npix, want);
@@ -1206,11 +1208,12 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         uint32_t *cb = l.counters.as<uint32_t>() + (size_t)kBounceWords * l.b;
         Queue cls[PG_NUM_CLASSES + 1];
         classQueues(l, cb, cls);
-        EventPair et = nextEvents(&l);
-        HIPC(c, hipEventRecord(et.a, l.stream));
+        EventPair et{};
+        if (evt) et = nextEvents(&l);
+        if (evt) HIPC(c, hipEventRecord(et.a, l.stream));
         pg_launch_trace(l.stream, g, sc, pathView(&l), lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb),
                         l.bound, cls, l.b == 0);
-        HIPC(c, hipEventRecord(et.b, l.stream));
+        if (evt) HIPC(c, hipEventRecord(et.b, l.stream));
         HIPC(c, hipMemcpyAsync(l.h_counts + (size_t)kBounceWords * l.b + kClassCounts, cb + kClassCounts,
                                (PG_NUM_CLASSES + 1) * PG_QSHARDS * 4, hipMemcpyDeviceToHost, l.stream));
         HIPC(c, hipEventRecord(l.ready, l.stream));
@@ -1362,17 +1365,18 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         const PathDev pv = pathView(&l);
         const Queue next = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb + kBounceWords);
         const Queue shq = lqueue(l, l.qs.as<uint32_t>(), cb + kShadowCounts);
-        EventPair es = nextEvents(&l), ew = nextEvents(&l);
-        HIPC(c, hipEventRecord(es.a, l.stream));
+        EventPair es{}, ew{};
+        if (evt) es = nextEvents(&l), ew = nextEvents(&l);
+        if (evt) HIPC(c, hipEventRecord(es.a, l.stream));
         for (int k = 0; k < PG_NUM_CLASSES; ++k) {
             pg_launch_shade_class(l.stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
             c->stats.shade_launches += clsMax[k] ? 1 : 0;
         }
-        HIPC(c, hipEventRecord(es.b, l.stream));
+        if (evt) HIPC(c, hipEventRecord(es.b, l.stream));
         l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
-        HIPC(c, hipEventRecord(ew.a, l.stream));
+        if (evt) HIPC(c, hipEventRecord(ew.a, l.stream));
         pg_launch_shadow(l.stream, sc, pv, shq, l.bound);
-        HIPC(c, hipEventRecord(ew.b, l.stream));
+        if (evt) HIPC(c, hipEventRecord(ew.b, l.stream));
         return launchTrace(l);
     };
 

@@ -8,7 +8,7 @@ pg = pgload.load()
 from mitsuba_path_guiding_amd.integrator import Device, GuidedPathTracer
 
 for name, sc, spp in [("cornell", pg.scenes.cornell(512, 512), 64), ("ajar", pg.scenes.ajar_door(1280, 720), 16)]:
-    d = Device(pg.capi.default_config())
+    d = Device(pg.capi.default_config(kernel_timing=1))
     t = time.time(); d.upload(sc); print(name, "upload", time.time() - t, "tris", sc.num_triangles, flush=True)
     d.render_pass(1, 0)
     t = time.time(); d.render_pass(spp, 1); dt = time.time() - t

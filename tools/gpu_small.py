@@ -9,7 +9,7 @@ from mitsuba_path_guiding_amd.integrator import Device
 spp = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 lanes = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 for name, sc in [("cornell", pg.scenes.cornell(512, 512)), ("ajar", pg.scenes.ajar_door(1280, 720))]:
-    d = Device(pg.capi.default_config(path_lanes=lanes))
+    d = Device(pg.capi.default_config(path_lanes=lanes, kernel_timing=1))
     d.upload(sc)
     d.render_pass(1, 0)
     t = time.time(); d.render_pass(spp, 1); dt = time.time() - t

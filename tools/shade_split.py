@@ -18,7 +18,7 @@ g.render(4)
 tree = g.dev.get_sdtree()
 g.postprocess()
 for guided in (0, 1):
-    d = Device(pg.capi.default_config(guiding=guided, path_lanes=1))
+    d = Device(pg.capi.default_config(guiding=guided, path_lanes=1, kernel_timing=1))
     d.upload(sc)
     if guided:
         d.put_sdtree(tree)
