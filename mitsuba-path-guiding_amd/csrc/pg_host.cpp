@@ -353,40 +353,28 @@ PathDev pathView(const Lane *c) {
 }
 
 pg_status uploadSd(Ctx *c) {
-    pgh::SdTree::Flat f;
-    c->sd.flatten(f);
-    const std::vector<uint64_t> count64(f.count.begin(), f.count.end());
-    // sampling nodes interleaved, 32 B each ({energies, children}): a walk reads one line per level
-    std::vector<uint32_t> qnode(2 * f.qsum.size());
-    for (size_t n = 0; n < f.qsum.size() / 4; ++n) {
-        std::memcpy(&qnode[8 * n], &f.qsum[4 * n], 16);
-        std::memcpy(&qnode[8 * n + 4], &f.qchild[4 * n], 16);
-    }
-    struct Part {
-        DevBuf *dst;
-        const void *src;
-        size_t bytes;
-    } parts[] = {{&c->sd_snodes, f.snodes.data(), f.snodes.size() * 4}, {&c->sd_meta, f.meta.data(), f.meta.size() * 4},
-                 {&c->sd_qnode, qnode.data(), qnode.size() * 4},
-                 {&c->sd_bchild, f.bchild.data(), f.bchild.size() * 4}, {&c->sd_bsum, f.bsum.data(), f.bsum.size() * 8},
-                 {&c->sd_count, count64.data(), count64.size() * 8},    {&c->sd_jump, f.jump.data(), f.jump.size() * 4}};
-    size_t total = 0;
-    for (const Part &pt : parts) total += (pt.bytes + 255) & ~(size_t)255;
-    HIPC(c, c->sd_stage.reserve(total));
-    size_t off = 0;
-    for (const Part &pt : parts) {
-        HIPC(c, pt.dst->grow(std::max<size_t>(pt.bytes, 16)));
-        if (pt.bytes) {
-            uint8_t *h = (uint8_t *)c->sd_stage.p + off;
-            std::memcpy(h, pt.src, pt.bytes);
-            HIPC(c, hipMemcpyAsync(pt.dst->p, h, pt.bytes, hipMemcpyHostToDevice, c->stream));
-        }
-        off += (pt.bytes + 255) & ~(size_t)255;
+    // the device layout is written straight into the pinned staging buffer (no intermediate
+    // arrays), then copied part by part
+    const pgh::SdTree &t = c->sd;
+    const size_t R = (size_t)1 << pgh::SdTree::kJumpBits;
+    const size_t nl = t.leaves.size(), ns = t.samplingNodes(), nb = t.buildingNodes();
+    DevBuf *dst[] = {&c->sd_snodes, &c->sd_meta, &c->sd_qnode, &c->sd_bchild, &c->sd_bsum, &c->sd_count, &c->sd_jump};
+    const size_t bytes[] = {4 * t.snode.size(), 16 * nl, 32 * ns, 16 * nb, 32 * nb, 8 * nl, 4 * R * R * R};
+    size_t off[8] = {0};
+    for (int k = 0; k < 7; ++k) off[k + 1] = off[k] + ((bytes[k] + 255) & ~(size_t)255);
+    HIPC(c, c->sd_stage.reserve(off[7]));
+    uint8_t *h = (uint8_t *)c->sd_stage.p;
+    t.flattenInto(pgh::SdTree::Layout{(uint32_t *)(h + off[0]), (uint32_t *)(h + off[1]), (uint32_t *)(h + off[2]),
+                                      (uint32_t *)(h + off[3]), (uint64_t *)(h + off[4]), (uint64_t *)(h + off[5]),
+                                      (uint32_t *)(h + off[6])});
+    for (int k = 0; k < 7; ++k) {
+        HIPC(c, dst[k]->grow(std::max<size_t>(bytes[k], 16)));
+        if (bytes[k]) HIPC(c, hipMemcpyAsync(dst[k]->p, h + off[k], bytes[k], hipMemcpyHostToDevice, c->stream));
     }
     HIPC(c, hipStreamSynchronize(c->stream));
-    c->stats.stree_nodes = c->sd.snode.size() / 2;
-    c->stats.dtree_nodes = c->sd.samplingNodes();
-    c->sd_jump_bits = f.jump_bits;
+    c->stats.stree_nodes = t.snode.size() / 2;
+    c->stats.dtree_nodes = ns;
+    c->sd_jump_bits = pgh::SdTree::kJumpBits;
     c->sd_dirty = false;
     return PG_OK;
 }
@@ -989,6 +977,9 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         c->has_env = true;
     }
     c->sd.reset(c->scene_lo, c->scene_hi);
+    // pinned staging for the tree transfers, sized once for a large tree here (growing it inside a
+    // training loop re-pins memory, ~10-20 ms per growth)
+    HIPC(c, c->sd_stage.reserve((size_t)48 << 20));
     if ((s = uploadSd(c))) return s;
     HIPC(c, hipStreamSynchronize(c->stream));
     c->has_scene = true;
@@ -1520,11 +1511,21 @@ pg_status pg_refit(void *ctx, uint32_t iteration) {
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_refit: no scene");
     HIPC(c, hipSetDevice(c->cfg.device));
     pg_status s;
+    const auto t0 = std::chrono::steady_clock::now();
     if ((s = downloadSd(c))) return s;
+    const auto t1 = std::chrono::steady_clock::now();
     c->sd.refit(iteration, c->cfg.s_tree_threshold, c->cfg.d_tree_threshold, c->cfg.d_tree_max_depth);
+    const auto t2 = std::chrono::steady_clock::now();
     if ((s = uploadSd(c))) return s;
     HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 8, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
+    if (std::getenv("PG_DEBUG_REFIT")) {
+        const auto t3 = std::chrono::steady_clock::now();
+        auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        std::fprintf(stderr, "refit %u: download %.2f ms, refit %.2f ms, upload %.2f ms (%zu D-trees, %zu / %zu nodes)\n",
+                     iteration, ms(t0, t1), ms(t1, t2), ms(t2, t3), c->sd.leaves.size(), c->sd.samplingNodes(),
+                     c->sd.buildingNodes());
+    }
     c->rec_host_count = 0;
     return PG_OK;
 }

@@ -160,7 +160,7 @@ size_t SdTree::buildingNodes() const {
 // Jump grid for the device lookup: cell (x, y, z) of a 2^k grid -> the S-tree node reached after
 // following the cell's bits for 3k axis-cycling levels (or the leaf met on the way).
 static void fillJump(const std::vector<uint32_t> &sn, uint32_t node, int depth, int k, uint32_t x0, uint32_t y0,
-                     uint32_t z0, uint32_t sx, uint32_t sy, uint32_t sz, std::vector<uint32_t> &jump) {
+                     uint32_t z0, uint32_t sx, uint32_t sy, uint32_t sz, uint32_t *jump) {
     const uint32_t R = 1u << k;
     if (sn[2 * node] == kLeafMark || depth == 3 * k) {
         for (uint32_t z = z0; z < z0 + sz; ++z)
@@ -182,19 +182,10 @@ static void fillJump(const std::vector<uint32_t> &sn, uint32_t node, int depth, 
     }
 }
 
-void SdTree::flatten(Flat &f) const {
-    f.snodes = snode;
-    f.jump_bits = 6;
-    const uint32_t R = 1u << f.jump_bits;
-    f.jump.assign((size_t)R * R * R, 0);
-    fillJump(snode, 0, 0, f.jump_bits, 0, 0, 0, R, R, R, f.jump);
-    f.meta.assign(4 * leaves.size(), 0);
-    size_t ns = samplingNodes(), nb = buildingNodes();
-    f.qsum.assign(4 * ns, 0.0f);
-    f.qchild.assign(4 * ns, 0);
-    f.bchild.assign(4 * nb, 0);
-    f.bsum.assign(4 * nb, 0);
-    f.count.assign(leaves.size(), 0);
+void SdTree::flattenInto(const Layout &d) const {
+    std::memcpy(d.snodes, snode.data(), 4 * snode.size());
+    const uint32_t R = 1u << kJumpBits;
+    fillJump(snode, 0, 0, kJumpBits, 0, 0, 0, R, R, R, d.jump);
     std::vector<uint32_t> sbase(leaves.size()), bbase(leaves.size());
     for (size_t i = 0, sb = 0, bb = 0; i < leaves.size(); ++i) {
         sbase[i] = (uint32_t)sb;
@@ -205,22 +196,35 @@ void SdTree::flatten(Flat &f) const {
     parallelFor(leaves.size(), [&](size_t i) {
         const SdLeaf &L = leaves[i];
         const uint32_t sb = sbase[i], bb = bbase[i];
-        f.meta[4 * i + 0] = sb;
-        f.meta[4 * i + 1] = bb;
-        f.meta[4 * i + 2] = L.count;
-        std::memcpy(&f.meta[4 * i + 3], &L.total, 4);
-        for (size_t k = 0; k < L.sampling.size(); ++k)
-            for (int q = 0; q < 4; ++q) {
-                f.qsum[4 * (sb + k) + q] = L.sampling[k].sum[q];
-                f.qchild[4 * (sb + k) + q] = L.sampling[k].child[q] ? L.sampling[k].child[q] + sb : 0;
-            }
+        d.meta[4 * i + 0] = sb;
+        d.meta[4 * i + 1] = bb;
+        d.meta[4 * i + 2] = L.count;
+        std::memcpy(&d.meta[4 * i + 3], &L.total, 4);
+        for (size_t k = 0; k < L.sampling.size(); ++k) {
+            uint32_t *q = d.qnode + 8 * (sb + k);
+            std::memcpy(q, L.sampling[k].sum, 16);
+            for (int j = 0; j < 4; ++j) q[4 + j] = L.sampling[k].child[j] ? L.sampling[k].child[j] + sb : 0;
+        }
         for (size_t k = 0; k < L.building.size(); ++k)
             for (int q = 0; q < 4; ++q) {
-                f.bchild[4 * (bb + k) + q] = L.building[k].child[q] ? L.building[k].child[q] + bb : 0;
-                f.bsum[4 * (bb + k) + q] = L.building[k].sum[q];
+                d.bchild[4 * (bb + k) + q] = L.building[k].child[q] ? L.building[k].child[q] + bb : 0;
+                d.bsum[4 * (bb + k) + q] = L.building[k].sum[q];
             }
-        f.count[i] = L.count;
+        d.count[i] = L.count;
     });
+}
+
+void SdTree::flatten(Flat &f) const {
+    const size_t R = (size_t)1 << kJumpBits;
+    f.snodes.resize(snode.size());
+    f.meta.resize(4 * leaves.size());
+    f.qnode.resize(8 * samplingNodes());
+    f.bchild.resize(4 * buildingNodes());
+    f.bsum.resize(4 * buildingNodes());
+    f.count.resize(leaves.size());
+    f.jump.resize(R * R * R);
+    flattenInto(Layout{f.snodes.data(), f.meta.data(), f.qnode.data(), f.bchild.data(), f.bsum.data(), f.count.data(),
+                       f.jump.data()});
 }
 
 void SdTree::absorb(const uint64_t *bsum, const uint32_t *count) {
@@ -257,7 +261,7 @@ std::vector<uint8_t> SdTree::serialize() const {
     put(box, 32);
     Flat f;
     flatten(f);
-    uint32_t cnt[4] = {(uint32_t)(snode.size() / 2), (uint32_t)leaves.size(), (uint32_t)(f.qsum.size() / 4),
+    uint32_t cnt[4] = {(uint32_t)(snode.size() / 2), (uint32_t)leaves.size(), (uint32_t)(f.qnode.size() / 8),
                        (uint32_t)(f.bchild.size() / 4)};
     put(cnt, 16);
     put(snode.data(), 4 * snode.size());
@@ -266,10 +270,7 @@ std::vector<uint8_t> SdTree::serialize() const {
                          (uint32_t)leaves[i].building.size(), f.meta[4 * i + 3], leaves[i].count, 0, 0};
         put(m, 32);
     }
-    for (size_t k = 0; k < f.qsum.size() / 4; ++k) {
-        put(&f.qsum[4 * k], 16);
-        put(&f.qchild[4 * k], 16);
-    }
+    put(f.qnode.data(), 4 * f.qnode.size());  // {f32 sum[4], u32 child[4]} per node
     for (size_t k = 0; k < f.bchild.size() / 4; ++k) {
         put(&f.bsum[4 * k], 32);
         put(&f.bchild[4 * k], 16);

@@ -38,17 +38,22 @@ struct SdTree {
     std::vector<uint8_t> serialize() const;
     bool deserialize(const uint8_t *p, size_t n);
 
-    // flat views for upload
+    // the device layout (pg_kernels.h SDDev), written in place (e.g. into a pinned staging buffer)
+    static constexpr int kJumpBits = 6;
+    struct Layout {
+        uint32_t *snodes;  // 2 per S-tree node
+        uint32_t *meta;    // 4 per leaf: sampling base, building base, count, bits(total)
+        uint32_t *qnode;   // 8 per sampling node: f32 sum[4], u32 child[4] (absolute, 0 = leaf)
+        uint32_t *bchild;  // 4 per building node (absolute)
+        uint64_t *bsum;    // 4 per building node
+        uint64_t *count;   // per leaf
+        uint32_t *jump;    // (2^kJumpBits)^3 S-tree node ids, index (z * R + y) * R + x
+    };
+    void flattenInto(const Layout &d) const;
+    // the same layout in owned arrays (wire format, tests)
     struct Flat {
-        std::vector<uint32_t> snodes;   // 2 per node
-        std::vector<uint32_t> meta;     // 4 per leaf
-        std::vector<float> qsum;        // 4 per sampling node
-        std::vector<uint32_t> qchild;   // 4 per sampling node (absolute)
-        std::vector<uint32_t> bchild;   // 4 per building node (absolute)
-        std::vector<uint64_t> bsum;     // 4 per building node
-        std::vector<uint32_t> count;    // per leaf
-        std::vector<uint32_t> jump;     // (2^jump_bits)^3 S-tree node ids, index (z * R + y) * R + x
-        int jump_bits = 0;
+        std::vector<uint32_t> snodes, meta, qnode, bchild, jump;
+        std::vector<uint64_t> bsum, count;
     };
     void flatten(Flat &f) const;
     // absorb device-side building sums/counts (same absolute layout as flatten())
