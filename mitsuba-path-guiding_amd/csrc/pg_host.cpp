@@ -436,7 +436,7 @@ pg_status ensurePaths(Ctx *c, uint32_t want, bool rec) {
             HIPC(c, hipHostMalloc((void **)&l.h_counts, kCounterWords * 4, hipHostMallocDefault));
             HIPC(c, hipHostMalloc((void **)&l.h_stats, kCounterWords * 4, hipHostMallocDefault));
             HIPC(c, l.counters.alloc(kCounterWords * 4));
-            HIPC(c, l.stack_ovf.alloc(pg_stack_overflow_words(0) * 4));
+            HIPC(c, l.stack_ovf.alloc(2 * pg_stack_overflow_words(0) * 4));  // k_rays: two launches' worth
         }
         const bool aovMissing = c->cfg.aovs && !l.aov.p;
         if (vslots > 0 && (vslots > l.vtx_slots || want > l.vtxP)) {
@@ -1174,6 +1174,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const SDDev sd = sdView(c);
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
     const bool evt = c->cfg.kernel_timing != 0;  // per-launch HIP events (pg_stats trace/shade/shadow_ms)
+    const bool fuseRays = !evt && !c->has_env && !std::getenv("PG_NO_RAYS_FUSION");
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
     const uint32_t pixPer = std::min(npix, want);
@@ -1194,16 +1195,18 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
                                                  : nullptr,
                             cb + kClassCounts + k * PG_QSHARDS);
     };
-    // trace of bounce l.b (closest hit + material-class partition), then the class counts to the host
-    auto launchTrace = [&](Lane &l) -> pg_status {
+    // trace of bounce l.b (closest hit + material-class partition), then the class counts to the host;
+    // shq: the previous bounce's shadow queue, traced in the same launch (k_rays)
+    auto launchTrace = [&](Lane &l, const Queue *shq) -> pg_status {
         uint32_t *cb = l.counters.as<uint32_t>() + (size_t)kBounceWords * l.b;
         Queue cls[PG_NUM_CLASSES + 1];
         classQueues(l, cb, cls);
         EventPair et{};
         if (evt) et = nextEvents(&l);
         if (evt) HIPC(c, hipEventRecord(et.a, l.stream));
-        pg_launch_trace(l.stream, g, sc, pathView(&l), lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb),
-                        l.bound, cls, l.b == 0);
+        const Queue tq = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb);
+        if (shq) pg_launch_rays(l.stream, g, sc, pathView(&l), tq, l.bound, cls, *shq, l.bound);
+        else pg_launch_trace(l.stream, g, sc, pathView(&l), tq, l.bound, cls, l.b == 0);
         if (evt) HIPC(c, hipEventRecord(et.b, l.stream));
         HIPC(c, hipMemcpyAsync(l.h_counts + (size_t)kBounceWords * l.b + kClassCounts, cb + kClassCounts,
                                (PG_NUM_CLASSES + 1) * PG_QSHARDS * 4, hipMemcpyDeviceToHost, l.stream));
@@ -1270,7 +1273,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         HIPC(c, hipMemsetAsync(l.counters.p, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, l.stream));
         pg_launch_camera(l.stream, g, pathView(&l), c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl,
                          sample_offset + l.layer0, lqueue(l, l.q0.as<uint32_t>(), l.counters.as<uint32_t>()));
-        return launchTrace(l);
+        return launchTrace(l, nullptr);
     };
     // film + record commit (in chunk order across lanes), statistics copy; then the next chunk
     auto finishChunk = [&](Lane &l) -> pg_status {
@@ -1365,10 +1368,13 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         }
         if (evt) HIPC(c, hipEventRecord(es.b, l.stream));
         l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
+        // without per-launch timing (and without an environment emitter, whose escaped-path radiance
+        // would race with the same path's NEE add) the shadow rays share the next trace's launch
+        if (fuseRays) return launchTrace(l, &shq);
         if (evt) HIPC(c, hipEventRecord(ew.a, l.stream));
         pg_launch_shadow(l.stream, sc, pv, shq, l.bound);
         if (evt) HIPC(c, hipEventRecord(ew.b, l.stream));
-        return launchTrace(l);
+        return launchTrace(l, nullptr);
     };
 
     for (int li = 0; li < c->nlanes; ++li)

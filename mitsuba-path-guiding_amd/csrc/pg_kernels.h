@@ -93,6 +93,10 @@ void pg_launch_trace(hipStream_t s, const GParams &g, const SceneDev &sc, const 
                      const Queue *class_queues, bool first_bounce);
 void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
                            const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shadow);
+// shadow rays of a bounce and the closest hits of the next in one launch (k_rays; scenes without an
+// environment emitter): the pair pg_launch_shadow + pg_launch_trace without the aov hook
+void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
+                    const Queue *class_queues, Queue shq, uint32_t max_shadow_shard);
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);
 // aov_albedo / aov_normal: per-pixel feature sums, read when p.aov is set
 void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels,

@@ -123,26 +123,20 @@ __device__ __forceinline__ void classAppend(int cls, uint32_t slot, const ClassQ
     }
 }
 
+// closest hits of the rows of queue shard bid % PG_QSHARDS that block bid of nblk takes (a
+// grid-stride loop: k_trace, or the trace blocks of k_rays).
 // ENV: the scene has an environment emitter (escaped paths pick up its radiance)
-template <bool ENV>
 // first: the camera rays' bounce with denoiser features on (pg_config.aovs): the hit record of every
 // path also goes to p.aov, which k_film resolves into albedo and normal (nullptr: off)
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
-                                                       float4 *first) {
-    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
-    // the BVH's top levels (breadth first, pg_layout.h PG_BVH_TOP_NODES), staged in LDS once per block
-    __shared__ float4 top[(PG_TRACE_LDS_TOP ? PG_BVH_TOP_NODES : 1) * PG_BVH_NODE_F4];
-    const TStack stk = threadStack(stack, p.stack_ovf);
-    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+template <bool ENV, bool LTOP>
+__device__ __forceinline__ void traceRows(const GParams &g, const SceneDev &sc, const PathDev &p, const Queue &q,
+                                          const ClassQueues &cqs, float4 *first, uint32_t bid, uint32_t nblk,
+                                          const TStack &stk, const float4 *top, int ntop) {
+    const uint32_t s = bid & (PG_QSHARDS - 1);
     const uint32_t n = q.counts[s];
     const uint32_t *items = q.items + (size_t)s * q.stride;
-    const int ntop = PG_TRACE_LDS_TOP ? (int)sc.top_nodes : 0;
-    if (PG_TRACE_LDS_TOP) {
-        for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_BVH_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
-        __syncthreads();
-    }
     // block-uniform loop bound, so whole waves reach the class ballots together
-    for (uint32_t base = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK; base < n; base += gridDim.x / PG_QSHARDS * TRACE_BLOCK) {
+    for (uint32_t base = (bid / PG_QSHARDS) * TRACE_BLOCK; base < n; base += nblk / PG_QSHARDS * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
         int cls = -1;
         uint32_t slot = 0;
@@ -152,8 +146,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
             float tmax = d.w;
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
-            bool h = traverse<false, PG_TRACE_LDS_TOP != 0>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk,
-                                                           top, ntop);
+            bool h = traverse<false, LTOP>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk, top, ntop);
             const float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
             stS(&p.hit[slot], hr);
             if (first) first[slot] = hr;
@@ -164,15 +157,29 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
     }
 }
 
+template <bool ENV>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
+                                                       float4 *first) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    // the BVH's top levels (breadth first, pg_layout.h PG_BVH_TOP_NODES), staged in LDS once per block
+    __shared__ float4 top[(PG_TRACE_LDS_TOP ? PG_BVH_TOP_NODES : 1) * PG_BVH_NODE_F4];
+    const int ntop = PG_TRACE_LDS_TOP ? (int)sc.top_nodes : 0;
+    if (PG_TRACE_LDS_TOP) {
+        for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_BVH_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
+        __syncthreads();
+    }
+    traceRows<ENV, PG_TRACE_LDS_TOP != 0>(g, sc, p, q, cqs, first, blockIdx.x, gridDim.x, threadStack(stack, p.stack_ovf),
+                                          top, ntop);
+}
+
 // any hit for queued shadow rays; unoccluded -> add the NEE contribution to L (and to the
 // training vertex's radiance snapshot, so its record excludes light arriving from elsewhere)
-__global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, Queue q) {
-    __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];
-    const WStack stk = threadWideStack(stack, p.stack_ovf);
-    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+__device__ __forceinline__ void shadowRows(const SceneDev &sc, const PathDev &p, const Queue &q, uint32_t bid,
+                                           uint32_t nblk, const WStack &stk) {
+    const uint32_t s = bid & (PG_QSHARDS - 1);
     const uint32_t n = q.counts[s];
     const uint32_t *items = q.items + (size_t)s * q.stride;
-    for (uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += gridDim.x / PG_QSHARDS * TRACE_BLOCK) {
+    for (uint32_t i = (bid / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += nblk / PG_QSHARDS * TRACE_BLOCK) {
         uint32_t slot = items[i];
         float4 o = ldS(&p.sh_o[slot]), d = ldS(&p.sh_d[slot]);
         float tmax = d.w;
@@ -191,6 +198,25 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
             }
         }
     }
+}
+
+__global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, Queue q) {
+    __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];
+    shadowRows(sc, p, q, blockIdx.x, gridDim.x, threadWideStack(stack, p.stack_ovf));
+}
+
+// a bounce's shadow rays and the next closest hits in one launch: blocks [0, shadow_blocks) run
+// k_shadow's rows, the rest k_trace's (no environment emitter: an escaped path's radiance would
+// race with the same path's NEE add).  Both parts are grid-stride loops over their shards; the
+// overflow ring holds two launches' worth of threads (2 x pg_stack_overflow_words(0)).
+__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
+                                                      Queue shq, uint32_t shadow_blocks) {
+    __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
+    if (blockIdx.x < shadow_blocks)
+        shadowRows(sc, p, shq, blockIdx.x, shadow_blocks, threadWideStack(stack, p.stack_ovf));
+    else
+        traceRows<false, false>(g, sc, p, q, cqs, nullptr, blockIdx.x - shadow_blocks, gridDim.x - shadow_blocks,
+                                threadStack(stack, p.stack_ovf), nullptr, 0);
 }
 
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
@@ -706,6 +732,19 @@ void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const Scene
     const dim3 grid = shardGrid(max_shard, SHADE_BLOCK, 0xFFFFFFFFu);
     if (sc.env) launchShade<true>(s, cls, grid, g, sc, sd, p, in, out, shq);
     else launchShade<false>(s, cls, grid, g, sc, sd, p, in, out, shq);
+}
+void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
+                    const Queue *class_queues, Queue shq, uint32_t max_shadow_shard) {
+    ClassQueues cq;
+    for (int c = 0; c <= PG_NUM_CLASSES; ++c) cq.q[c] = class_queues[c];
+    const uint32_t sb = max_shadow_shard ? shardGrid(max_shadow_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS).x : 0;
+    const uint32_t tb = max_shard ? shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS).x : 0;
+    if (sb + tb == 0) return;
+    if (tb == 0) {  // no trace rows: k_rays needs at least one trace block per shard to stay sharded
+        hipLaunchKernelGGL(k_shadow, dim3(sb), dim3(TRACE_BLOCK), 0, s, sc, p, shq);
+        return;
+    }
+    hipLaunchKernelGGL(k_rays, dim3(sb + tb), dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq, shq, sb);
 }
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard) {
     if (!max_shard) return;
