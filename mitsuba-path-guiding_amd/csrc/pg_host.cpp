@@ -1175,6 +1175,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
     const bool evt = c->cfg.kernel_timing != 0;  // per-launch HIP events (pg_stats trace/shade/shadow_ms)
     const bool fuseRays = !evt && !c->has_env && !std::getenv("PG_NO_RAYS_FUSION");
+    const bool fuseShade = !evt && !c->has_env && !std::getenv("PG_NO_SHADE_FUSION");
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
     const uint32_t pixPer = std::min(npix, want);
@@ -1362,9 +1363,14 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         EventPair es{}, ew{};
         if (evt) es = nextEvents(&l), ew = nextEvents(&l);
         if (evt) HIPC(c, hipEventRecord(es.a, l.stream));
-        for (int k = 0; k < PG_NUM_CLASSES; ++k) {
-            pg_launch_shade_class(l.stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
-            c->stats.shade_launches += clsMax[k] ? 1 : 0;
+        if (fuseShade) {  // one launch for every class present
+            pg_launch_shade_all(l.stream, g, sc, sd, pv, cls, clsMax, next, shq);
+            c->stats.shade_launches += 1;
+        } else {
+            for (int k = 0; k < PG_NUM_CLASSES; ++k) {
+                pg_launch_shade_class(l.stream, k, g, sc, sd, pv, cls[k], clsMax[k], next, shq);
+                c->stats.shade_launches += clsMax[k] ? 1 : 0;
+            }
         }
         if (evt) HIPC(c, hipEventRecord(es.b, l.stream));
         l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);

@@ -93,6 +93,10 @@ void pg_launch_trace(hipStream_t s, const GParams &g, const SceneDev &sc, const 
                      const Queue *class_queues, bool first_bounce);
 void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const SceneDev &sc, const SDDev &sd,
                            const PathDev &p, Queue in, uint32_t max_shard, Queue out, Queue shadow);
+// every material class of a bounce in one launch (k_shade_all; scenes without an environment
+// emitter): pg_launch_shade_class for each class c with max_shard[c] > 0
+void pg_launch_shade_all(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
+                         const Queue *class_queues, const uint32_t *max_shard, Queue out, Queue shq);
 // shadow rays of a bounce and the closest hits of the next in one launch (k_rays; scenes without an
 // environment emitter): the pair pg_launch_shadow + pg_launch_trace without the aov hook
 void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,

@@ -225,14 +225,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))
 // ENV compiles in environment-emitter sampling for NEE (kept out of the other instantiations: it
 // costs 4-8 VGPRs).
 template <int MODEL, bool CAN_GUIDE, bool ENV>
-__global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue in,
-                                                       Queue out, Queue shq) {
+__device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
+                                           const Queue &in, const Queue &out, const Queue &shq, uint32_t bid) {
     // one item per thread (a grid-stride loop here cost ~45 VGPRs of hoisted invariants): block b
     // takes row b / PG_QSHARDS of shard b % PG_QSHARDS; rows past the shard's count exit at once
-    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+    const uint32_t s = bid & (PG_QSHARDS - 1);
     const uint32_t n = in.counts[s];
     {
-    const uint32_t base = (blockIdx.x / PG_QSHARDS) * SHADE_BLOCK;
+    const uint32_t base = (bid / PG_QSHARDS) * SHADE_BLOCK;
     if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
     bool alive = false, shadow = false, dirtyL = false;
@@ -428,6 +428,30 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
     waveAppend(alive, slot, out.items + (size_t)s * out.stride, out.counts + s);
     waveAppend(shadow, slot, shq.items + (size_t)s * shq.stride, shq.counts + s);
     }
+}
+
+template <int MODEL, bool CAN_GUIDE, bool ENV>
+__global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue in,
+                                                       Queue out, Queue shq) {
+    shadeBlock<MODEL, CAN_GUIDE, ENV>(g, sc, sd, p, in, out, shq, blockIdx.x);
+}
+
+// every material class of a bounce in one launch (no environment emitter): blocks
+// [end[c-1], end[c]) shade class c.  All class bodies fit 128 VGPRs, so the shared register budget
+// keeps the 4 waves/SIMD each class kernel has alone.
+struct ShadeRanges {
+    uint32_t end[PG_NUM_CLASSES];
+};
+__global__ __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_all(
+    GParams g, SceneDev sc, SDDev sd, PathDev p, ClassQueues in, Queue out, Queue shq, ShadeRanges r) {
+    static_assert(PG_NUM_CLASSES == 6, "class ranges");
+    const uint32_t b = blockIdx.x;
+    if (b < r.end[0]) shadeBlock<PG_BSDF_DIFFUSE, true, false>(g, sc, sd, p, in.q[0], out, shq, b);
+    else if (b < r.end[1]) shadeBlock<PG_BSDF_ROUGHCONDUCTOR, true, false>(g, sc, sd, p, in.q[1], out, shq, b - r.end[0]);
+    else if (b < r.end[2]) shadeBlock<PG_BSDF_ROUGHDIELECTRIC, true, false>(g, sc, sd, p, in.q[2], out, shq, b - r.end[1]);
+    else if (b < r.end[3]) shadeBlock<PG_BSDF_PLASTIC, false, false>(g, sc, sd, p, in.q[3], out, shq, b - r.end[2]);
+    else if (b < r.end[4]) shadeBlock<PG_BSDF_ROUGHPLASTIC, true, false>(g, sc, sd, p, in.q[4], out, shq, b - r.end[3]);
+    else shadeBlock<-1, false, false>(g, sc, sd, p, in.q[5], out, shq, b - r.end[4]);
 }
 
 // film: box-filtered accumulation of every layer's sample into its pixel, in sample order
@@ -732,6 +756,20 @@ void pg_launch_shade_class(hipStream_t s, int cls, const GParams &g, const Scene
     const dim3 grid = shardGrid(max_shard, SHADE_BLOCK, 0xFFFFFFFFu);
     if (sc.env) launchShade<true>(s, cls, grid, g, sc, sd, p, in, out, shq);
     else launchShade<false>(s, cls, grid, g, sc, sd, p, in, out, shq);
+}
+void pg_launch_shade_all(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
+                         const Queue *class_queues, const uint32_t *max_shard, Queue out, Queue shq) {
+    ClassQueues cq;
+    ShadeRanges r;
+    uint32_t total = 0;
+    for (int c = 0; c < PG_NUM_CLASSES; ++c) {
+        cq.q[c] = class_queues[c];
+        total += max_shard[c] ? shardGrid(max_shard[c], SHADE_BLOCK, 0xFFFFFFFFu).x : 0;
+        r.end[c] = total;
+    }
+    cq.q[PG_NUM_CLASSES] = class_queues[PG_NUM_CLASSES];
+    if (!total) return;
+    hipLaunchKernelGGL(k_shade_all, dim3(total), dim3(SHADE_BLOCK), 0, s, g, sc, sd, p, cq, out, shq, r);
 }
 void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
                     const Queue *class_queues, Queue shq, uint32_t max_shadow_shard) {

@@ -220,12 +220,13 @@ def test_max_render_time(pg):
 
 def test_training_independent_of_lanes_and_runs(pg):
     """Paths are pure functions of (pixel, sample): guided kitchen training gives the same sorted
-    records, films and trees for 1 and 3 lanes in flight, and again on a fresh context (closest-hit
-    ties resolved independently of traversal order; DESIGN.md §4 Determinism)."""
+    records, films and trees for 1 and 3 lanes in flight, again on a fresh context (closest-hit
+    ties resolved independently of traversal order; DESIGN.md §4 Determinism), and with the fused
+    per-bounce launches or separate ones."""
     sc = pg.scenes.kitchen(128, 72)
 
-    def train(lanes):
-        d = make_dev(pg, sc, guiding=1, s_tree_threshold=1500.0, path_lanes=lanes)
+    def train(lanes, timing=0):
+        d = make_dev(pg, sc, guiding=1, s_tree_threshold=1500.0, path_lanes=lanes, kernel_timing=timing)
         off, out = 0, []
         for it in range(4):
             d.render_pass(2 ** it, off, True)
@@ -241,3 +242,6 @@ def test_training_independent_of_lanes_and_runs(pg):
     a = train(3)
     assert train(1) == a
     assert train(3) == a
+    # per-launch timing runs every class, shadow and trace kernel as its own launch; without it a
+    # bounce runs k_shade_all + k_rays: same paths either way
+    assert train(3, timing=1) == a
