@@ -1068,7 +1068,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
                 }
                 c->rec_bound += add;
                 pg_launch_commit(c->stream, pv, (uint32_t)items, maxV, c->records.as<pg_record>(),
-                                 c->rec_count.as<unsigned long long>(), c->rec_capacity);
+                                 c->rec_count.as<unsigned long long>(), c->rec_capacity, 0);
             }
             pg_launch_film(c->stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
                            c->film_sq.as<float4>());
@@ -1174,7 +1174,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const SDDev sd = sdView(c);
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
     const bool evt = c->cfg.kernel_timing != 0;  // per-launch HIP events (pg_stats trace/shade/shadow_ms)
-    const bool fuseRays = !evt && !c->has_env && !std::getenv("PG_NO_RAYS_FUSION");
+    const bool fuseRays = !evt && !std::getenv("PG_NO_RAYS_FUSION");
     const bool fuseShade = !evt && !c->has_env && !std::getenv("PG_NO_SHADE_FUSION");
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
@@ -1299,7 +1299,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             }
             c->rec_bound += add;
             pg_launch_commit(l.stream, pv, l.n, g.max_vertices, c->records.as<pg_record>(),
-                             c->rec_count.as<unsigned long long>(), c->rec_capacity);
+                             c->rec_count.as<unsigned long long>(), c->rec_capacity, c->has_env ? 1 : 0);
         }
         HIPC(c, hipEventRecord(c->film_order, l.stream));
         HIPC(c, hipEventRecord(l.done, l.stream));
@@ -1374,8 +1374,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         }
         if (evt) HIPC(c, hipEventRecord(es.b, l.stream));
         l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
-        // without per-launch timing (and without an environment emitter, whose escaped-path radiance
-        // would race with the same path's NEE add) the shadow rays share the next trace's launch
+        // without per-launch timing the shadow rays share the next trace's launch
         if (fuseRays) return launchTrace(l, &shq);
         if (evt) HIPC(c, hipEventRecord(ew.a, l.stream));
         pg_launch_shadow(l.stream, sc, pv, shq, l.bound);

@@ -109,8 +109,9 @@ void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const P
 // unit-level environment-emitter queries (pg_envmap_query)
 void pg_launch_envmap_query(hipStream_t s, const SceneDev &sc, int op, const float *in, uint32_t n, float *out);
 // p.pinfo == nullptr: the vertex count of slot i is bits(p.rad[i].w) (volpath items)
+// env_hits: surface path with an environment emitter (escape radiance in the hit record)
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
-                      unsigned long long *rec_count, unsigned long long rec_capacity);
+                      unsigned long long *rec_count, unsigned long long rec_capacity, int env_hits);
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n);
 // one volpath sample per (pixel, layer) item of the chunk, written to v.rad[item]
 void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,

@@ -73,17 +73,21 @@ __device__ __forceinline__ f3 bsdfAlbedo(const GMat &M) {
 
 // A path whose extension ray escaped (progressive_path.cpp:150-158 for the camera ray, :252-267 +
 // :276-284 after a bounce): the environment emitter's radiance, MIS-weighted against its NEE pdf.
-__device__ __forceinline__ void envEscape(const GParams &g, const SceneDev &sc, const PathDev &p, uint32_t slot,
-                                          f3 rd) {
+// radiance an escaped path picks up from the environment emitter.  k_trace stores it in the path's
+// hit record (t, u, v of a miss; the escape ends the path), and k_film / k_commit add it to L
+// (envHitRadiance): the sum (L + NEE of the last vertex) + environment keeps its order while the
+// last vertex's shadow ray may run in the same launch (k_rays)
+__device__ __forceinline__ f3 envEscapeRadiance(const GParams &g, const SceneDev &sc, const PathDev &p, uint32_t slot,
+                                                f3 rd) {
     const uint4 pi = p.pinfo[slot];
     const uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16;
     const float4 T4 = p.thr[slot];
     f3 add;
     if (depth == 1) {  // camera ray: the loop-top miss with EEmittedRadiance
-        if (!(flags & PF_EMITTED_QUERY) || (g.hide_emitters && !(flags & PF_SCATTERED))) return;
+        if (!(flags & PF_EMITTED_QUERY) || (g.hide_emitters && !(flags & PF_SCATTERED))) return mk1(0.f);
         add = xyz(T4) * envEval(*sc.env, rd);
     } else {
-        if (g.hide_emitters && !(flags & PF_SCATTERED)) return;
+        if (g.hide_emitters && !(flags & PF_SCATTERED)) return mk1(0.f);
         const float4 pv = p.prev[slot];
         float w = 1.0f;
         if (g.use_nee) {
@@ -92,8 +96,16 @@ __device__ __forceinline__ void envEscape(const GParams &g, const SceneDev &sc, 
         }
         add = xyz(T4) * envEval(*sc.env, rd) * w;
     }
-    const float4 L = p.rad[slot];
-    p.rad[slot] = make_float4(L.x + add.x, L.y + add.y, L.z + add.z, L.w);
+    return add;
+}
+// L of a finished path plus the environment radiance its escape left in the hit record
+__device__ __forceinline__ float4 envHitRadiance(float4 L, float4 hv) {
+    if (__float_as_uint(hv.y) == 0xFFFFFFFFu) {
+        L.x += hv.x;
+        L.y += hv.z;
+        L.z += hv.w;
+    }
+    return L;
 }
 
 
@@ -147,13 +159,16 @@ __device__ __forceinline__ void traceRows(const GParams &g, const SceneDev &sc, 
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
             bool h = traverse<false, LTOP>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk, top, ntop);
-            const float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
-            stS(&p.hit[slot], hr);
+            float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
             if (first) first[slot] = hr;
+            if (ENV && !h) {
+                const f3 e = envEscapeRadiance(g, sc, p, slot, xyz(d));
+                hr = make_float4(e.x, hr.y, e.y, e.z);
+            }
+            stS(&p.hit[slot], hr);
             cls = h ? (int)sc.tclass[tri] : PG_NUM_CLASSES;
         }
         classAppend(cls, slot, cqs, s);
-        if (ENV && cls == PG_NUM_CLASSES) envEscape(g, sc, p, slot, xyz(ldS(&p.ray_d[slot])));
     }
 }
 
@@ -206,16 +221,17 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
 }
 
 // a bounce's shadow rays and the next closest hits in one launch: blocks [0, shadow_blocks) run
-// k_shadow's rows, the rest k_trace's (no environment emitter: an escaped path's radiance would
-// race with the same path's NEE add).  Both parts are grid-stride loops over their shards; the
+// k_shadow's rows, the rest k_trace's (an escaped path's environment radiance goes to its hit
+// record, not to L, so it cannot race with the same path's NEE add).  Both parts are grid-stride loops over their shards; the
 // overflow ring holds two launches' worth of threads (2 x pg_stack_overflow_words(0)).
+template <bool ENV>
 __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                       Queue shq, uint32_t shadow_blocks) {
     __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
     if (blockIdx.x < shadow_blocks)
         shadowRows(sc, p, shq, blockIdx.x, shadow_blocks, threadWideStack(stack, p.stack_ovf));
     else
-        traceRows<false, false>(g, sc, p, q, cqs, nullptr, blockIdx.x - shadow_blocks, gridDim.x - shadow_blocks,
+        traceRows<ENV, false>(g, sc, p, q, cqs, nullptr, blockIdx.x - shadow_blocks, gridDim.x - shadow_blocks,
                                 threadStack(stack, p.stack_ovf), nullptr, 0);
 }
 
@@ -485,6 +501,7 @@ __global__ __launch_bounds__(256) void k_film(GParams g, SceneDev sc, PathDev p,
     float4 a = film[pix], q = sumsq[pix];
     for (uint32_t l = 0; l < nlayers; ++l) {
         float4 L = p.rad[(size_t)l * npix + lp];
+        if (sc.env && p.hit) L = envHitRadiance(L, p.hit[(size_t)l * npix + lp]);  // surface path (volpath: no hit)
         float m = fmaxf(L.x, fmaxf(L.y, L.z));
         if (m > g.max_component_value) {
             float s = g.max_component_value / m;
@@ -507,9 +524,10 @@ __global__ __launch_bounds__(256) void k_film(GParams g, SceneDev sc, PathDev p,
 }
 
 // training records of finished paths: radiance along wo_i = (L_final - L_i) / T_i (channel-wise)
+// env_hits: the surface path of a scene with an environment emitter (envHitRadiance)
 __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int maxV, pg_record *__restrict__ recs,
                                                 unsigned long long *__restrict__ rec_count,
-                                                unsigned long long capacity) {
+                                                unsigned long long capacity, int env_hits) {
     uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t nv = 0;
     if (slot < nslots) nv = min(p.pinfo ? p.pinfo[slot].w : __float_as_uint(p.rad[slot].w), (uint32_t)maxV);
@@ -527,6 +545,7 @@ __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int 
     if (nv == 0) return;
     unsigned long long o = base + (incl - nv);
     float4 L = p.rad[slot];
+    if (env_hits) L = envHitRadiance(L, p.hit[slot]);
     for (uint32_t k = 0; k < nv; ++k, ++o) {
         if (o >= capacity) return;
         const float4 *vb = p.vtx + ((size_t)k * p.vtxP + slot) * 3;
@@ -782,7 +801,8 @@ void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const P
         hipLaunchKernelGGL(k_shadow, dim3(sb), dim3(TRACE_BLOCK), 0, s, sc, p, shq);
         return;
     }
-    hipLaunchKernelGGL(k_rays, dim3(sb + tb), dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq, shq, sb);
+    if (sc.env) hipLaunchKernelGGL(k_rays<true>, dim3(sb + tb), dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq, shq, sb);
+    else hipLaunchKernelGGL(k_rays<false>, dim3(sb + tb), dim3(TRACE_BLOCK), 0, s, g, sc, p, q, cq, shq, sb);
 }
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard) {
     if (!max_shard) return;
@@ -830,10 +850,10 @@ void pg_launch_envmap_query(hipStream_t s, const SceneDev &sc, int op, const flo
     hipLaunchKernelGGL(k_envmap_query, dim3(blocks(n, 256)), dim3(256), 0, s, sc, op, in, n, out);
 }
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
-                      unsigned long long *rec_count, unsigned long long rec_capacity) {
+                      unsigned long long *rec_count, unsigned long long rec_capacity, int env_hits) {
     if (!nslots) return;
     hipLaunchKernelGGL(k_commit, dim3(blocks(nslots, 256)), dim3(256), 0, s, p, nslots, max_vertices, records, rec_count,
-                       rec_capacity);
+                       rec_capacity, env_hits);
 }
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n) {
     if (!n) return;

@@ -665,4 +665,4 @@ def smoke(width=1024, height=1024, res=256, seed=7, scale=40.0, albedo=0.9, g=0.
     return s.finalize()
 
 
-SCENES = {"cornell": cornell, "ajar_door": ajar_door, "kitchen": kitchen, "smoke": smoke}
+SCENES = {"cornell": cornell, "ajar_door": ajar_door, "kitchen": kitchen, "smoke": smoke, "sky_courtyard": sky_courtyard}
