@@ -6,11 +6,16 @@
 
 using namespace pgd;
 
-#define TRACE_BLOCK 128
+// block sizes (C3, profiles/r02zj_block_ab: shading 128 / traversal 256 beat 256 / 128 by 1.7 %)
+#ifndef TRACE_BLOCK
+#define TRACE_BLOCK 256
+#endif
 #define STACK_DEPTH 48  // total traversal stack entries (the BVH builder bounds the depth below this)
-#define LDS_STACK 16    // binary BVH: top entries in LDS (4 B each: 8 KiB per block), deeper ones spill
-#define WIDE_LDS_STACK 8  // wide BVH: top group entries in LDS (8 B each: 8 KiB per block)
-#define SHADE_BLOCK 256
+#define LDS_STACK 16    // binary BVH: top entries in LDS (4 B each: 16 KiB per block), deeper ones spill
+#define WIDE_LDS_STACK 8  // wide BVH: top group entries in LDS (8 B each: 16 KiB per block)
+#ifndef SHADE_BLOCK
+#define SHADE_BLOCK 128
+#endif
 // persistent grid-stride launches: enough blocks to fill 256 CUs at full occupancy
 #define TRACE_MAX_BLOCKS (256 * 16)
 
