@@ -224,6 +224,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
 // k_shadow's rows, the rest k_trace's (an escaped path's environment radiance goes to its hit
 // record, not to L, so it cannot race with the same path's NEE add).  Both parts are grid-stride loops over their shards; the
 // overflow ring holds two launches' worth of threads (2 x pg_stack_overflow_words(0)).
+static_assert(2 * WIDE_LDS_STACK >= LDS_STACK, "k_rays / k_trace_rays share one LDS stack array");
 template <bool ENV>
 __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                       Queue shq, uint32_t shadow_blocks) {

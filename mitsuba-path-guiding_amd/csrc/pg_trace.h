@@ -11,13 +11,19 @@ using namespace pgd;
 #define TRACE_BLOCK 256
 #endif
 #define STACK_DEPTH 48  // total traversal stack entries (the BVH builder bounds the depth below this)
+#ifndef LDS_STACK
 #define LDS_STACK 16    // binary BVH: top entries in LDS (4 B each: 16 KiB per block), deeper ones spill
+#endif
+#ifndef WIDE_LDS_STACK
 #define WIDE_LDS_STACK 8  // wide BVH: top group entries in LDS (8 B each: 16 KiB per block)
+#endif
 #ifndef SHADE_BLOCK
 #define SHADE_BLOCK 128
 #endif
 // persistent grid-stride launches: enough blocks to fill 256 CUs at full occupancy
+#ifndef TRACE_MAX_BLOCKS
 #define TRACE_MAX_BLOCKS (256 * 16)
+#endif
 
 namespace {
 
