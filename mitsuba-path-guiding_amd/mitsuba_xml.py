@@ -16,7 +16,8 @@ adapter's flatten() produces from Scene::getShapes()/getBSDFs() (INTEGRATION.md)
   bsdf              diffuse, conductor, roughconductor (material Cu / Al / Au / none, or eta + k),
                     dielectric, roughdielectric, plastic, roughplastic (intIOR / extIOR by value or
                     by name: src/bsdfs/ior.h), twosided, null; distribution beckmann / ggx
-  shape             obj, ply (ascii / binary), rectangle, cube, disk and sphere (tessellated), with
+  shape             obj, ply (ascii / binary), serialized (Mitsuba's zlib mesh format, any shapeIndex),
+                    rectangle, cube, disk and sphere (tessellated), with
                     toWorld, flipNormals, faceNormals, a nested or referenced bsdf and an area emitter
   emitter           area (in a shape), envmap (.npy / .pfm / uncompressed or zlib EXR), constant
                     (as a uniform envmap)
@@ -298,6 +299,11 @@ class _Loader:
             r = float(P.get("radius", 1.0))
             V, F, N = scenes.uv_sphere(c, r, *self.sphere_res)
             V, N = V.astype(np.float64), N.astype(np.float64)
+        elif typ == "serialized":  # src/shapes/serialized.cpp:148-210
+            if "maxSmoothAngle" in P:
+                self.unsupported("shape", typ, "maxSmoothAngle (TriMesh::rebuildTopology) is not restated; "
+                                 "the file's normals or smooth vertex normals are used")
+            V, F, N = read_serialized(self.path(P["filename"]), int(P.get("shapeIndex", 0)))
         else:
             return None
         V, F = np.asarray(V, np.float64), np.asarray(F, np.int64)
@@ -312,6 +318,8 @@ class _Loader:
         flip = P.get("flipNormals", False)
         if np.linalg.det(M[:3, :3]) < 0 and typ in ("rectangle", "cube", "disk", "sphere"):
             F = F[:, ::-1]
+        elif np.linalg.det(M[:3, :3]) < 0 and typ == "serialized":
+            F = F[:, [1, 0, 2]]  # serialized.cpp:197-202 swaps idx[0] and idx[1]
         if face:
             if flip:
                 F = F[:, ::-1]
@@ -323,7 +331,7 @@ class _Loader:
     def shape(self, el):
         typ = self.attr(el, "type")
         P = self.props(el)
-        if typ in ("shapegroup", "instance", "hair", "heightfield", "serialized", "cylinder"):
+        if typ in ("shapegroup", "instance", "hair", "heightfield", "cylinder"):
             return self.unsupported("shape", typ, "not flattened by this loader")
         res = self.mesh(el, typ, P)
         if res is None:
@@ -511,6 +519,90 @@ def _read_obj(path):
     V = np.array([P[k[0]] for k, _ in order], np.float64)
     N = np.array([Nn[k[1]] if k[1] >= 0 else [0, 0, 0] for k, _ in order], np.float64) if has_n else None
     return V, np.array(faces, np.int64), N
+
+
+# TriMesh serialization flags (trimesh.cpp:89-97) and file header (trimesh.cpp:34-36)
+_SER_HEADER, _SER_V3, _SER_V4 = 0x041C, 0x0003, 0x0004
+_SER_NORMALS, _SER_TEXCOORDS, _SER_COLORS, _SER_FACE_NORMALS = 0x0001, 0x0002, 0x0008, 0x0010
+_SER_SINGLE, _SER_DOUBLE = 0x1000, 0x2000
+
+
+def read_serialized(path, index=0):
+    """Mesh `index` of a Mitsuba .serialized file (TriMesh::loadCompressed / readHeader / readOffset,
+    trimesh.cpp:175-294): a little-endian (u16 0x041C, u16 version) header, then a zlib stream of
+    u32 flags, [v4: NUL-terminated name], u64 vertex and triangle counts, positions, [normals],
+    [texcoords], [colors] (f32 or f64 by flag) and u32 triangle indices.  Files with several meshes
+    end with a dictionary of per-mesh byte offsets (u64 in v4, u32 in v3) and a u32 mesh count.
+    Returns (V, F, N or None) as float64 / int64 arrays."""
+    with open(path, "rb") as f:
+        data = f.read()
+
+    def header(off):
+        fmt, ver = struct.unpack_from("<HH", data, off)
+        if fmt == 0x1C04:
+            raise ValueError(f"{path}: geometry file of an old Mitsuba version (re-import it)")
+        if fmt != _SER_HEADER or ver not in (_SER_V3, _SER_V4):
+            raise ValueError(f"{path}: not a serialized mesh (header {fmt:#06x}, version {ver})")
+        return ver
+
+    version = header(0)
+    off = 0
+    if index != 0:
+        count = struct.unpack_from("<I", data, len(data) - 4)[0]
+        if index < 0 or index >= count:
+            raise ValueError(f"{path}: shape index {index} out of range 0..{count - 1}")
+        if version == _SER_V4:
+            off = struct.unpack_from("<Q", data, len(data) - 8 * (count - index) - 4)[0]
+        else:
+            off = struct.unpack_from("<I", data, len(data) - 4 * (count - index + 1))[0]
+        version = header(off)
+    z = zlib.decompressobj()
+    raw = z.decompress(data[off + 4:])
+    pos = 0
+    flags = struct.unpack_from("<I", raw, pos)[0]
+    pos += 4
+    if version == _SER_V4:
+        pos = raw.index(b"\0", pos) + 1
+    nv, nt = struct.unpack_from("<QQ", raw, pos)
+    pos += 16
+    ft = np.dtype("<f8") if flags & _SER_DOUBLE else np.dtype("<f4")
+
+    def take(dt, n):
+        nonlocal pos
+        a = np.frombuffer(raw, dt, n, pos)
+        pos += dt.itemsize * n
+        return a
+
+    V = take(ft, 3 * nv).reshape(nv, 3).astype(np.float64)
+    N = take(ft, 3 * nv).reshape(nv, 3).astype(np.float64) if flags & _SER_NORMALS else None
+    if flags & _SER_TEXCOORDS:
+        take(ft, 2 * nv)
+    if flags & _SER_COLORS:
+        take(ft, 3 * nv)
+    F = take(np.dtype("<u4"), 3 * nt).reshape(nt, 3).astype(np.int64)
+    if nv and (F.min() < 0 or F.max() >= nv):
+        raise ValueError(f"{path}: triangle index out of range")
+    return V, F, N
+
+
+def write_serialized(path, meshes):
+    """Write meshes [(V, F, N or None[, name])] as a version-4 .serialized file, float32, the layout of
+    TriMesh::serialize (trimesh.cpp:1131-1176) plus the offset dictionary of a multi-mesh file."""
+    out, offsets = bytearray(), []
+    for m in meshes:
+        V, F, N = m[0], m[1], m[2]
+        name = m[3] if len(m) > 3 else ""
+        flags = _SER_SINGLE | (_SER_NORMALS if N is not None else 0)
+        body = struct.pack("<I", flags) + name.encode() + b"\0" + struct.pack("<QQ", len(V), len(F))
+        body += np.asarray(V, "<f4").tobytes()
+        if N is not None:
+            body += np.asarray(N, "<f4").tobytes()
+        body += np.asarray(F, "<u4").tobytes()
+        offsets.append(len(out))
+        out += struct.pack("<HH", _SER_HEADER, _SER_V4) + zlib.compress(body)
+    out += np.asarray(offsets, "<u8").tobytes() + struct.pack("<I", len(meshes))
+    with open(path, "wb") as f:
+        f.write(bytes(out))
 
 
 _PLY_TYPES = {"char": "i1", "int8": "i1", "uchar": "u1", "uint8": "u1", "short": "i2", "int16": "i2",

@@ -163,3 +163,60 @@ def test_ply_and_obj_readers(pg, tmp_path):
     assert np.array_equal(Vo, V) and Fo.tolist() == [[0, 1, 2], [0, 2, 3]] and No is None
     N = X._vertex_normals(Vo, Fo)
     assert np.allclose(N, [0, 0, 1])
+
+
+def _ser_mesh_v3(V, F, N=None, double=True):
+    """One mesh in the version-3 .serialized layout, packed by hand (trimesh.cpp:175-252: header,
+    then a zlib stream of flags, counts, positions, [normals], indices; no name in v3)."""
+    import struct
+    import zlib
+    flags = (0x2000 if double else 0x1000) | (0x0001 if N is not None else 0)
+    ft = "<f8" if double else "<f4"
+    body = struct.pack("<IQQ", flags, len(V), len(F)) + np.asarray(V, ft).tobytes()
+    if N is not None:
+        body += np.asarray(N, ft).tobytes()
+    body += np.asarray(F, "<u4").tobytes()
+    return struct.pack("<HH", 0x041C, 0x0003) + zlib.compress(body)
+
+
+def test_serialized_reader(pg, tmp_path):
+    """TriMesh::loadCompressed (trimesh.cpp:175-294): v3 multi-mesh file with a u32 offset
+    dictionary, f64 positions, normals; v4 round trip through write_serialized; shapeIndex and the
+    det < 0 index swap of serialized.cpp:197-202 through the XML loader."""
+    import struct
+    X = pg.mitsuba_xml
+    V0 = np.array([[0, 0, 0], [1, 0, 0], [0, 1, 0]], np.float64)
+    V1 = np.array([[0, 0, 1], [2, 0, 1], [2, 2, 1], [0, 2, 1]], np.float64)
+    F1 = np.array([[0, 1, 2], [0, 2, 3]])
+    N1 = np.tile([0.0, 0.0, 1.0], (4, 1))
+    m0 = _ser_mesh_v3(V0, [[0, 1, 2]])
+    m1 = _ser_mesh_v3(V1, F1, N1)
+    blob = m0 + m1 + struct.pack("<III", 0, len(m0), 2)
+    path = tmp_path / "two.serialized"
+    path.write_bytes(blob)
+    V, F, N = X.read_serialized(str(path), 0)
+    assert np.array_equal(V, V0) and F.tolist() == [[0, 1, 2]] and N is None
+    V, F, N = X.read_serialized(str(path), 1)
+    assert np.array_equal(V, V1) and np.array_equal(F, F1) and np.array_equal(N, N1)
+    with pytest.raises(ValueError):
+        X.read_serialized(str(path), 2)
+    bad = tmp_path / "bad.serialized"
+    bad.write_bytes(struct.pack("<HH", 0x1C04, 3) + b"\0" * 16)
+    with pytest.raises(ValueError):
+        X.read_serialized(str(bad))
+    # v4 (names, f32) round trip
+    p4 = tmp_path / "four.serialized"
+    X.write_serialized(str(p4), [(V0, [[0, 1, 2]], None, "tri"), (V1, F1, N1, "quad")])
+    V, F, N = X.read_serialized(str(p4), 1)
+    assert np.array_equal(V, V1) and np.array_equal(F, F1) and np.array_equal(N, N1)
+    # through the loader: shapeIndex 1, mirrored toWorld -> idx[0] <-> idx[1], normals (0, 0, 1) kept
+    # (the mirror is along x, so the inverse-transpose leaves z normals unchanged)
+    xml = ('<scene version="0.5.0"><shape type="serialized"><string name="filename" value="two.serialized"/>'
+           '<integer name="shapeIndex" value="1"/><transform name="toWorld"><scale x="-1"/></transform></shape>'
+           '</scene>')
+    (tmp_path / "s.xml").write_text(xml)
+    sc = X.load(str(tmp_path / "s.xml")).scene
+    assert len(sc.shapes) == 1 and sc.shapes[0].tri_count == 2
+    assert np.array_equal(sc._pos[0].astype(np.float64), V1 * [-1, 1, 1])
+    assert sc._idx[0].tolist() == [[1, 0, 2], [2, 0, 3]]
+    assert np.allclose(sc._nrm[0], N1)
