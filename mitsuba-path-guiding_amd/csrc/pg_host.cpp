@@ -1112,7 +1112,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const bool rec = record && c->cfg.guiding;
     // 2^25 paths per chunk by default: bigger chunks mean fewer sparse tail bounces (each costs a
     // class-count readback) per path.  C3 with 3 lanes: 2^22 491, 2^23 552, 2^24 569, 2^25 587
-    // Mpaths/s (DESIGN.md "Lanes"); the lanes then hold ~58 GB each, mostly training vertices.
+    // Mpaths/s (DESIGN.md "Lanes"); 2^26 / 2^27 measured within noise of 2^25 (profiles/r02zq_chunk_ab).
+    // A non-recording lane then holds ~6.6 GB; recording lanes add 32 training vertices per path.
     uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
     if (!c->cfg.max_paths_in_flight) {
         // ... but at most 70 % of the device memory this context can use for path state (free memory
