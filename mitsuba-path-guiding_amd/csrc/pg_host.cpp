@@ -103,6 +103,9 @@ struct EventPair {
 // interleaves pg_config.path_lanes lanes, so while the host waits for one lane's per-bounce class counts the
 // GPU runs the other lane's kernels (and a lane's sparse late bounces overlap the other's).
 #define PG_MAX_LANES 4
+#ifndef PG_PIXEL_BLOCK
+#define PG_PIXEL_BLOCK 8  // local pixel order inside a tile: 8x8 blocks (0: row-major)
+#endif
 #define PG_DEFAULT_LANES 3
 struct Lane {
     hipStream_t stream = nullptr;
@@ -913,8 +916,14 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     for (uint32_t t = 0; t < tx * ty; ++t) {
         if ((int32_t)(t % (uint32_t)c->cfg.world_size) != c->cfg.rank) continue;
         uint32_t x0 = (t % tx) * T, y0 = (t / tx) * T;
-        for (uint32_t y = y0; y < std::min(y0 + T, cam.height); ++y)
-            for (uint32_t x = x0; x < std::min(x0 + T, cam.width); ++x) c->local_pixels.push_back(y * cam.width + x);
+        const uint32_t x1 = std::min(x0 + T, cam.width), y1 = std::min(y0 + T, cam.height);
+        // within a tile, PG_PIXEL_BLOCK^2 pixel blocks (one wave of camera rays per 8x8 block) in
+        // row-major block order; 0 = plain row-major.  Per-pixel results do not depend on the order.
+        const uint32_t B = PG_PIXEL_BLOCK > 0 ? PG_PIXEL_BLOCK : T;
+        for (uint32_t by = y0; by < y1; by += B)
+            for (uint32_t bx = x0; bx < x1; bx += B)
+                for (uint32_t y = by; y < std::min(by + B, y1); ++y)
+                    for (uint32_t x = bx; x < std::min(bx + B, x1); ++x) c->local_pixels.push_back(y * cam.width + x);
     }
     if ((s = upload(c, c->d_local_pixels, c->local_pixels))) return s;
     size_t fb = (size_t)cam.width * cam.height * 16;
