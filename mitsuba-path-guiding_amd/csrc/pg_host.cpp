@@ -103,6 +103,9 @@ struct EventPair {
 // interleaves pg_config.path_lanes lanes, so while the host waits for one lane's per-bounce class counts the
 // GPU runs the other lane's kernels (and a lane's sparse late bounces overlap the other's).
 #define PG_MAX_LANES 4
+#ifndef PG_SMALL_PASS
+#define PG_SMALL_PASS (1u << 21)  // paths: passes up to this size run as one chunk (0: always one per lane)
+#endif
 #ifndef PG_PIXEL_BLOCK
 #define PG_PIXEL_BLOCK 8  // local pixel order inside a tile: 8x8 blocks (0: row-major)
 #endif
@@ -1151,6 +1154,10 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         // into one chunk per lane
         uint64_t chunks = std::max<uint64_t>(1, (total + cap - 1) / cap);
         chunks = (chunks + c->nlanes - 1) / c->nlanes * c->nlanes;
+        // a small pass (early training iterations, a rank's shard of them) runs as ONE chunk: three
+        // lanes would each pay the whole bounce tail of launches and count readbacks for a third of
+        // the paths.  Per-pixel sums keep their layer order either way.
+        if (total <= (uint64_t)PG_SMALL_PASS) chunks = 1;
         if ((uint64_t)npix * chunks <= total) {  // whole sample layers per chunk
             const uint64_t layers = (spp + chunks - 1) / chunks;
             want = (uint32_t)std::min<uint64_t>(layers * npix, cap);
