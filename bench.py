@@ -53,7 +53,9 @@ GT_C3 = os.path.join(ROOT, "tests", "golden", "c3_gt.npz")
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU).  Without a torchrun environment and N > 1, bench.py launches N "
+                         "ranks itself (torch.distributed.run, 127.0.0.1); under torchrun N must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--scene", default="ajar_door")
@@ -65,17 +67,67 @@ def parse():
     ap.add_argument("--no-quality", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3)")
     ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = auto: 2^25)")
-    ap.add_argument("--exchange", default="allreduce", choices=["allreduce", "allgather", "capi"],
-                    help="postprogression exchange: torch.distributed all-reduce of the tree statistics (default), "
-                         "record all-gather, or the library's own RCCL communicator (pg_comm_*, the C++ adapter's path)")
+    ap.add_argument("--exchange", default=None, choices=["allreduce", "allgather", "capi", "capi-allgather"],
+                    help="postprogression exchange (N > 1): the library's own RCCL communicator (pg_comm_*, the C++ "
+                         "adapter's path): all-reduce of the tree statistics ('capi', default with RCCL) or all-gather "
+                         "of the records ('capi-allgather'); or torch.distributed: 'allreduce' (default with "
+                         "PG_DIST_BACKEND=gloo, whose ranks may share a GPU, which RCCL refuses) or 'allgather'")
+    ap.add_argument("--plumbing-check", action="store_true",
+                    help="launcher self-test: every rank joins the process group and reports (rank, world); no GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU budget of the final-render sample")
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
     ap.add_argument("--props", default="{}", help="extra integrator properties (JSON), for A/B runs")
     return ap.parse_args()
 
 
+def launch_ranks(n, argv):
+    """Start n ranks of this script through torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) and return their exit status.  Runs in a parent that has not touched the GPU (no torch
+    or library import yet): the ranks are child processes, never an exec of this one."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free port for the rendezvous
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    return subprocess.call(cmd, env=env)
+
+
+def plumbing_check(a, rank, world):
+    """--plumbing-check: the launcher's rank / world wiring without a GPU (gloo process group)."""
+    from mitsuba_path_guiding_amd import distributed as D
+    import torch
+    import torch.distributed as dist
+    D.init("gloo")
+    assert dist.get_world_size() == world == a.gpus, (dist.get_world_size(), world, a.gpus)
+    got = [None] * world
+    dist.all_gather_object(got, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", -1)),
+                                 "world": dist.get_world_size(), "pid": os.getpid()})
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"plumbing_check": True, "n_gpus": world, "ranks": got,
+                          "rank_sum": float(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    rank, world, _ = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("WORLD_SIZE", 1), ("LOCAL_RANK", 0)))
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        # the driver's `bench.py --gpus N` without torchrun: launch the N ranks here (before any GPU use)
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    if a.gpus is None:
+        a.gpus = world
+    if a.gpus != world:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)")
+    if a.plumbing_check:
+        import pgload
+        pgload.load()
+        return plumbing_check(a, rank, world)
     vol = a.scene == "smoke"  # C5: guided volumetric path tracer on the smoke cloud
     if a.width is None:
         a.width = 1024 if vol else 1280
@@ -93,17 +145,26 @@ def main():
     # RCCL ("nccl") over xGMI; PG_DIST_BACKEND=gloo rehearses the multi-rank path with ranks
     # sharing the visible GPUs (collectives through host memory)
     backend = os.environ.get("PG_DIST_BACKEND", "nccl")
+    import torch
+    if world > 1 and backend == "nccl" and torch.cuda.device_count() < world:
+        sys.exit(f"bench.py: {world} ranks need {world} visible GPUs, found {torch.cuda.device_count()} "
+                 "(PG_DIST_BACKEND=gloo rehearses ranks that share a GPU)")
     if world > 1:
         D.init(backend)
-    import torch
+        assert torch.distributed.get_world_size() == world == a.gpus
 
     on_dev = torch.cuda.is_available() and backend == "nccl"
     device = local % max(1, torch.cuda.device_count())
     scene = pg.scenes.SCENES[a.scene](a.width, a.height)
-    # postprogression exchange: all-reduce of the SD-tree building statistics
-    capi_comm = world > 1 and a.exchange == "capi"
+    # postprogression exchange (N > 1): by default the library's own RCCL communicator (pg_comm_*, what
+    # the C++ adapter runs): all-reduce of the SD-tree building statistics.  RCCL
+    # refuses two ranks on one device, so gloo rehearsals use the torch.distributed exchange.
+    if a.exchange is None:
+        a.exchange = "capi" if backend == "nccl" else "allreduce"
+    capi_comm = world > 1 and a.exchange.startswith("capi")
     if world > 1:
-        exchange = D.make_capi_exchange() if capi_comm else D.make_exchange(on_dev, mode=a.exchange)
+        exchange = (D.make_capi_exchange(mode="allgather" if a.exchange == "capi-allgather" else "allreduce")
+                    if capi_comm else D.make_exchange(on_dev, mode=a.exchange))
     else:
         exchange = None
     # one progression for the final render (the device chunks it into 2^25-path chunks, 3 in flight)
@@ -152,7 +213,7 @@ def main():
     # ---- §8d pipeline figure over the timed wall clock
     d = {k: s1[k] - s0[k] for k in s1}
     if world > 1:
-        for k in ("segments", "density_lookups"):
+        for k in ("segments", "escaped", "records", "shadow_rays", "density_lookups"):
             d[k] = int(D.sum_over_ranks(d[k], on_dev))
     if vol:
         pipe_bytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
@@ -162,11 +223,17 @@ def main():
                     "note": "density-grid gathers of k_volpath over the timed wall clock, all ranks"}
         roofline = volume_roofline(d)
     else:
-        pipe_bytes = d["segments"] * BYTES_SEGMENT
+        # §8d's 420 B per segment, split by what each segment does: every segment is traced, escaped
+        # ones are not shaded, only recording passes write training records, and only NEE vertices
+        # send a shadow ray
+        pipe_bytes = (d["segments"] * BYTES_TRACE_PER_RAY + (d["segments"] - d["escaped"]) * BYTES_SHADE_PER_VERTEX
+                      + d["records"] * BYTES_SHADE_RECORD + d["shadow_rays"] * BYTES_SHADOW_PER_RAY)
         pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
                     "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
-                    "bytes_per_segment": BYTES_SEGMENT, "segments_per_step": int(d["segments"] / a.steps),
-                    "note": "SURVEY.md §8d: segments/s x 420 B over the timed wall clock, all ranks"}
+                    "bytes_per_segment_nominal": BYTES_SEGMENT, "segments_per_step": int(d["segments"] / a.steps),
+                    "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
+                    "note": "SURVEY.md §8d over the timed wall clock, all ranks: segments x 48 B (trace) + shaded "
+                            "segments x 300 B + training records x 40 B + shadow rays x 32 B"}
         roofline = kernel_roofline(pg, scene, integ, device, a)
 
     quality = None
@@ -205,10 +272,14 @@ def main():
 
 
 def kernel_roofline(pg, scene, integ, local, a, spp=32):
-    """Roofline of the dominant kernel.  The timed job runs three path lanes concurrently, so a HIP
-    event pair around one launch also covers the other lanes' kernels; per-kernel durations are
-    therefore measured on a one-lane context (same scene, same trained SD-tree, guided final-render
-    passes without records, launches serialized on one stream) right after the timed region."""
+    """Roofline of the dominant kernel of the kernels the render ships: k_shade_all (every material
+    class of a bounce in one launch), k_rays (a bounce's shadow rays + the next bounce's closest hits
+    in one launch) and k_trace (the camera rays' closest hits).  The timed job runs three path lanes
+    concurrently, so a HIP event pair around one launch would also cover the other lanes' kernels;
+    the durations therefore come from a one-lane context (same scene, same trained SD-tree, a guided
+    final-render pass without records, the same fused launches serialized on its one stream, each
+    bracketed by a HIP event pair on that stream) right after the timed region.  rocprofv3 sees the
+    same launches on that stream (tools/pmc_summary.py "calibration")."""
     from mitsuba_path_guiding_amd.integrator import Device
     cfg = pg.capi.default_config(guiding=1, device=local, path_lanes=1, kernel_timing=1, rank=integ.dev.cfg.rank,
                                  world_size=integ.dev.cfg.world_size,
@@ -224,37 +295,53 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
     s1 = dev.stats()
     d = {k: s1[k] - s0[k] for k in s1}
     shaded = d["segments"] - d["escaped"]
-    kernels = {  # name: (total ms, algorithmic bytes, launches); record=False: no training-record bytes
-        "k_trace": (d["trace_ms"], d["segments"] * BYTES_TRACE_PER_RAY, d["trace_launches"]),
-        "k_shade": (d["shade_ms"], shaded * BYTES_SHADE_PER_VERTEX, d["shade_launches"]),
-        "k_shadow": (d["shadow_ms"], d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["trace_launches"]),
+    shade_name = "k_shade" if scene.envmap is not None else "k_shade_all"  # env scenes shade per class
+    kernels = {  # name: (total ms, algorithmic bytes, launches); no records: no training-record bytes
+        "k_trace": (d["trace_ms"], d["paths"] * BYTES_TRACE_PER_RAY, d["trace_launches"]),
+        shade_name: (d["shade_ms"], shaded * BYTES_SHADE_PER_VERTEX, d["shade_launches"]),
+        "k_rays": (d["rays_ms"], (d["segments"] - d["paths"]) * BYTES_TRACE_PER_RAY
+                   + d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["rays_launches"]),
     }
     dev.close()
     dom = max(kernels, key=lambda k: kernels[k][0])
     ms, nbytes, launches = kernels[dom]
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic, source = None, None
+    per_launch = nbytes / max(launches, 1)
+    traffic, source, measured = None, None, {}
     pmc = os.path.join(ROOT, "profiles", "pmc_latest.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
-            traffic = pj.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            measured = pj.get("kernels", {})
+            traffic = measured.get(dom, {}).get("hbm_bytes_per_launch")
             source = {"file": "profiles/pmc_latest.json", "profiled": pj.get("source"),
                       "revision": pj.get("revision")}
         except (OSError, ValueError):
             traffic = None
+    out = {}
+    for k, v in kernels.items():
+        e = {"ms": round(v[0], 2), "launches": int(v[2]),
+             "algorithmic_bytes_per_launch": int(v[1] / max(v[2], 1)),
+             "avg_launch_ms": round(v[0] / max(v[2], 1), 4),
+             "achieved_gbs": round(v[1] / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else 0.0}
+        t = measured.get(k, {}).get("hbm_bytes_per_launch")
+        if t and v[2]:
+            e["traffic_bytes_per_launch"] = t
+            e["traffic_over_algorithmic"] = round(t / (v[1] / v[2]), 3)
+        out[k] = e
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
-            "kernel": dom, "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
+            "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
+            "kernel": dom, "algorithmic_bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(ms / max(launches, 1), 4),
-            "bytes_model": {"k_trace": f"{BYTES_TRACE_PER_RAY} B/ray", "k_shade": f"{BYTES_SHADE_PER_VERTEX} B/vertex "
-                            f"(+{BYTES_SHADE_RECORD} B when recording)", "k_shadow": f"{BYTES_SHADOW_PER_RAY} B/ray",
+            "bytes_model": {"k_trace": f"{BYTES_TRACE_PER_RAY} B/camera ray",
+                            shade_name: f"{BYTES_SHADE_PER_VERTEX} B/shaded vertex (+{BYTES_SHADE_RECORD} B when "
+                                        "recording)",
+                            "k_rays": f"{BYTES_TRACE_PER_RAY} B/bounce ray + {BYTES_SHADOW_PER_RAY} B/shadow ray",
                             "sum": f"{BYTES_SEGMENT} B/segment (SURVEY.md §8d)"},
             "measured": f"1-lane context, guided {scene.width}x{scene.height} x {spp} spp with the trained tree, "
-                        f"no records",
-            "kernels": {k: {"ms": round(v[0], 2), "launches": int(v[2]),
-                            "achieved_gbs": round(v[1] / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else 0.0}
-                        for k, v in kernels.items()}}
+                        f"no records; the fused launches the timed job runs, HIP events on the lane's stream",
+            "kernels": out}
 
 
 def volume_roofline(d):
@@ -342,6 +429,34 @@ def quality_block(pg, scene, final, job_s, a):
     return out
 
 
+def cpu_share():
+    """Host threads the CPU baseline may use, and where that number comes from: the smallest of the
+    scheduler affinity, the cgroup CPU quota (cgroup v2 cpu.max, v1 cfs_quota/period) and the job's
+    declared thread budget (OMP_NUM_THREADS, which gpurun sets to the box's CPU share)."""
+    import math
+    limits = {}
+    if hasattr(os, "sched_getaffinity"):
+        limits["affinity"] = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else (float(q), float(p))
+        limits["cgroup_cpu.max"] = "max" if quota is None else math.ceil(quota[0] / quota[1])
+    except (OSError, ValueError):
+        try:
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            limits["cgroup_cfs_quota"] = "max" if q <= 0 else math.ceil(q / p)
+        except (OSError, ValueError):
+            pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        limits["OMP_NUM_THREADS"] = int(os.environ["OMP_NUM_THREADS"])
+    nums = {k: v for k, v in limits.items() if isinstance(v, int) and v > 0}
+    src = min(nums, key=nums.get) if nums else "os.cpu_count"
+    cores = max(1, nums[src] if nums else (os.cpu_count() or 1))
+    return cores, {"used": src, **{k: v for k, v in limits.items()}}
+
+
 def cpu_baseline(pg, scene, integ, final, a):
     """The oracle (CPU restatement, up to 16 host threads = the GPU box's CPU share) runs the same
     guided job on a bounded sample: the full training (every pixel, 1..16 spp, its own records,
@@ -351,8 +466,7 @@ def cpu_baseline(pg, scene, integ, final, a):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py as O  # checker / CPU baseline only
     host_cpus = os.cpu_count()
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host_cpus
-    cores = max(1, min(cores, 16))  # gpurun: size pools to the box's CPU share of 16
+    cores, cores_source = cpu_share()
     vol = a.scene == "smoke"
     osc = O.OracleScene(pg.capi, scene)
     cfg = integ.cfg  # same integrator parameters as the GPU job
@@ -385,7 +499,7 @@ def cpu_baseline(pg, scene, integ, final, a):
     t_render = time.perf_counter() - t
     paths += int(st[0])
     cpu = {"value": round(paths / (t_train + t_render) / 1e6, 4), "unit": "Mpaths/s", "cores": cores,
-           "host_cpus": host_cpus, "kind": "port",
+           "cores_source": cores_source, "host_cpus": host_cpus, "kind": "port",
            "sample": f"the guided {'C5' if vol else 'C3'} job on the CPU oracle: full training "
                      f"({a.train} iterations, every pixel, {t_train:.1f} s) + the {a.spp}-spp final render of "
                      f"{ntiles} tiles of 32x32 ({len(pix)} px, {t_render:.1f} s); {paths} paths"}

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 9
+#define PG_ABI_VERSION 10
 
 typedef int32_t pg_status;
 enum {
@@ -247,7 +247,8 @@ typedef struct pg_stats {
     double shade_ms;          /* device time of the shading kernels (all material classes) */
     double shadow_ms;
     double other_ms;
-    uint64_t trace_launches;  /* bounces launched (one trace + one shadow launch each) */
+    uint64_t trace_launches;  /* closest-hit launches timed alone (the camera rays; every bounce with
+                                 PG_NO_RAYS_FUSION) */
     uint64_t stree_nodes;
     uint64_t dtree_nodes;
     uint64_t shade_launches;  /* material-class shading launches */
@@ -255,6 +256,9 @@ typedef struct pg_stats {
     uint64_t volume_launches;
     uint64_t density_lookups; /* volpath: trilinear density-grid lookups (tentative collisions) */
     uint64_t escaped;         /* path integrator: segments whose ray left the scene (not shaded) */
+    double rays_ms;           /* device time of the fused shadow + closest-hit launches (k_rays; kernel_timing) */
+    uint64_t rays_launches;   /* k_rays launches (a bounce's shadow rays + the next bounce's closest hits) */
+    uint64_t shadow_launches; /* unfused shadow-ray launches (PG_NO_RAYS_FUSION) */
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */
@@ -380,6 +384,14 @@ pg_status pg_comm_allreduce_tree_stats(void *ctx);
 pg_status pg_comm_reduce_film(void *ctx, int32_t root);
 /* In-place sum over ranks of n host doubles (e.g. inverse-variance combination statistics). */
 pg_status pg_comm_allreduce_f64(void *ctx, double *values, uint64_t n);
+/* The record exchange SURVEY.md §5/§8e names (north_star: "RCCL all-gather of records"), the
+ * alternative to pg_splat_local_records + pg_comm_allreduce_tree_stats in the postprogression slot:
+ * every rank's record count (ncclAllGather of one u64), then every rank's records (ncclAllGather,
+ * padded to the largest count), then every rank splats ALL records into its building tree, in rank
+ * order.  Integer splat sums commute, so every rank ends with the tree one GPU builds from all
+ * records, bit for bit -- the same tree as the statistics all-reduce.  counts_out (may be NULL):
+ * world_size record counts.  The local records stay until pg_refit. */
+pg_status pg_comm_allgather_records(void *ctx, uint64_t *counts_out);
 
 #ifdef __cplusplus
 }

@@ -99,7 +99,8 @@ class pg_stats(C.Structure):
                 ("trace_ms", C.c_double), ("shade_ms", C.c_double), ("shadow_ms", C.c_double), ("other_ms", C.c_double),
                 ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
                 ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64),
-                ("density_lookups", C.c_uint64), ("escaped", C.c_uint64)]
+                ("density_lookups", C.c_uint64), ("escaped", C.c_uint64), ("rays_ms", C.c_double),
+                ("rays_launches", C.c_uint64), ("shadow_launches", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -176,10 +177,11 @@ SIGNATURES = [
     ("pg_comm_allreduce_tree_stats", C.c_int32, [VP]),
     ("pg_comm_reduce_film", C.c_int32, [VP, C.c_int32]),
     ("pg_comm_allreduce_f64", C.c_int32, [VP, VP, C.c_uint64]),
+    ("pg_comm_allgather_records", C.c_int32, [VP, VP]),
 ]
 
 
-PG_ABI_VERSION = 9  # include/pg_capi.h
+PG_ABI_VERSION = 10  # include/pg_capi.h
 PG_COMM_ID_BYTES = 128
 
 

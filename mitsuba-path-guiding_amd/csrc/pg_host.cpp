@@ -98,6 +98,8 @@ struct PinnedBuf {
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
+// what a timed launch ran (pg_stats buckets)
+enum LaunchKind { KT_TRACE = 0, KT_SHADE = 1, KT_SHADOW = 2, KT_RAYS = 3 };
 
 // One in-flight chunk of paths: its own stream, path state, queues and counters.  pg_render_pass
 // interleaves pg_config.path_lanes lanes, so while the host waits for one lane's per-bounce class counts the
@@ -120,6 +122,7 @@ struct Lane {
     uint32_t *h_counts = nullptr;  // pinned: per-bounce class counts of the running chunk
     uint32_t *h_stats = nullptr;   // pinned: counters of the last finished chunk
     std::vector<EventPair> ev[2];  // kernel-timing events: running chunk / last finished chunk
+    std::vector<uint8_t> evkind[2];  // LaunchKind of each used pair
     size_t evused[2] = {0, 0};
     int evcur = 0;
     hipEvent_t ready = nullptr;    // class counts of the current bounce are on the host
@@ -401,8 +404,11 @@ pg_status downloadSd(Ctx *c) {
     return PG_OK;
 }
 
-EventPair nextEvents(Lane *l) {
+EventPair nextEvents(Lane *l, LaunchKind kind) {
     std::vector<EventPair> &pool = l->ev[l->evcur];
+    std::vector<uint8_t> &kinds = l->evkind[l->evcur];
+    kinds.resize(l->evused[l->evcur] + 1);
+    kinds[l->evused[l->evcur]] = (uint8_t)kind;
     if (l->evused[l->evcur] == pool.size()) {
         EventPair e;
         (void)hipEventCreate(&e.a);
@@ -1191,8 +1197,11 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     const SDDev sd = sdView(c);
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);
     const bool evt = c->cfg.kernel_timing != 0;  // per-launch HIP events (pg_stats trace/shade/shadow_ms)
-    const bool fuseRays = !evt && !std::getenv("PG_NO_RAYS_FUSION");
-    const bool fuseShade = !evt && !c->has_env && !std::getenv("PG_NO_SHADE_FUSION");
+    // the fused launches (k_rays: shadow rays + next closest hits; k_shade_all: every material class)
+    // are what a render runs; with kernel_timing they are timed as launched (pg_stats rays_ms /
+    // shade_ms), so a one-lane calibration context measures the shipped kernels
+    const bool fuseRays = !std::getenv("PG_NO_RAYS_FUSION");
+    const bool fuseShade = !c->has_env && !std::getenv("PG_NO_SHADE_FUSION");
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
     const uint32_t pixPer = std::min(npix, want);
@@ -1220,7 +1229,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         Queue cls[PG_NUM_CLASSES + 1];
         classQueues(l, cb, cls);
         EventPair et{};
-        if (evt) et = nextEvents(&l);
+        if (evt) et = nextEvents(&l, shq ? KT_RAYS : KT_TRACE);
         if (evt) HIPC(c, hipEventRecord(et.a, l.stream));
         const Queue tq = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb);
         if (shq) pg_launch_rays(l.stream, g, sc, pathView(&l), tq, l.bound, cls, *shq, l.bound);
@@ -1250,15 +1259,15 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         }
         const int prev = l.evcur ^ 1;
         std::vector<EventPair> &pool = l.ev[prev];
-        for (size_t e = 0; e + 2 < l.evused[prev]; e += 3) {
+        for (size_t e = 0; e < l.evused[prev]; ++e) {
             float ms = 0;
             (void)hipEventElapsedTime(&ms, pool[e].a, pool[e].b);
-            c->stats.trace_ms += ms;
-            (void)hipEventElapsedTime(&ms, pool[e + 1].a, pool[e + 1].b);
-            c->stats.shade_ms += ms;
-            (void)hipEventElapsedTime(&ms, pool[e + 2].a, pool[e + 2].b);
-            c->stats.shadow_ms += ms;
-            c->stats.trace_launches++;
+            switch (l.evkind[prev][e]) {
+                case KT_TRACE: c->stats.trace_ms += ms; c->stats.trace_launches++; break;
+                case KT_SHADE: c->stats.shade_ms += ms; break;
+                case KT_SHADOW: c->stats.shadow_ms += ms; c->stats.shadow_launches++; break;
+                default: c->stats.rays_ms += ms; c->stats.rays_launches++;
+            }
         }
         l.evused[prev] = 0;
         l.stats_pending = false;
@@ -1378,7 +1387,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         const Queue next = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb + kBounceWords);
         const Queue shq = lqueue(l, l.qs.as<uint32_t>(), cb + kShadowCounts);
         EventPair es{}, ew{};
-        if (evt) es = nextEvents(&l), ew = nextEvents(&l);
+        if (evt) es = nextEvents(&l, KT_SHADE);
         if (evt) HIPC(c, hipEventRecord(es.a, l.stream));
         if (fuseShade) {  // one launch for every class present
             pg_launch_shade_all(l.stream, g, sc, sd, pv, cls, clsMax, next, shq);
@@ -1393,6 +1402,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
         // without per-launch timing the shadow rays share the next trace's launch
         if (fuseRays) return launchTrace(l, &shq);
+        if (evt) ew = nextEvents(&l, KT_SHADOW);
         if (evt) HIPC(c, hipEventRecord(ew.a, l.stream));
         pg_launch_shadow(l.stream, sc, pv, shq, l.bound);
         if (evt) HIPC(c, hipEventRecord(ew.b, l.stream));
@@ -1628,15 +1638,18 @@ pg_status pg_comm_allreduce_tree_stats(void *ctx) {
     if (!c->comm) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_tree_stats: no communicator (pg_comm_init)");
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_tree_stats: no scene");
     HIPC(c, hipSetDevice(c->cfg.device));
-    const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
-    // in place on the device building state: the u64 quadrant sums and per-D-tree record counts
-    // (the pg_get_tree_stats vector); integer sums, so every rank ends with identical statistics
-    NCCLC(c, ncclGroupStart());
-    NCCLC(c, ncclAllReduce(c->sd_bsum.p, c->sd_bsum.p, 4 * nb, ncclUint64, ncclSum, c->comm, c->stream));
-    NCCLC(c, ncclAllReduce(c->sd_count.p, c->sd_count.p, nl, ncclUint64, ncclSum, c->comm, c->stream));
-    NCCLC(c, ncclGroupEnd());
-    HIPC(c, hipStreamSynchronize(c->stream));
-    return PG_OK;
+    // the reduced vector IS the pg_get_tree_stats vector (u64 quadrant sums, then per-D-tree record
+    // counts): gathered with pg_get_tree_stats into one device buffer, summed over ranks, put back
+    // with pg_put_tree_stats -- so the multi-rank arithmetic is the one the torch.distributed /
+    // gloo exchange tests check.  Integer sums: every rank ends with identical statistics.
+    uint64_t words = 0;
+    pg_status st;
+    if ((st = pg_get_tree_stats(ctx, nullptr, 0, 1, &words))) return st;
+    DevBuf v;
+    HIPC(c, v.alloc(std::max<uint64_t>(words, 1) * 8));
+    if ((st = pg_get_tree_stats(ctx, v.p, words, 1, &words))) return st;
+    NCCLC(c, ncclAllReduce(v.p, v.p, words, ncclUint64, ncclSum, c->comm, c->stream));
+    return pg_put_tree_stats(ctx, v.p, words, 1);
 }
 
 pg_status pg_comm_reduce_film(void *ctx, int32_t root) {
@@ -1671,6 +1684,40 @@ pg_status pg_comm_allreduce_f64(void *ctx, double *values, uint64_t n) {
     HIPC(c, hipMemcpyAsync(b.p, values, n * 8, hipMemcpyHostToDevice, c->stream));
     NCCLC(c, ncclAllReduce(b.p, b.p, n, ncclFloat64, ncclSum, c->comm, c->stream));
     HIPC(c, hipMemcpyAsync(values, b.p, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_comm_allgather_records(void *ctx, uint64_t *counts_out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c) return fail(nullptr, PG_ERR_INVALID, "pg_comm_allgather_records: null context");
+    if (!c->comm) return fail(c, PG_ERR_STATE, "pg_comm_allgather_records: no communicator (pg_comm_init)");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_comm_allgather_records: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    const int W = c->cfg.world_size;
+    // 1. every rank's record count
+    DevBuf cnt;
+    HIPC(c, cnt.alloc((size_t)(W + 1) * 8));
+    const uint64_t mine = c->rec_host_count;
+    HIPC(c, hipMemcpyAsync(cnt.as<uint64_t>() + W, &mine, 8, hipMemcpyHostToDevice, c->stream));
+    NCCLC(c, ncclAllGather(cnt.as<uint64_t>() + W, cnt.p, 1, ncclUint64, c->comm, c->stream));
+    std::vector<uint64_t> counts(W);
+    HIPC(c, hipMemcpyAsync(counts.data(), cnt.p, (size_t)W * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    const uint64_t maxn = *std::max_element(counts.begin(), counts.end());
+    if (counts_out) std::copy(counts.begin(), counts.end(), counts_out);
+    if (maxn == 0) return PG_OK;
+    // 2. the records, each rank's block padded to the largest count (the send buffer is the local
+    //    record buffer, grown to maxn: its tail past the local count is never splatted)
+    pg_status st;
+    if ((st = ensureRecords(c, maxn))) return st;
+    HIPC(c, c->ext_records.alloc((size_t)W * maxn * sizeof(pg_record)));
+    NCCLC(c, ncclAllGather(c->records.p, c->ext_records.p, maxn * sizeof(pg_record), ncclUint8, c->comm, c->stream));
+    // 3. splat every rank's records (rank order; integer sums, so the order does not change the tree)
+    const SDDev sd = sdView(c);
+    for (int r = 0; r < W; ++r)
+        if (counts[r]) pg_launch_splat(c->stream, sd, c->ext_records.as<pg_record>() + (size_t)r * maxn, counts[r]);
+    HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }
@@ -1824,7 +1871,7 @@ pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hi
     DevBuf r, h, ovf;
     HIPC(c, r.alloc(n * 32));
     HIPC(c, h.alloc(n * 16));
-    HIPC(c, ovf.alloc(pg_stack_overflow_words((n + 127) / 128 * 128) * 4));
+    HIPC(c, ovf.alloc(pg_stack_overflow_words(pg_trace_rays_threads(n)) * 4));
     HIPC(c, hipMemcpyAsync(r.p, rays, n * 32, hipMemcpyHostToDevice, c->stream));
     pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, any_hit, h.as<float>(), ovf.as<uint32_t>());
     HIPC(c, hipGetLastError());

@@ -125,6 +125,8 @@ void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, 
                           uint32_t *ovf);
 // words of traversal-stack overflow storage for a launch of max_threads (0 = persistent grid)
 size_t pg_stack_overflow_words(uint64_t max_threads);
+// threads pg_launch_trace_rays launches for n rays (size its overflow ring with this)
+uint64_t pg_trace_rays_threads(uint64_t n);
 void pg_launch_bsdf_query(hipStream_t s, const GMat *mat, const float *wi, const float *u, const float *wog,
                           uint32_t n, float *out);
 void pg_launch_sd_pdf(hipStream_t s, const SDDev &sd, const float *pos, const float *dir, uint32_t n, float *out);

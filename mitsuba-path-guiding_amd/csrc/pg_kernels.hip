@@ -608,8 +608,9 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
         valid = woPdf > 0 && val >= 0 && val < 1e30f;
         if (valid) {
             float s = val * 16777216.0f;
-            // cap 2^48 (value <= 2^24): 2^16 records at the cap still fit one u64 quadrant sum, so the
-            // sums over records and ranks cannot wrap (oracle kSplatCap)
+            // cap 2^48 (value <= 2^24; oracle kSplatCap).  A leaf quadrant's u64 atomic sum over all
+            // records and ranks of an iteration wraps only past 2^40 value units (e.g. 2^16 records at
+            // the cap); the host refit's interior sums saturate (pg_sdtree.cpp propagate)
             if (s >= 281474976710656.0f) s = 281474976710656.0f;
             fx = (unsigned long long)s;
             const SDView sv = sdv(sd);
@@ -723,6 +724,8 @@ size_t pg_stack_overflow_words(uint64_t max_threads) {
     const size_t words = std::max<size_t>(STACK_DEPTH - LDS_STACK, 2 * (STACK_DEPTH - WIDE_LDS_STACK));
     return words * max_threads;
 }
+// threads k_trace_rays launches for n rays: its overflow stride is gridDim.x * TRACE_BLOCK
+uint64_t pg_trace_rays_threads(uint64_t n) { return (uint64_t)blocks(n, TRACE_BLOCK) * TRACE_BLOCK; }
 
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
                       uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q) {

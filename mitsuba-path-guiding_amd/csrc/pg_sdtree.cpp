@@ -37,12 +37,13 @@ void parallelFor(size_t n, F &&f) {
 }
 inline float total4(const float *s) { return ((s[0] + s[1]) + s[2]) + s[3]; }
 
-// bottom-up quadrant sums of a building tree (integer, exact)
+// bottom-up quadrant sums of a building tree (integer, exact below 2^64; saturating above, as the
+// oracle's buildSums: a D-tree's total is the sum of all its records over every rank)
 uint64_t propagate(std::vector<SdNodeB> &b, uint32_t n) {
     uint64_t tot = 0;
     for (int q = 0; q < 4; ++q) {
         if (b[n].child[q]) b[n].sum[q] = propagate(b, b[n].child[q]);
-        tot += b[n].sum[q];
+        tot = (tot + b[n].sum[q] < tot) ? ~0ull : tot + b[n].sum[q];
     }
     return tot;
 }

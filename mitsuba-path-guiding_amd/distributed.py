@@ -124,10 +124,19 @@ def init_capi_comm(dev):
     dev.comm_init(np.frombuffer(obj[0], np.uint8))
 
 
-def make_capi_exchange():
-    """exchange(dev) through the library's communicator (after init_capi_comm): splat the local
-    records, then pg_comm_allreduce_tree_stats (in-place RCCL all-reduce of the device building
-    statistics).  Returns every rank's record count."""
+def make_capi_exchange(mode="allreduce"):
+    """exchange(dev) through the library's communicator (after init_capi_comm).  Returns every
+    rank's record count.
+
+    mode="allreduce": splat the local records, then pg_comm_allreduce_tree_stats (in-place RCCL
+    all-reduce of the device building statistics).
+    mode="allgather": pg_comm_allgather_records (RCCL all-gather of every rank's records, each rank
+    splats all of them); the same tree bit for bit."""
+    if mode not in ("allreduce", "allgather"):
+        raise ValueError(f"unknown exchange mode {mode!r}")
+    if mode == "allgather":
+        return lambda dev: dev.comm_allgather_records()
+
     def exchange(dev):
         import torch.distributed as dist
         counts = np.zeros(dist.get_world_size(), np.float64)

@@ -179,6 +179,13 @@ class Device:
     def comm_reduce_film(self, root=0):
         self._chk(self.lib.pg_comm_reduce_film(self.h, int(root)))
 
+    def comm_allgather_records(self):
+        """pg_comm_allgather_records: every rank's records splatted into every rank's building tree;
+        returns the per-rank record counts."""
+        out = np.zeros(self.cfg.world_size, np.uint64)
+        self._chk(self.lib.pg_comm_allgather_records(self.h, _p(out)))
+        return [int(x) for x in out]
+
     def comm_allreduce_f64(self, values):
         v = np.ascontiguousarray(values, np.float64).copy()
         self._chk(self.lib.pg_comm_allreduce_f64(self.h, _p(v), len(v)))
@@ -293,9 +300,12 @@ class ProgressivePathTracer:
     guided = False
     integrator = capi.PG_INTEGRATOR_PATH
 
-    def __init__(self, props=None, device=0, rank=0, world_size=1):
+    def __init__(self, props=None, device=0, rank=0, world_size=1, reduce_sum=None):
         props = dict(props or {})
         self.props = props
+        # callable(np.float64 array) -> its element-wise sum over ranks (world_size > 1): maxRenderTime's
+        # progression agreement, inverse-variance weights over the whole image
+        self.reduce_sum = reduce_sum
         self.cfg = capi.default_config(
             device=device, rank=rank, world_size=world_size,
             max_depth=int(props.get("maxDepth", -1)), rr_depth=int(props.get("rrDepth", 5)),
@@ -348,7 +358,9 @@ class ProgressivePathTracer:
         (whole progressions until the budget, counted from budget_start, is spent); returns (rgbw, sumsq)."""
         import time
         t0 = time.perf_counter() if budget_start is None else budget_start
-        if self.max_render_time > 0:
+        if self.max_render_time > 0 and self.cfg.world_size > 1:
+            self.rendered_spp = self._render_time_sharded(t0)
+        elif self.max_render_time > 0:
             left = self.max_render_time - (time.perf_counter() - t0)
             done = 0
             if left > 0 and not self._cancel.is_set():
@@ -369,6 +381,36 @@ class ProgressivePathTracer:
         if getattr(self.dev.scene, "mirror_x", False):  # a mirrored sensor (e.g. <scale x="-1"/> in toWorld)
             rgbw, sq = rgbw[:, ::-1].copy(), sq[:, ::-1].copy()
         return rgbw, sq
+
+    def _render_time_sharded(self, t0):
+        """maxRenderTime with a tile shard (world_size > 1): the ranks must render the same number of
+        whole progressions, or the reduced image would mix tile-dependent sample counts (the
+        reference's renderTime keeps progressions image-wide, progressiveintegrator.cpp:117-168).
+        Every decision is taken from all-reduced clocks, so it is identical on every rank: before
+        each batch the ranks sum a vector holding each rank's elapsed time and seconds per progression
+        in its own slot; the slowest rank's figures size the next batch (at most half the remaining
+        budget, as pg_render_time does) or stop the render.  Needs reduce_sum (a sum over ranks)."""
+        import time
+        reduce_sum = self.reduce_sum
+        if reduce_sum is None:
+            raise ValueError("maxRenderTime with world_size > 1 needs reduce_sum (a sum over ranks) to keep the "
+                             "ranks' progression counts equal")
+        W, r = self.cfg.world_size, self.cfg.rank
+        done, per_prog = 0, 0.0
+        while not self._cancel.is_set():
+            v = np.zeros(2 * W, np.float64)
+            v[r], v[W + r] = time.perf_counter() - t0, per_prog
+            v = np.asarray(reduce_sum(v), np.float64)
+            elapsed, pp = float(v[:W].max()), float(v[W:].max())
+            if elapsed >= self.max_render_time:
+                break
+            progs = 1 if done == 0 else int(max(1.0, min(np.floor(0.5 * (self.max_render_time - elapsed) /
+                                                                   max(pp, 1e-9)), 1e6)))
+            t = time.perf_counter()
+            self.render_progression(progs * self.spp_per_progression)
+            done += progs * self.spp_per_progression
+            per_prog = (time.perf_counter() - t) / progs
+        return done
 
     def denoiser_features(self):
         """Per-pixel means of the first-hit albedo and normal (what Denoiser::add averages,
@@ -418,12 +460,9 @@ class GuidedPathTracer(ProgressivePathTracer):
     guided = True
 
     def __init__(self, props=None, device=0, rank=0, world_size=1, exchange=None, reduce_sum=None):
-        super().__init__(props, device, rank, world_size)
+        super().__init__(props, device, rank, world_size, reduce_sum)
         self.training_iterations = int(self.props.get("trainingIterations", 5))
         self.exchange = exchange  # callable(dev): the postprogression statistics exchange (N > 1)
-        # callable(np.float64 array) -> its sum over ranks (N > 1): inverse-variance weights from the
-        # whole image, not this rank's tiles
-        self.reduce_sum = reduce_sum
         self.initial_tree = None
         self.sample_combination = str(self.props.get("sampleCombination", "discard")).lower()
         if self.sample_combination not in ("discard", "inversevar"):

@@ -25,8 +25,9 @@
 namespace orc {
 
 constexpr float kFixedScale = 16777216.0f;  // 2^24
-// per-record cap of the fixed-point value, 2^48 (radiance / woPdf <= 2^24): 2^16 records at the cap
-// still fit a u64 quadrant sum, so sums across records and ranks cannot wrap
+// per-record cap of the fixed-point value, 2^48 (radiance / woPdf <= 2^24).  A leaf quadrant's u64 sum
+// (device atomics, all records and ranks of one iteration) wraps only past 2^40 value units, e.g. 2^16
+// records at the cap; interior sums saturate instead of wrapping (buildSums)
 constexpr float kSplatCap = 281474976710656.0f;
 constexpr uint32_t kSdMagic = 0x44534750u;    // 'PGSD'
 
@@ -251,7 +252,7 @@ struct SDTree {
         uint64_t tot = 0;
         for (int q = 0; q < 4; ++q) {
             if (b[n].child[q] != 0) b[n].sum[q] = buildSums(b, b[n].child[q]);
-            tot += b[n].sum[q];
+            tot = (tot + b[n].sum[q] < tot) ? ~0ull : tot + b[n].sum[q];  // saturating (pg_sdtree.cpp propagate)
         }
         return tot;
     }

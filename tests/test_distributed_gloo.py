@@ -165,3 +165,47 @@ def test_shard_covers_image_once():
     parts = [tile_shard(W, H, r, 3) for r in range(3)]
     allp = np.concatenate(parts)
     assert len(allp) == W * H and len(np.unique(allp)) == W * H
+
+
+class _SleepDevice:
+    """Stand-in for the render-time test: a pass of spp samples takes spp x `per_spp` seconds."""
+
+    def __init__(self, per_spp):
+        self.per_spp = per_spp
+        self.spp = 0
+
+    def render_pass(self, spp, offset, record=False):
+        import time
+        time.sleep(spp * self.per_spp)
+        self.spp += spp
+
+
+def _render_time_worker(rank, world, port, outdir):
+    sys.path.insert(0, ROOT)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    import pgload
+    pg = pgload.load()
+    from mitsuba_path_guiding_amd import distributed as D
+    from mitsuba_path_guiding_amd.integrator import ProgressivePathTracer
+    import time
+    D.init("gloo")
+    t = ProgressivePathTracer({"maxRenderTime": 0.6, "samplesPerProgression": 2}, rank=rank, world_size=world,
+                              reduce_sum=D.make_reduce_sum(False))
+    t.dev = _SleepDevice(0.002 * (1 + 3 * rank))  # rank 1 is 4x slower: its clock must rule
+    t0 = time.perf_counter()
+    done = t._render_time_sharded(t0)
+    np.save(os.path.join(outdir, f"rt{rank}.npy"), np.array([done, t.dev.spp, time.perf_counter() - t0]))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_max_render_time_sharded_ranks_agree(tmp_path):
+    """maxRenderTime with a tile shard: every rank renders the same number of whole progressions,
+    sized by the slowest rank's clock, and the budget holds (per-rank clocks left the
+    reduced image with tile-dependent sample counts)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_render_time_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = np.load(tmp_path / "rt0.npy"), np.load(tmp_path / "rt1.npy")
+    assert r0[0] == r1[0] == r0[1] == r1[1] > 0 and r0[0] % 2 == 0
+    assert r1[2] < 0.6 * 1.6 + 0.2  # overshoot below about half the budget plus one progression

@@ -11,7 +11,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _train(pg, sc, comm):
+def _train(pg, sc, comm, mode="allreduce"):
     from mitsuba_path_guiding_amd.integrator import Device
     d = Device(pg.capi.default_config(guiding=1, s_tree_threshold=200.0))
     d.upload(sc)
@@ -22,8 +22,12 @@ def _train(pg, sc, comm):
     for it in range(3):
         d.render_pass(2 ** it, off, record=True)
         off += 2 ** it
-        d.splat_local()
-        if comm:
+        if comm and mode == "allgather":  # pg_comm_allgather_records: gather + splat of every rank's records
+            n = d.record_count()
+            assert d.comm_allgather_records() == [n] and n > 0
+        else:
+            d.splat_local()
+        if comm and mode == "allreduce":
             before = d.get_tree_stats()
             d.comm_allreduce_tree_stats()
             assert np.array_equal(before, d.get_tree_stats())
@@ -46,6 +50,9 @@ def test_single_rank_communicator_is_identity(pg):
     t1, f1 = _train(pg, sc, True)
     assert np.array_equal(t0, t1)
     assert np.array_equal(f0[0], f1[0])
+    t2, f2 = _train(pg, sc, True, mode="allgather")
+    assert np.array_equal(t0, t2)
+    assert np.array_equal(f0[0], f2[0])
 
 
 def test_comm_calls_need_a_communicator(pg):
@@ -56,4 +63,6 @@ def test_comm_calls_need_a_communicator(pg):
         d.comm_allreduce_tree_stats()
     with pytest.raises(PGError, match="no communicator"):
         d.comm_reduce_film(0)
+    with pytest.raises(PGError, match="no communicator"):
+        d.comm_allgather_records()
     d.close()

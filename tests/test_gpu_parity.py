@@ -61,6 +61,37 @@ def test_trace_parity(pg, O, scenes, name):
     dev.close()
 
 
+@pytest.mark.parametrize("n", [1, 257, 4097])
+def test_trace_rays_ragged_bunny(pg, O, n):
+    """pg_trace_rays at ragged ray counts on the deep bunny BVH (data/tests/bunny.ply): the overflow
+    ring is sized from the launched threads (pg_trace_rays_threads), not a hard-coded block size."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "bunny.npz"))
+    V, F = z["positions"], z["faces"]
+    s = pg.scenes.Scene()
+    s.add_mesh(V, F, material=s.add_material(pg.scenes.material("diffuse")))
+    c = V.mean(0)
+    s.set_camera(tuple(c + np.array([0, 0, 1.0])), tuple(c), (0, 1, 0), 40, 8, 8)
+    s.finalize()
+    rng = np.random.default_rng(n)
+    lo, hi = V.min(0), V.max(0)
+    ctr, rad = (lo + hi) / 2, np.linalg.norm(hi - lo) / 2
+    a, b = rng.normal(size=(n, 3)), rng.normal(size=(n, 3))
+    a = ctr + rad * a / np.linalg.norm(a, axis=1, keepdims=True)
+    b = ctr + rad * 0.2 * b / np.linalg.norm(b, axis=1, keepdims=True)  # chords through the body
+    d = (b - a) / np.linalg.norm(b - a, axis=1, keepdims=True)
+    rays = np.zeros((n, 8), np.float32)
+    rays[:, 0:3], rays[:, 3], rays[:, 4:7], rays[:, 7] = a, 0.0, d, np.inf
+    dev = make_dev(pg, s)
+    g = dev.trace_rays(rays)
+    occ = dev.trace_rays(rays, any_hit=True)[:, 0] > 0.5
+    dev.close()
+    cpu = O.OracleScene(pg.capi, s).trace(rays)
+    gp, cp = g[:, 1].view(np.uint32), cpu[:, 1].view(np.uint32)
+    assert (gp == cp).mean() >= (0.99 if n > 100 else 1.0)
+    assert (occ == (gp != 0xFFFFFFFF)).mean() >= (0.999 if n > 100 else 1.0)
+
+
 def test_dgeom_kat_gpu(pg, O):
     """src/tests/test_dgeom.cpp:36-121 through the GPU traversal (t, barycentrics)."""
     import json, os

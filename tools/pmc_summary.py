@@ -7,8 +7,9 @@ WRITE_SIZE is taken as-is.  Both counters are in KiB.
 
 bench.py measures the kernel roofline on a one-lane context after the timed region (the timed job
 overlaps three lanes, so per-launch durations there include other lanes' work).  That context's
-stream is the last one to launch k_trace, so the path kernels (k_trace, k_shade, k_shadow) are
-summarised over that stream only ("calibration" view) as well as over the whole run.
+stream is the last one to launch k_trace, so the path kernels (k_trace, k_shade_all, k_rays; the
+unfused k_shade, k_shadow when fusion is off) are summarised over that stream only ("calibration"
+view) as well as over the whole run.
 usage: python tools/pmc_summary.py gpurun_out/prof_rNN profiles/rNN
 """
 import csv
@@ -18,7 +19,7 @@ import subprocess
 import sys
 from collections import defaultdict
 
-PATH_KERNELS = ("k_trace", "k_shade", "k_shadow")
+PATH_KERNELS = ("k_trace", "k_shade", "k_shadow", "k_shade_all", "k_rays")
 
 
 def base_name(n):
