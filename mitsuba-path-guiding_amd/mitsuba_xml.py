@@ -21,6 +21,11 @@ adapter's flatten() produces from Scene::getShapes()/getBSDFs() (INTEGRATION.md)
                     toWorld, flipNormals, faceNormals, a nested or referenced bsdf and an area emitter
   emitter           area (in a shape), envmap (.npy / .pfm / uncompressed or zlib EXR), constant
                     (as a uniform envmap)
+  medium            homogeneous (sigmaS / sigmaA or sigmaT / albedo, scale, g; grey sigmaT) with an hg or
+                    isotropic phase, declared at the top level or nested in a shape, attached to
+                    shapes as <ref name="interior|exterior">; a shape without a BSDF is a null
+                    (index-matched) surface when it is a medium transition, black diffuse when it is
+                    an emitter, 0.5 diffuse otherwise (Shape::configure, shape.cpp:48-72)
 
 Anything else raises NotImplementedError naming the plugin (strict=True), or is collected in
 `XMLScene.skipped` (strict=False).  Mesh normals follow TriMesh::computeNormals (trimesh.cpp:608-680):
@@ -97,6 +102,7 @@ class _Loader:
         self.strict = strict
         self.sphere_res = sphere_res
         self.ids = {}
+        self.media = []  # homogeneous media in declaration order: (sigma_t, albedo rgb, g); built in finish()
         self.out = XMLScene()
         self.sc = scenes.Scene()
         self.mat_index = {}  # id(pg_material) -> scene material index
@@ -339,6 +345,7 @@ class _Loader:
         V, F, N = res
         mat = None
         radiance = None
+        sides = {"interior": -1, "exterior": -1}
         for c in el:
             if c.tag in ("bsdf", "ref") and (c.tag == "bsdf" or isinstance(self.ids.get(c.get("id")), capi.pg_material)):
                 mat = self.child_bsdf(c)
@@ -350,16 +357,84 @@ class _Loader:
                 radiance = tuple(np.asarray(ep.get("radiance", np.ones(3))).reshape(-1).tolist())
                 if len(radiance) == 1:
                     radiance = radiance * 3
-            elif c.tag in ("medium",) or (c.tag == "ref" and c.get("name") in ("interior", "exterior")):
-                self.unsupported("shape", typ, "participating media are built with Scene.add_medium")
-        if mat is None:
-            mat = scenes.material("diffuse", reflectance=(0.5, 0.5, 0.5))  # Shape default BSDF (shape.cpp)
+            elif c.tag == "medium" or (c.tag == "ref" and c.get("name") in ("interior", "exterior")):
+                side = self.attr(c, "name")
+                if side not in sides:
+                    raise ValueError(f"<{c.tag}> in a shape needs name=\"interior\" or \"exterior\"")
+                if c.tag == "medium":
+                    sides[side] = self.medium(c)
+                else:
+                    obj = self.ids.get(self.attr(c, "id"))
+                    if not (isinstance(obj, tuple) and obj[0] == "medium"):
+                        raise ValueError(f"<ref id=\"{c.get('id')}\"> is not a medium")
+                    sides[side] = obj[1]
+        transition = sides["interior"] >= 0 or sides["exterior"] >= 0
+        if mat is None:  # Shape::configure (shape.cpp:48-72)
+            if radiance is not None:
+                mat = scenes.material("diffuse", reflectance=(0.0, 0.0, 0.0))
+            elif transition:
+                mat = scenes.material("null")
+            else:
+                mat = scenes.material("diffuse", reflectance=(0.5, 0.5, 0.5))
         m = self.material_index(mat)
-        if N is None:
-            self.sc.add_mesh(V.astype(np.float32), F.astype(np.uint32), None, material=m, radiance=radiance)
-        else:
-            self.sc.add_mesh(V.astype(np.float32), F.astype(np.uint32), N.astype(np.float32), material=m,
-                             radiance=radiance)
+        self.sc.add_mesh(V.astype(np.float32), F.astype(np.uint32), None if N is None else N.astype(np.float32),
+                         material=m, radiance=radiance, interior=sides["interior"], exterior=sides["exterior"])
+
+    # -- participating media (src/medium/homogeneous.cpp, materials.h:90-195 lookupMaterial)
+    def medium(self, el):
+        typ = self.attr(el, "type")
+        if typ != "homogeneous":
+            raise NotImplementedError(f"<medium type=\"{typ}\">: only homogeneous media are flattened from XML "
+                                      "(heterogeneous grids are built with Scene.add_medium)")
+        P = self.props(el)
+        if "material" in P:
+            raise NotImplementedError("<medium>: material presets (materials.h) are not restated; give sigmaS/sigmaA "
+                                      "or sigmaT/albedo")
+        has_as, has_ta = "sigmaS" in P or "sigmaA" in P, "sigmaT" in P or "albedo" in P
+        if has_as and has_ta:
+            raise ValueError("<medium>: sigmaS & sigmaA *or* sigmaT & albedo (materials.h:104-106)")
+        one = np.ones(3)
+        if has_ta:
+            st, alb = np.asarray(P.get("sigmaT", one), np.float64), np.asarray(P.get("albedo", one), np.float64)
+            ss, sa = alb * st, st - alb * st
+        else:  # the Skin1 default preset is not restated: both coefficients must then be given
+            if not has_as:
+                raise NotImplementedError("<medium>: no coefficients (the default Skin1 preset is not restated)")
+            ss, sa = np.asarray(P.get("sigmaS", 0 * one), np.float64), np.asarray(P.get("sigmaA", 0 * one), np.float64)
+        g_red = float(P.get("g", 0.0)) if not isinstance(P.get("g", 0.0), np.ndarray) else float(P["g"][0])
+        scale = float(P.get("scale", 1.0))
+        ss, sa = ss * (1 - g_red) * scale, sa * scale  # Medium::Medium reduced scattering, then lookupMaterial scale
+        st = ss + sa
+        if not np.allclose(st, st[0], rtol=1e-6):
+            raise NotImplementedError("<medium>: chromatic sigmaT (the GPU medium has one extinction per point)")
+        if not st[0] > 0:
+            raise ValueError("<medium>: sigmaT must be > 0")
+        g = 0.0
+        for c in el:
+            if c.tag == "phase":
+                pt = self.attr(c, "type")
+                if pt == "hg":
+                    g = float(self.props(c).get("g", 0.8))  # hg.cpp:50
+                elif pt != "isotropic":
+                    raise NotImplementedError(f"<phase type=\"{pt}\"> (hg and isotropic only)")
+        self.media.append((float(st[0]), tuple((ss / st).tolist()), g))
+        idx = len(self.media) - 1
+        if el.get("id"):
+            self.ids[el.get("id")] = ("medium", idx)
+        return idx
+
+    def finish_media(self):
+        """A homogeneous medium is a constant density over a box that holds the whole scene (shape
+        bounds enlarged by their extent): paths only enter it through transition surfaces and end at
+        scene geometry, so the box bounds nothing that matters."""
+        if not self.media:
+            return
+        P = np.concatenate(self.sc._pos)
+        lo, hi = P.min(0), P.max(0)
+        ext = float((hi - lo).max()) + 1e-3
+        for st, alb, g in self.media:
+            self.sc.add_medium(np.ones((2, 2, 2), np.float32), tuple((lo - ext).tolist()), tuple((hi + ext).tolist()),
+                               st, alb, g)
 
     # -- emitters, sensor, integrator
     def emitter(self, el):
@@ -440,7 +515,14 @@ class _Loader:
             elif el.tag in ("default", "include"):
                 if el.tag == "include":
                     self.run(ET.parse(self.path(self.attr(el, "filename"))).getroot())
-            elif el.tag in ("medium", "phase", "texture"):
+            elif el.tag == "medium":
+                try:
+                    self.medium(el)
+                except NotImplementedError as e:
+                    if self.strict:
+                        raise
+                    self.out.skipped.append(("medium", self.attr(el, "type"), str(e)))
+            elif el.tag in ("phase", "texture"):
                 self.unsupported(el.tag, self.attr(el, "type"), "not flattened by this loader")
         return self.out
 
@@ -457,6 +539,7 @@ def load(source, defines=None, strict=True, sphere_res=(64, 32)):
         base = os.getcwd()
     L = _Loader(base, defines or {}, strict, sphere_res)
     out = L.run(root)
+    L.finish_media()
     if L.sc.shapes and L.sc.camera is not None:
         out.scene = L.sc.finalize()
     elif L.sc.shapes:
