@@ -216,14 +216,18 @@ typedef struct pg_config {
                                      f / (alpha p_bsdf + (1 - alpha) p_guide) <= (f / p_bsdf) / alpha by 1 for albedo
                                      bounded BSDF weights.  PG_FRACTION_THROUGHPUT: as ALBEDO with a scaled by the path
                                      throughput max(T), so a path may regain throughput it lost, but not grow past 1.
+                                     PG_FRACTION_LEARNED: alpha per S-tree leaf, learned from the training records
+                                     (after Mueller 2019: the candidate mixture in 0.05, 0.15 .. 0.95 with the largest
+                                     estimated cross-entropy against f * L_i; bsdf_sampling_fraction
+                                     until a leaf has 64 guided records).
                                      Any per-vertex choice independent of the sampled direction is unbiased.
-                                     Default PG_FRACTION_ALBEDO (C3 quality). */
+                                     Default PG_FRACTION_FIXED (Mueller et al. 2017's fixed fraction). */
     int32_t kernel_timing;        /* 1: bracket every closest-hit, shading and shadow launch with HIP events and sum
                                      their device times into pg_stats trace_ms / shade_ms / shadow_ms.  Six event
                                      records per bounce cost ~2 % on C3, so 0 (the default) leaves
                                      those three statistics at 0. */
 } pg_config;
-enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2 };
+enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2, PG_FRACTION_LEARNED = 3 };
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
 enum { PG_MAJORANT_GRID = 0, PG_MAJORANT_GLOBAL = 1 };
 
@@ -233,8 +237,10 @@ typedef struct pg_record {
     uint32_t dir;      /* canonical (cos theta, phi) square coords as 2 x u16 */
     float radiance;    /* average incident radiance estimate along dir */
     float wo_pdf;      /* pdf the direction was sampled with (one-sample MIS) */
-    float product;     /* radiance * bsdf average (reserved for product-driven loss) */
-    float weight;      /* statistical weight (1) */
+    float product;     /* guided vertex: f * L_i / wo_pdf, the BSDF-weighted contribution along dir divided
+                          by the throughput before the vertex (channel average); 0 otherwise */
+    float weight;      /* guided vertex: the D-tree pdf of dir (the mixture's p_guide); -1: not guided.
+                          The learned fraction (PG_FRACTION_LEARNED) reads both in the splat. */
 } pg_record;
 
 typedef struct pg_stats {

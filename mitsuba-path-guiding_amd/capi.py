@@ -16,7 +16,7 @@ PG_OK, PG_ERR_INVALID, PG_ERR_HIP, PG_ERR_OOM, PG_ERR_STATE, PG_ERR_CANCELLED, P
 PG_MEDIUM_HETEROGENEOUS = 0
 PG_INTEGRATOR_PATH, PG_INTEGRATOR_VOLPATH = 0, 1
 PG_MAJORANT_GRID, PG_MAJORANT_GLOBAL = 0, 1
-PG_FRACTION_FIXED, PG_FRACTION_ALBEDO, PG_FRACTION_THROUGHPUT = 0, 1, 2
+PG_FRACTION_FIXED, PG_FRACTION_ALBEDO, PG_FRACTION_THROUGHPUT, PG_FRACTION_LEARNED = 0, 1, 2, 3
 MAJORANT_CELL = 8  # voxels per majorant-grid cell edge (pg_host.cpp / oracle/orc_medium.h)
 PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
 PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
@@ -129,7 +129,7 @@ def default_config(**overrides):
     c.integrator = PG_INTEGRATOR_PATH
     c.distance_guiding = 0.25
     c.aovs = 0
-    c.bsdf_fraction_bound = PG_FRACTION_ALBEDO
+    c.bsdf_fraction_bound = PG_FRACTION_FIXED
     c.kernel_timing = 0
     for k, v in overrides.items():
         if not hasattr(c, k):

@@ -965,6 +965,40 @@ PGD void sdDual(const SDView &v, uint4 meta, bool aOn, float au, float aw, float
         }
     }
 }
+
+// ---- learned BSDF-sampling fraction per S-tree leaf (pg_config.bsdf_fraction_bound =
+// PG_FRACTION_LEARNED; after Mueller 2019, "Practical Path Guiding in Production", which optimizes the
+// selection probability per spatial cell against the KL divergence from the product f * L_i).
+// Instead of Mueller's per-sample Adam steps (sequential, not reproducible across devices), each
+// training iteration estimates the cross-entropy E_{p*}[log2 q_k] of a fixed set of candidate
+// mixtures q_k = a_k p_bsdf + (1 - a_k) p_guide from the iteration's guided records, by importance
+// weights w = f L_i / q0 (q0: the mixture that drew the record):  sum_j w_j log2(q_k(wj) / q0(wj)).
+// The sums are 2^-16 fixed point (exact, order-independent, like the splat) and the refit picks the
+// candidate with the largest (oracle: orc_sdtree.h SDTree::learnedFractions).  Arithmetic shared
+// bit for bit with the oracle (fp contraction off, no libm).
+constexpr int kFracCandidates = 10;
+PGD float fracCandidate(int k) { return 0.05f + 0.1f * (float)k; }  // 0.05 .. 0.95
+constexpr float kFracFixedScale = 65536.0f;                         // 2^16
+constexpr float kFracCap = 70368744177664.0f;                       // 2^46: |w log2 ratio| <= 2^30
+// log2 without libm: exponent bits + 2 atanh((m - 1) / (m + 1)) / ln 2 as a 5-term series, m in [1, 2)
+PGD float pgLog2(float x) {
+    if (!(x > 1.17549435e-38f)) return -126.0f;
+    const uint32_t b = __float_as_uint(x);
+    const float e = (float)((int)((b >> 23) & 0xFFu) - 127);
+    const float m = __uint_as_float((b & 0x7FFFFFu) | 0x3F800000u);
+    const float t = (m - 1.0f) / (m + 1.0f), t2 = t * t;
+    const float s = t * (1.0f + t2 * (0.333333343f + t2 * (0.2f + t2 * (0.142857149f + t2 * 0.111111112f))));
+    return e + s * 2.88539004f;  // 2 / ln 2
+}
+// 2^-16 fixed-point value of w * log2(q_k / q0) for candidate k (two's complement in a u64)
+PGD unsigned long long fracStat(float w, float pb, float pg, float q0, int k) {
+    const float a = fracCandidate(k);
+    const float qk = a * pb + (1.0f - a) * pg;
+    float v = w * pgLog2(qk / q0) * kFracFixedScale;
+    if (v > kFracCap) v = kFracCap;
+    if (v < -kFracCap) v = -kFracCap;
+    return (unsigned long long)(long long)v;
+}
 #pragma clang fp contract(on)
 
 }  // namespace pgd

@@ -183,6 +183,7 @@ struct Ctx {
     // sd-tree
     pgh::SdTree sd;
     DevBuf sd_snodes, sd_meta, sd_qnode, sd_bchild, sd_bsum, sd_count, sd_jump;  // sd_qnode: {energies, children}
+    DevBuf sd_frac;  // learned-fraction statistics, pgh::kFracStats u64 per leaf
     int sd_jump_bits = 0;
     PinnedBuf sd_stage;
     bool sd_dirty = true;
@@ -348,7 +349,10 @@ SDDev sdView(const Ctx *c) {
     s.bsum = c->sd_bsum.as<unsigned long long>();
     s.count = c->sd_count.as<unsigned long long>();
     s.jump = c->sd_jump.as<uint32_t>();
+    s.frac = c->sd_frac.as<unsigned long long>();
     s.jump_bits = c->sd_jump_bits;
+    s.learned = c->cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED ? 1 : 0;
+    s.alpha0 = c->cfg.bsdf_sampling_fraction;
     for (int a = 0; a < 3; ++a) s.lo[a] = c->sd.lo[a];
     s.extent = c->sd.extent;
     s.built = c->sd.built ? 1 : 0;
@@ -367,16 +371,18 @@ pg_status uploadSd(Ctx *c) {
     const pgh::SdTree &t = c->sd;
     const size_t R = (size_t)1 << pgh::SdTree::kJumpBits;
     const size_t nl = t.leaves.size(), ns = t.samplingNodes(), nb = t.buildingNodes();
-    DevBuf *dst[] = {&c->sd_snodes, &c->sd_meta, &c->sd_qnode, &c->sd_bchild, &c->sd_bsum, &c->sd_count, &c->sd_jump};
-    const size_t bytes[] = {4 * t.snode.size(), 16 * nl, 32 * ns, 16 * nb, 32 * nb, 8 * nl, 4 * R * R * R};
-    size_t off[8] = {0};
-    for (int k = 0; k < 7; ++k) off[k + 1] = off[k] + ((bytes[k] + 255) & ~(size_t)255);
-    HIPC(c, c->sd_stage.reserve(off[7]));
+    DevBuf *dst[] = {&c->sd_snodes, &c->sd_meta, &c->sd_qnode, &c->sd_bchild, &c->sd_bsum, &c->sd_count, &c->sd_jump,
+                     &c->sd_frac};
+    const size_t bytes[] = {4 * t.snode.size(), 16 * nl, 32 * ns, 16 * nb, 32 * nb, 8 * nl, 4 * R * R * R,
+                            8 * pgh::kFracStats * nl};
+    size_t off[9] = {0};
+    for (int k = 0; k < 8; ++k) off[k + 1] = off[k] + ((bytes[k] + 255) & ~(size_t)255);
+    HIPC(c, c->sd_stage.reserve(off[8]));
     uint8_t *h = (uint8_t *)c->sd_stage.p;
     t.flattenInto(pgh::SdTree::Layout{(uint32_t *)(h + off[0]), (uint32_t *)(h + off[1]), (uint32_t *)(h + off[2]),
                                       (uint32_t *)(h + off[3]), (uint64_t *)(h + off[4]), (uint64_t *)(h + off[5]),
-                                      (uint32_t *)(h + off[6])});
-    for (int k = 0; k < 7; ++k) {
+                                      (uint32_t *)(h + off[6]), (uint64_t *)(h + off[7])});
+    for (int k = 0; k < 8; ++k) {
         HIPC(c, dst[k]->grow(std::max<size_t>(bytes[k], 16)));
         if (bytes[k]) HIPC(c, hipMemcpyAsync(dst[k]->p, h + off[k], bytes[k], hipMemcpyHostToDevice, c->stream));
     }
@@ -391,16 +397,18 @@ pg_status uploadSd(Ctx *c) {
 // pull device-side building sums + counts into the host tree
 pg_status downloadSd(Ctx *c) {
     size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
-    const size_t sb = (32 * nb + 255) & ~(size_t)255;
-    HIPC(c, c->sd_stage.reserve(sb + 8 * nl));
+    const size_t sb = (32 * nb + 255) & ~(size_t)255, sc = (8 * nl + 255) & ~(size_t)255;
+    HIPC(c, c->sd_stage.reserve(sb + sc + 8 * pgh::kFracStats * nl));
     uint64_t *bsum = (uint64_t *)c->sd_stage.p;
     uint64_t *cnt = (uint64_t *)((uint8_t *)c->sd_stage.p + sb);
+    uint64_t *frac = (uint64_t *)((uint8_t *)c->sd_stage.p + sb + sc);
     HIPC(c, hipMemcpyAsync(bsum, c->sd_bsum.p, 32 * nb, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipMemcpyAsync(cnt, c->sd_count.p, 8 * nl, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipMemcpyAsync(frac, c->sd_frac.p, 8 * pgh::kFracStats * nl, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     std::vector<uint32_t> cnt32(nl);
     for (size_t i = 0; i < nl; ++i) cnt32[i] = (uint32_t)std::min<uint64_t>(cnt[i], 0xFFFFFFFFu);
-    c->sd.absorb(bsum, cnt32.data());
+    c->sd.absorb(bsum, cnt32.data(), frac);
     return PG_OK;
 }
 
@@ -454,7 +462,7 @@ pg_status ensurePaths(Ctx *c, uint32_t want, bool rec) {
         if (vslots > 0 && (vslots > l.vtx_slots || want > l.vtxP)) {
             const int vs = std::max(vslots, l.vtx_slots);
             const uint32_t vp = std::max(want, l.vtxP);
-            HIPC(c, l.vtx.alloc((size_t)vs * vp * 48));
+            HIPC(c, l.vtx.alloc((size_t)vs * vp * 16 * PG_VTX_F4));
             l.vtx_slots = vs;
             l.vtxP = vp;
         }
@@ -599,7 +607,7 @@ pg_status pg_config_default(pg_config *c) {
     c->path_lanes = 0;
     c->integrator = PG_INTEGRATOR_PATH;
     c->distance_guiding = 0.25f;
-    c->bsdf_fraction_bound = PG_FRACTION_ALBEDO;
+    c->bsdf_fraction_bound = PG_FRACTION_FIXED;
     c->kernel_timing = 0;
     return PG_OK;
 }
@@ -636,7 +644,7 @@ pg_status pg_create(const pg_config *cfg, void **out) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown integrator");
     }
-    if (c->cfg.bsdf_fraction_bound < PG_FRACTION_FIXED || c->cfg.bsdf_fraction_bound > PG_FRACTION_THROUGHPUT) {
+    if (c->cfg.bsdf_fraction_bound < PG_FRACTION_FIXED || c->cfg.bsdf_fraction_bound > PG_FRACTION_LEARNED) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: unknown bsdf_fraction_bound");
     }
@@ -1017,7 +1025,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     }
     const int maxV = std::min(std::max(c->cfg.record_max_vertices, 0), 64);
     if (rec && maxV > 0 && c->vol_vtx_cap < (uint64_t)want * maxV) {
-        HIPC(c, c->vol_vtx.alloc((size_t)want * maxV * 48));
+        HIPC(c, c->vol_vtx.alloc((size_t)want * maxV * 16 * PG_VTX_F4));
         c->vol_vtx_cap = (uint64_t)want * maxV;
     }
     if (!c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
@@ -1146,7 +1154,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
                     held += b->bytes;
             }
             const int vs = vertexSlots(c, rec);
-            const double perPath = 10.0 * 16 + (3 + PG_NUM_CLASSES) * 4.0 + vs * 48.0 + (c->cfg.aovs ? 16.0 : 0.0);
+            const double perPath = 10.0 * 16 + (3 + PG_NUM_CLASSES) * 4.0 + vs * 16.0 * PG_VTX_F4 + (c->cfg.aovs ? 16.0 : 0.0);
             const double fit = 0.7 * (double)(freeB + held) / (perPath * c->nlanes);
             if (fit < (double)cap) cap = std::max<uint32_t>(1u << 20, (uint32_t)fit & ~4095u);
         }
@@ -1552,7 +1560,8 @@ pg_status pg_refit(void *ctx, uint32_t iteration) {
     const auto t0 = std::chrono::steady_clock::now();
     if ((s = downloadSd(c))) return s;
     const auto t1 = std::chrono::steady_clock::now();
-    c->sd.refit(iteration, c->cfg.s_tree_threshold, c->cfg.d_tree_threshold, c->cfg.d_tree_max_depth);
+    c->sd.refit(iteration, c->cfg.s_tree_threshold, c->cfg.d_tree_threshold, c->cfg.d_tree_max_depth,
+                c->cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED);
     const auto t2 = std::chrono::steady_clock::now();
     if ((s = uploadSd(c))) return s;
     HIPC(c, hipMemsetAsync(c->rec_count.p, 0, 8, c->stream));
@@ -1574,12 +1583,13 @@ pg_status pg_get_tree_stats(void *ctx, void *dst, uint64_t capacity_words, int32
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_get_tree_stats: no scene");
     HIPC(c, hipSetDevice(c->cfg.device));
     const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
-    *words = 4 * nb + nl;
+    *words = 4 * nb + nl + pgh::kFracStats * nl;
     if (!dst) return PG_OK;
     if (capacity_words < *words) return fail(c, PG_ERR_INVALID, "pg_get_tree_stats: buffer too small");
     const hipMemcpyKind k = dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
     HIPC(c, hipMemcpyAsync(dst, c->sd_bsum.p, 32 * nb, k, c->stream));
     HIPC(c, hipMemcpyAsync((uint64_t *)dst + 4 * nb, c->sd_count.p, 8 * nl, k, c->stream));
+    HIPC(c, hipMemcpyAsync((uint64_t *)dst + 4 * nb + nl, c->sd_frac.p, 8 * pgh::kFracStats * nl, k, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }
@@ -1590,10 +1600,12 @@ pg_status pg_put_tree_stats(void *ctx, const void *src, uint64_t words, int32_t 
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_put_tree_stats: no scene");
     HIPC(c, hipSetDevice(c->cfg.device));
     const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
-    if (words != 4 * nb + nl) return fail(c, PG_ERR_INVALID, "pg_put_tree_stats: size does not match the tree");
+    if (words != 4 * nb + nl + pgh::kFracStats * nl)
+        return fail(c, PG_ERR_INVALID, "pg_put_tree_stats: size does not match the tree");
     const hipMemcpyKind k = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     HIPC(c, hipMemcpyAsync(c->sd_bsum.p, src, 32 * nb, k, c->stream));
     HIPC(c, hipMemcpyAsync(c->sd_count.p, (const uint64_t *)src + 4 * nb, 8 * nl, k, c->stream));
+    HIPC(c, hipMemcpyAsync(c->sd_frac.p, (const uint64_t *)src + 4 * nb + nl, 8 * pgh::kFracStats * nl, k, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }

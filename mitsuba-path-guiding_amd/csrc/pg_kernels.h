@@ -20,11 +20,14 @@ struct SceneDev {
     uint32_t top_nodes;     // binary-BVH nodes [0, top_nodes) are the top levels (k_trace stages them in LDS)
 };
 
+// float4 per training vertex: (x, woPdf), (T after the vertex, packed canonical wo), (L snapshot, -),
+// (T before the vertex, p_guide(wo) or -1 when the vertex was not guided)
+#define PG_VTX_F4 4
 struct PathDev {
     float4 *ray_o, *ray_d, *hit, *thr, *rad, *prev;
     uint4 *pinfo;
     float4 *sh_o, *sh_d, *sh_c;
-    float4 *vtx;       // [max_vertices][P][3]
+    float4 *vtx;       // [max_vertices][P][PG_VTX_F4]
     uint32_t *stack_ovf;  // traversal-stack overflow ring, pg_stack_overflow_words(0) words
     uint32_t P;        // path-state capacity
     uint32_t vtxP;     // slot stride of vtx (recording passes)
@@ -42,10 +45,13 @@ struct SDDev {
     unsigned long long *bsum;  // 4 per building node
     unsigned long long *count;  // records per D-tree (u64, so the building statistics are one u64 vector)
     const uint32_t *jump;      // S-tree jump grid, (2^jump_bits)^3 node ids
+    unsigned long long *frac;  // learned-fraction statistics, kFracStats (pg_sdtree.h) per D-tree
     float lo[3];
     float extent;
     int jump_bits;
     int built;
+    int learned;               // pg_config.bsdf_fraction_bound == PG_FRACTION_LEARNED
+    float alpha0;              // pg_config.bsdf_sampling_fraction: a leaf's fraction before it is learned
 };
 
 // Volumetric path tracing (pg_config.integrator == PG_INTEGRATOR_VOLPATH)
@@ -59,7 +65,7 @@ struct VolDev {
     uint32_t *next;            // work counter (zeroed by the launcher)
     unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries, [2] density lookups
     uint32_t *stack_ovf;       // pg_stack_overflow_words(0) words
-    float4 *vtx;               // guided training vertices [max_vertices][vtx_P][3] (PathDev::vtx layout)
+    float4 *vtx;               // guided training vertices [max_vertices][vtx_P][PG_VTX_F4] (PathDev::vtx layout)
     uint32_t vtx_P;            // slot stride of vtx (>= items per launch)
     float dist_beta;           // pg_config.distance_guiding
 };

@@ -207,7 +207,7 @@ __device__ __forceinline__ void shadowRows(const SceneDev &sc, const PathDev &p,
             stS(&p.rad[slot], make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w));
             uint32_t vi = __float_as_uint(c.w);
             if (vi != 0xFFFFFFFFu) {
-                float4 *vl = p.vtx + ((size_t)vi * p.vtxP + slot) * 3 + 2;
+                float4 *vl = p.vtx + ((size_t)vi * p.vtxP + slot) * PG_VTX_F4 + 2;
                 float4 a = *vl;
                 *vl = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w);
             }
@@ -323,8 +323,13 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
             const SDView sv = sdv(sd);
             uint4 meta = make_uint4(0, 0, 0, 0);
             if (guide) meta = sd.meta[sdLookup(sv, h.p)];
-            // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction)
-            const float alpha = guideFraction(g.fraction_bound, g.bsdf_fraction, M.wbound, maxc(T));
+            // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction):
+            // PG_FRACTION_LEARNED reads the leaf's learned fraction (meta.z; 0 = not learned yet)
+            const float leafAlpha = __uint_as_float(meta.z);
+            const float alpha = g.fraction_bound == PG_FRACTION_LEARNED ? (leafAlpha > 0 ? leafAlpha : g.bsdf_fraction)
+                                                                         : guideFraction(g.fraction_bound, g.bsdf_fraction,
+                                                                                         M.wbound, maxc(T));
+            float pgWo = -1.0f;  // p_guide of the sampled direction at a guided vertex (training record)
 
             // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow.  With
             // guiding, the D-tree pdf of the light direction is resolved below, in one lockstep walk
@@ -382,6 +387,7 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
                     if (neePending) dirToCanonical(neeD, au, aw);
                     sdDual(sv, meta, neePending, au, aw, aPdf, mode != 0, mode == 2, bu, bw, cu, cv, dPdf);
                     if (neePending) neeC = neeV * miWeight(neeEmPdf, alpha * neeBp + (1 - alpha) * aPdf);
+                    pgWo = dPdf;
                     if (mode == 1) {
                         woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
                         weight = weight * (bs.pdf / woPdf);
@@ -415,10 +421,11 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
                     if (g.record && !(bs.type & EDelta) && nv < (uint32_t)g.max_vertices) {
                         float cu, cv;
                         dirToCanonical(wo, cu, cv);
-                        float4 *vb = p.vtx + ((size_t)nv * p.vtxP + slot) * 3;
+                        float4 *vb = p.vtx + ((size_t)nv * p.vtxP + slot) * PG_VTX_F4;
                         stS(vb + 0, f4(h.p, woPdf));
                         stS(vb + 1, f4(Tn, __uint_as_float(packCanonical(cu, cv))));
                         stS(vb + 2, f4(L, 0.0f));
+                        stS(vb + 3, f4(T, guide ? pgWo : -1.0f));
                         vtxIndex = nv;
                         nv++;
                     }
@@ -549,12 +556,16 @@ __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int 
     if (env_hits) L = envHitRadiance(L, p.hit[slot]);
     for (uint32_t k = 0; k < nv; ++k, ++o) {
         if (o >= capacity) return;
-        const float4 *vb = p.vtx + ((size_t)k * p.vtxP + slot) * 3;
-        float4 a = vb[0], b = vb[1], c = vb[2];
+        const float4 *vb = p.vtx + ((size_t)k * p.vtxP + slot) * PG_VTX_F4;
+        float4 a = vb[0], b = vb[1], c = vb[2], e = vb[3];
         float woPdf = a.w;
         float lr = (b.x * woPdf > 1e-4f) ? (L.x - c.x) / b.x : 0.0f;
         float lg = (b.y * woPdf > 1e-4f) ? (L.y - c.y) / b.y : 0.0f;
         float lb = (b.z * woPdf > 1e-4f) ? (L.z - c.z) / b.z : 0.0f;
+        // f L_i / woPdf per channel = (L_final - L_snapshot) / T_before (oracle: the same guards)
+        float wr = (b.x * woPdf > 1e-4f) ? (L.x - c.x) / e.x : 0.0f;
+        float wg = (b.y * woPdf > 1e-4f) ? (L.y - c.y) / e.y : 0.0f;
+        float wb = (b.z * woPdf > 1e-4f) ? (L.z - c.z) / e.z : 0.0f;
         pg_record r;
         r.pos[0] = a.x;
         r.pos[1] = a.y;
@@ -562,8 +573,8 @@ __global__ __launch_bounds__(256) void k_commit(PathDev p, uint32_t nslots, int 
         r.dir = __float_as_uint(b.w);
         r.radiance = (lr + lg + lb) * (1.0f / 3.0f);
         r.wo_pdf = woPdf;
-        r.product = 0.0f;
-        r.weight = 1.0f;
+        r.product = e.w >= 0.0f ? (wr + wg + wb) * (1.0f / 3.0f) : 0.0f;
+        r.weight = e.w;
         float4 *dst = reinterpret_cast<float4 *>(recs + o);
         dst[0] = make_float4(r.pos[0], r.pos[1], r.pos[2], __uint_as_float(r.dir));
         dst[1] = make_float4(r.radiance, r.wo_pdf, r.product, r.weight);
@@ -587,6 +598,28 @@ __device__ __forceinline__ void waveKeyedAdd(T *base, uint32_t key, T v, bool va
         T sum = mine ? v : (T)0;
         for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
         if (lane == leader) atomicAdd(base + k, sum);
+        pending &= ~m;
+    }
+}
+
+// the learned-fraction statistics of a wave's guided records: per group of lanes with one D-tree,
+// kFracCandidates wave-summed fixed-point values and the group's record count, added by its leader
+__device__ __forceinline__ void waveKeyedFracAdd(unsigned long long *base, uint32_t key, float w, float pb, float pg,
+                                                 float q0, bool valid) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long pending = __ballot(valid);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const uint32_t k = __shfl(key, leader);
+        const bool mine = valid && key == k;
+        const unsigned long long m = __ballot(mine);
+        unsigned long long *dst = base + (size_t)k * (kFracCandidates + 1);
+        for (int c = 0; c < kFracCandidates; ++c) {
+            unsigned long long v = mine ? fracStat(w, pb, pg, q0, c) : 0ull;
+            for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+            if (lane == leader) atomicAdd(dst + c, v);
+        }
+        if (lane == leader) atomicAdd(dst + kFracCandidates, (unsigned long long)__popcll(m));
         pending &= ~m;
     }
 }
@@ -633,6 +666,26 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
     }
     waveKeyedAdd<unsigned long long>(sd.count, dt, 1ull, valid);
     waveKeyedAdd<unsigned long long>(sd.bsum, slot, fx, found);
+    if (!sd.learned) return;
+    // learned BSDF-sampling fraction (pg_device.h fracStat): a guided record (weight = p_guide >= 0)
+    // with a contribution adds w log2(q_k / q0) for every candidate k, and 1 to its guided count.  p_bsdf
+    // comes back from q0 = a0 p_bsdf + (1 - a0) p_guide with a0 the leaf's fraction that sampled it.
+    bool stat = false;
+    float w = 0, pb = 0, pg = 0, q0 = 0;
+    if (valid) {
+        const float4 b = reinterpret_cast<const float4 *>(recs + i)[1];
+        pg = b.w;
+        w = b.z;
+        q0 = b.y;
+        if (pg >= 0.0f && w > 0.0f && w < 1e30f) {
+#pragma clang fp contract(off)
+            const float la = __uint_as_float(sd.meta[dt].z);
+            const float a0 = la > 0 ? la : sd.alpha0;
+            pb = fmaxf((q0 - (1.0f - a0) * pg) / a0, 0.0f);
+            stat = true;
+        }
+    }
+    waveKeyedFracAdd(sd.frac, dt, w, pb, pg, q0, stat);
 }
 
 // ---- unit-level kernels used by the parity tests ---------------------------------------------

@@ -91,6 +91,7 @@ void rebuildTopology(SdLeaf &L, int maxDepth, float rho) {
     for (size_t i = 0; i < nodes.size(); ++i)
         for (int q = 0; q < 4; ++q) L.building[i].child[q] = nodes[i].c[q];
     L.count = 0;
+    for (uint64_t &f : L.frac) f = 0;
 }
 
 }  // namespace
@@ -104,10 +105,18 @@ void SdTree::reset(const float bmin[3], const float bmax[3]) {
     built = false;
 }
 
-void SdTree::refit(uint32_t iteration, float sThreshold, float rho, int maxDepth) {
-    // 1. build: building -> sampling (fp32 from the exact integer sums)
+void SdTree::refit(uint32_t iteration, float sThreshold, float rho, int maxDepth, bool learn) {
+    // 1. build: building -> sampling (fp32 from the exact integer sums); the learned fraction: the
+    //    candidate of the largest cross-entropy estimate (ties: the larger fraction) when the leaf saw
+    //    enough guided records (pg_device.h fracStat; oracle SDTree::learnedFraction)
     parallelFor(leaves.size(), [&](size_t li) {
         SdLeaf &L = leaves[li];
+        if (learn && L.frac[kFracCandidates] >= kFracMinRecords) {
+            int best = 0;
+            for (int k = 1; k < kFracCandidates; ++k)
+                if ((int64_t)L.frac[k] >= (int64_t)L.frac[best]) best = k;
+            L.alpha = fracCandidate(best);
+        }
         propagate(L.building, 0);
         L.sampling.assign(L.building.size(), SdNodeS{});
         for (size_t i = 0; i < L.building.size(); ++i)
@@ -199,8 +208,9 @@ void SdTree::flattenInto(const Layout &d) const {
         const uint32_t sb = sbase[i], bb = bbase[i];
         d.meta[4 * i + 0] = sb;
         d.meta[4 * i + 1] = bb;
-        d.meta[4 * i + 2] = L.count;
+        std::memcpy(&d.meta[4 * i + 2], &L.alpha, 4);
         std::memcpy(&d.meta[4 * i + 3], &L.total, 4);
+        for (int k = 0; k < kFracStats; ++k) d.frac[(size_t)kFracStats * i + k] = L.frac[k];
         for (size_t k = 0; k < L.sampling.size(); ++k) {
             uint32_t *q = d.qnode + 8 * (sb + k);
             std::memcpy(q, L.sampling[k].sum, 16);
@@ -224,11 +234,12 @@ void SdTree::flatten(Flat &f) const {
     f.bsum.resize(4 * buildingNodes());
     f.count.resize(leaves.size());
     f.jump.resize(R * R * R);
+    f.frac.resize((size_t)kFracStats * leaves.size());
     flattenInto(Layout{f.snodes.data(), f.meta.data(), f.qnode.data(), f.bchild.data(), f.bsum.data(), f.count.data(),
-                       f.jump.data()});
+                       f.jump.data(), f.frac.data()});
 }
 
-void SdTree::absorb(const uint64_t *bsum, const uint32_t *count) {
+void SdTree::absorb(const uint64_t *bsum, const uint32_t *count, const uint64_t *frac) {
     std::vector<size_t> bbase(leaves.size());
     for (size_t i = 0, bb = 0; i < leaves.size(); ++i) {
         bbase[i] = bb;
@@ -239,24 +250,27 @@ void SdTree::absorb(const uint64_t *bsum, const uint32_t *count) {
         for (size_t k = 0; k < L.building.size(); ++k)
             for (int q = 0; q < 4; ++q) L.building[k].sum[q] = bsum[4 * (bbase[i] + k) + q];
         L.count = count[i];
+        for (int k = 0; k < kFracStats; ++k) L.frac[k] = frac[(size_t)kFracStats * i + k];
     });
 }
 
 // Wire format (little endian), shared with the oracle's golden vectors:
-//   u32 magic 'PGSD', u32 version 1, u32 built, u32 0
+//   u32 magic 'PGSD', u32 version 2, u32 built, u32 0
 //   f32 lo.xyz, 0, hi.xyz, 0            (cube)
 //   u32 num_snodes, num_dtrees, num_sampling_nodes, num_building_nodes
 //   num_snodes x {u32 child0, u32 child1}
-//   num_dtrees x {u32 sampling_base, building_base, sampling_count, building_count, f32 total, u32 count, 0, 0}
+//   num_dtrees x {u32 sampling_base, building_base, sampling_count, building_count, f32 total, u32 count,
+//                 f32 alpha (learned BSDF-sampling fraction, 0 = none), 0}
 //   sampling nodes x {f32 sum[4], u32 child[4] (absolute, 0 = leaf)}
 //   building nodes x {u64 sum[4], u32 child[4] (absolute, 0 = leaf)}
+//   num_dtrees x {u64 frac[kFracStats]}  (learned-fraction building statistics)
 std::vector<uint8_t> SdTree::serialize() const {
     std::vector<uint8_t> out;
     auto put = [&](const void *p, size_t n) {
         const uint8_t *b = (const uint8_t *)p;
         out.insert(out.end(), b, b + n);
     };
-    uint32_t hdr[4] = {kMagic, 1u, built ? 1u : 0u, 0u};
+    uint32_t hdr[4] = {kMagic, 2u, built ? 1u : 0u, 0u};
     put(hdr, 16);
     float box[8] = {lo[0], lo[1], lo[2], extent, lo[0] + extent, lo[1] + extent, lo[2] + extent, 0};
     put(box, 32);
@@ -268,7 +282,7 @@ std::vector<uint8_t> SdTree::serialize() const {
     put(snode.data(), 4 * snode.size());
     for (size_t i = 0; i < leaves.size(); ++i) {
         uint32_t m[8] = {f.meta[4 * i], f.meta[4 * i + 1], (uint32_t)leaves[i].sampling.size(),
-                         (uint32_t)leaves[i].building.size(), f.meta[4 * i + 3], leaves[i].count, 0, 0};
+                         (uint32_t)leaves[i].building.size(), f.meta[4 * i + 3], leaves[i].count, f.meta[4 * i + 2], 0};
         put(m, 32);
     }
     put(f.qnode.data(), 4 * f.qnode.size());  // {f32 sum[4], u32 child[4]} per node
@@ -276,6 +290,7 @@ std::vector<uint8_t> SdTree::serialize() const {
         put(&f.bsum[4 * k], 32);
         put(&f.bchild[4 * k], 16);
     }
+    put(f.frac.data(), 8 * f.frac.size());
     return out;
 }
 
@@ -289,7 +304,7 @@ bool SdTree::deserialize(const uint8_t *p, size_t n) {
     };
     uint32_t hdr[4], cnt[4];
     float box[8];
-    if (!get(hdr, 16) || hdr[0] != kMagic || hdr[1] != 1 || !get(box, 32) || !get(cnt, 16)) return false;
+    if (!get(hdr, 16) || hdr[0] != kMagic || hdr[1] != 2 || !get(box, 32) || !get(cnt, 16)) return false;
     built = hdr[2] != 0;
     for (int a = 0; a < 3; ++a) lo[a] = box[a];
     extent = box[3];
@@ -306,6 +321,7 @@ bool SdTree::deserialize(const uint8_t *p, size_t n) {
         leaves[i].building.assign(m[3], SdNodeB{});
         std::memcpy(&leaves[i].total, &m[4], 4);
         leaves[i].count = m[5];
+        std::memcpy(&leaves[i].alpha, &m[6], 4);
     }
     for (uint32_t i = 0; i < cnt[1]; ++i)
         for (auto &nd : leaves[i].sampling) {
@@ -319,6 +335,8 @@ bool SdTree::deserialize(const uint8_t *p, size_t n) {
             for (int q = 0; q < 4; ++q)
                 if (nd.child[q]) nd.child[q] -= bb[i];
         }
+    for (uint32_t i = 0; i < cnt[1]; ++i)
+        if (!get(leaves[i].frac, 8 * kFracStats)) return false;
     return off == n;
 }
 

@@ -20,11 +20,20 @@ struct SdNodeB {  // building quadtree node
     uint64_t sum[4] = {0, 0, 0, 0};    // 2^-24 fixed point
     uint32_t child[4] = {0, 0, 0, 0};
 };
+// learned BSDF-sampling fraction (PG_FRACTION_LEARNED, pg_device.h fracStat): candidates and the
+// number of u64 statistics per leaf (one cross-entropy sum per candidate + the guided-record count)
+constexpr int kFracCandidates = 10;
+constexpr int kFracStats = kFracCandidates + 1;
+constexpr uint64_t kFracMinRecords = 64;  // fewer guided records: the leaf keeps its fraction
+inline float fracCandidate(int k) { return 0.05f + 0.1f * (float)k; }
+
 struct SdLeaf {  // D-tree pair attached to one S-tree leaf
     std::vector<SdNodeS> sampling{SdNodeS{}};
     float total = 0;
+    float alpha = 0;  // learned BSDF-sampling fraction (0: not learned, pg_config.bsdf_sampling_fraction)
     std::vector<SdNodeB> building{SdNodeB{}};
     uint32_t count = 0;
+    uint64_t frac[kFracStats] = {};  // building statistics of the fraction (two's complement sums)
 };
 
 struct SdTree {
@@ -34,7 +43,8 @@ struct SdTree {
     bool built = false;
 
     void reset(const float bmin[3], const float bmax[3]);
-    void refit(uint32_t iteration, float s_threshold, float rho, int max_depth);
+    // learn: pick each leaf's BSDF-sampling fraction from its statistics (PG_FRACTION_LEARNED)
+    void refit(uint32_t iteration, float s_threshold, float rho, int max_depth, bool learn = false);
     std::vector<uint8_t> serialize() const;
     bool deserialize(const uint8_t *p, size_t n);
 
@@ -42,22 +52,23 @@ struct SdTree {
     static constexpr int kJumpBits = 6;
     struct Layout {
         uint32_t *snodes;  // 2 per S-tree node
-        uint32_t *meta;    // 4 per leaf: sampling base, building base, count, bits(total)
+        uint32_t *meta;    // 4 per leaf: sampling base, building base, bits(alpha), bits(total)
         uint32_t *qnode;   // 8 per sampling node: f32 sum[4], u32 child[4] (absolute, 0 = leaf)
         uint32_t *bchild;  // 4 per building node (absolute)
         uint64_t *bsum;    // 4 per building node
         uint64_t *count;   // per leaf
         uint32_t *jump;    // (2^kJumpBits)^3 S-tree node ids, index (z * R + y) * R + x
+        uint64_t *frac;    // kFracStats per leaf
     };
     void flattenInto(const Layout &d) const;
     // the same layout in owned arrays (wire format, tests)
     struct Flat {
         std::vector<uint32_t> snodes, meta, qnode, bchild, jump;
-        std::vector<uint64_t> bsum, count;
+        std::vector<uint64_t> bsum, count, frac;
     };
     void flatten(Flat &f) const;
-    // absorb device-side building sums/counts (same absolute layout as flatten())
-    void absorb(const uint64_t *bsum, const uint32_t *count);
+    // absorb device-side building sums/counts/fraction statistics (same absolute layout as flatten())
+    void absorb(const uint64_t *bsum, const uint32_t *count, const uint64_t *frac);
     size_t samplingNodes() const;
     size_t buildingNodes() const;
 };

@@ -494,15 +494,17 @@ struct VPath {
     uint32_t nv;  // training vertices written (GUIDED with g.record)
 };
 
-// training vertex nv of this item: (x, woPdf), (T after the bounce, packed canonical wo), (L snapshot)
+// training vertex nv of this item: (x, woPdf), (T after the bounce, packed canonical wo), (L snapshot),
+// (-, -1: no learned-fraction statistics from the volumetric path)
 __device__ __forceinline__ void writeVertex(const VolDev &v, uint32_t item, uint32_t k, f3 x, f3 wo, float woPdf, f3 Tn,
                                             f3 L) {
     float cu, cv;
     dirToCanonical(wo, cu, cv);
-    float4 *vb = v.vtx + ((size_t)k * v.vtx_P + item) * 3;
+    float4 *vb = v.vtx + ((size_t)k * v.vtx_P + item) * PG_VTX_F4;
     vb[0] = f4(x, woPdf);
     vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
     vb[2] = f4(L, 0.0f);
+    vb[3] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
 }
 
 // one iteration of the Li loop; false when the path ends.  GUIDED: SD-tree guiding at medium and

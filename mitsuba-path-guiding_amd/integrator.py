@@ -44,7 +44,7 @@ def _p(a):
 
 
 _FRACTION_BOUNDS = {"fixed": capi.PG_FRACTION_FIXED, "albedo": capi.PG_FRACTION_ALBEDO,
-                    "throughput": capi.PG_FRACTION_THROUGHPUT}
+                    "throughput": capi.PG_FRACTION_THROUGHPUT, "learned": capi.PG_FRACTION_LEARNED}
 
 
 class PGError(RuntimeError):
@@ -321,7 +321,7 @@ class ProgressivePathTracer:
             path_lanes=int(props.get("pathLanes", 0)),
             distance_guiding=float(props.get("distanceGuiding", 0.25)),
             aovs=int(bool(props.get("aovs", False))),
-            bsdf_fraction_bound=_FRACTION_BOUNDS[str(props.get("bsdfSamplingFractionBound", "albedo")).lower()])
+            bsdf_fraction_bound=_FRACTION_BOUNDS[str(props.get("bsdfSamplingFractionBound", "fixed")).lower()])
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         # maxRenderTime (progressiveintegrator.cpp:296-300): > 0 renders whole progressions until this
         # many seconds have passed (renderTime, :117-168); rendered_spp / render_seconds report the

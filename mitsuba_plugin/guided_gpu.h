@@ -50,9 +50,9 @@ public:
         m_cfg.d_tree_threshold = props.getFloat("dTreeThreshold", 0.01f);
         m_cfg.distance_guiding = props.getFloat("distanceGuiding", m_cfg.distance_guiding);  // volpath only
         m_cfg.aovs = props.getBoolean("aovs", false);
-        std::string bound = boost::to_lower_copy(props.getString("bsdfSamplingFractionBound", "albedo"));
-        m_cfg.bsdf_fraction_bound = bound == "fixed" ? PG_FRACTION_FIXED
-                                    : bound == "throughput" ? PG_FRACTION_THROUGHPUT : PG_FRACTION_ALBEDO;
+        std::string bound = boost::to_lower_copy(props.getString("bsdfSamplingFractionBound", "fixed"));
+        m_cfg.bsdf_fraction_bound = bound == "albedo" ? PG_FRACTION_ALBEDO : bound == "learned" ? PG_FRACTION_LEARNED
+                                    : bound == "throughput" ? PG_FRACTION_THROUGHPUT : PG_FRACTION_FIXED;
         // multi-GPU: one Mitsuba process per GPU (e.g. mitsuba -Drank=2 -DworldSize=8 scene.xml); the
         // context renders its 32x32 tile shard, rank 0 writes the whole image
         m_cfg.rank = props.getInteger("rank", 0);

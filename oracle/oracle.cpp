@@ -44,7 +44,8 @@ inline float guideFraction(int mode, float alpha, const Material &M, float maxT)
 struct Vtx {
     V3 p, dir, T, Lat;
     float woPdf;
-    float product;
+    V3 Tpre;    // throughput before the vertex (learned fraction: w = f L_i / woPdf = dL / Tpre)
+    float pg;   // p_guide(dir) at a guided vertex, -1 otherwise
 };
 
 struct Counters {
@@ -83,7 +84,10 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
         V3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? its.sh.n : V3(0.f);
         const bool guidable = guiding && (M.type & ESmooth) && !(M.type & EDelta);
         const DTreeW *dt = guidable ? &tree->dtrees[tree->lookup(its.p)] : nullptr;
-        const float alpha = guideFraction(cfg.bsdf_fraction_bound, cfg.bsdf_sampling_fraction, M, maxc(T));
+        const float alpha = cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED
+                                ? ((dt && dt->alpha > 0) ? dt->alpha : cfg.bsdf_sampling_fraction)
+                                : guideFraction(cfg.bsdf_fraction_bound, cfg.bsdf_sampling_fraction, M, maxc(T));
+        float pgWo = -1.0f;  // p_guide of the sampled direction (guided vertex)
 
         // ---- direct illumination (NEE)
         if (cfg.use_nee && (M.type & ESmooth)) {
@@ -125,6 +129,7 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                     float dPdf = SDTree::pdfDir(*dt, its.toWorld(bs.wo));
                     woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
                     weight = weight * (bs.pdf / woPdf);
+                    pgWo = dPdf;
                 } else {
                     float g0, g1, dPdf;
                     rng.next2(dimOf(depth, SLOT_GUIDE), g0, g1);
@@ -135,6 +140,7 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                     woPdf = alpha * bp + (1 - alpha) * dPdf;
                     if (!(woPdf > 0) || isZero(f)) break;
                     weight = f / woPdf;
+                    pgWo = dPdf;
                     bs.wo = woL;
                     bs.pdf = bp;
                     bool refl = its.wi.z * woL.z > 0;
@@ -157,6 +163,8 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
             vtx[nv].T = T * weight;
             vtx[nv].Lat = L;
             vtx[nv].woPdf = woPdf;
+            vtx[nv].Tpre = T;
+            vtx[nv].pg = dt ? pgWo : -1.0f;
             nv++;
         }
 
@@ -201,9 +209,11 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
     if (recs) {
         for (int i = 0; i < nv; ++i) {
             const Vtx &v = vtx[i];
-            V3 loc;
-            for (int c = 0; c < 3; ++c)
+            V3 loc, wl;
+            for (int c = 0; c < 3; ++c) {
                 loc[c] = (v.T[c] * v.woPdf > 1e-4f) ? (L[c] - v.Lat[c]) / v.T[c] : 0.0f;
+                wl[c] = (v.T[c] * v.woPdf > 1e-4f) ? (L[c] - v.Lat[c]) / v.Tpre[c] : 0.0f;
+            }
             pg_record r;
             r.pos[0] = v.p.x;
             r.pos[1] = v.p.y;
@@ -213,8 +223,8 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
             r.dir = packCanonical(cu, cv);
             r.radiance = avg(loc);
             r.wo_pdf = v.woPdf;
-            r.product = 0.0f;
-            r.weight = 1.0f;
+            r.product = v.pg >= 0.0f ? avg(wl) : 0.0f;
+            r.weight = v.pg;
             recs->push_back(r);
         }
         cnt.records += (uint64_t)nv;
@@ -255,6 +265,10 @@ int oracle_render(void *sp, const pg_config *cfg, void *tp, uint32_t spp, uint32
                   const uint32_t *pixels, uint64_t npix, int32_t nthreads, float *rgbw, float *sumsq, uint64_t *stats) {
     const Scene &S = *(const Scene *)sp;
     SDTree *tree = (SDTree *)tp;
+    if (tree && record) {  // the splat of these records gathers learned-fraction statistics (orc_sdtree.h)
+        tree->learned = cfg->bsdf_fraction_bound == PG_FRACTION_LEARNED;
+        tree->alpha0 = cfg->bsdf_sampling_fraction;
+    }
     const uint32_t W = S.cam.W, H = S.cam.H;
     if (!pixels) npix = (uint64_t)W * H;
     if (nthreads <= 0) nthreads = oracle_hardware_threads();
@@ -346,6 +360,11 @@ void oracle_sdtree_splat_pending(void *tp) {
     SDTree *t = (SDTree *)tp;
     t->splat(t->pending.data(), t->pending.size());
     t->pending.clear();
+}
+// the learned BSDF-sampling fraction (PG_FRACTION_LEARNED): splat gathers its statistics, refit learns
+void oracle_sdtree_configure(void *tp, int32_t learned, float alpha0) {
+    ((SDTree *)tp)->learned = learned != 0;
+    ((SDTree *)tp)->alpha0 = alpha0;
 }
 void oracle_sdtree_refit(void *tp, uint32_t iter, float sthr, float rho, int32_t maxDepth) {
     ((SDTree *)tp)->refit(iter, sthr, rho, maxDepth);

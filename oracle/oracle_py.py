@@ -40,6 +40,7 @@ def lib(capi):
             "oracle_sdtree_splat": (None, [VP, VP, C.c_uint64]),
             "oracle_sdtree_splat_pending": (None, [VP]),
             "oracle_sdtree_refit": (None, [VP, C.c_uint32, C.c_float, C.c_float, C.c_int32]),
+            "oracle_sdtree_configure": (None, [VP, C.c_int32, C.c_float]),
             "oracle_sdtree_serialize": (C.c_uint64, [VP, VP, C.c_uint64]),
             "oracle_sdtree_deserialize": (C.c_int, [VP, VP, C.c_uint64]),
             "oracle_sdtree_pdf": (None, [VP, VP, VP, C.c_uint64, VP]),
@@ -154,7 +155,14 @@ class OracleSDTree:
     def splat_pending(self):
         self.L.oracle_sdtree_splat_pending(self.h)
 
+    def configure(self, cfg):
+        """Learned BSDF-sampling fraction on or off (cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED), as the
+        device context does: the splat gathers its statistics, the refit learns.  render(record=True) and
+        refit() call it; call it before splatting records that did not come from this oracle."""
+        self.L.oracle_sdtree_configure(self.h, int(cfg.bsdf_fraction_bound == 3), cfg.bsdf_sampling_fraction)
+
     def refit(self, it, cfg):
+        self.configure(cfg)
         self.L.oracle_sdtree_refit(self.h, it, cfg.s_tree_threshold, cfg.d_tree_threshold, cfg.d_tree_max_depth)
 
     def serialize(self):

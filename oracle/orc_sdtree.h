@@ -43,11 +43,48 @@ struct BNode {  // building node
     uint64_t sum[4] = {0, 0, 0, 0};
     uint32_t child[4] = {0, 0, 0, 0};
 };
+// ---- learned BSDF-sampling fraction per S-tree leaf (PG_FRACTION_LEARNED; kernels: pg_device.h
+// fracStat, k_splat, pg_sdtree.cpp refit).  After Mueller 2019 ("Practical Path Guiding in
+// Production": the selection probability optimised per spatial cell against the KL divergence from
+// f * L_i), restated as a batch choice: every training iteration estimates the cross-entropy
+// E_{p*}[log2 q_k] of the candidate mixtures q_k = a_k p_bsdf + (1 - a_k) p_guide, a_k = 0.05 + 0.1 k,
+// from its guided records with importance weights w = f L_i / q0, as 2^-16 fixed-point sums; the
+// refit keeps the candidate with the largest sum (ties: the larger fraction) once a leaf has 64 guided
+// records.  No libm: pgLog2 is a fixed polynomial, bit-identical with the device.
+constexpr int kFracCandidates = 10;
+constexpr int kFracStats = kFracCandidates + 1;
+constexpr uint64_t kFracMinRecords = 64;
+constexpr float kFracFixedScale = 65536.0f;
+constexpr float kFracCap = 70368744177664.0f;  // 2^46
+inline float fracCandidate(int k) { return 0.05f + 0.1f * (float)k; }
+inline float pgLog2(float x) {
+    if (!(x > 1.17549435e-38f)) return -126.0f;
+    uint32_t b;
+    std::memcpy(&b, &x, 4);
+    const float e = (float)((int)((b >> 23) & 0xFFu) - 127);
+    const uint32_t mb = (b & 0x7FFFFFu) | 0x3F800000u;
+    float m;
+    std::memcpy(&m, &mb, 4);
+    const float t = (m - 1.0f) / (m + 1.0f), t2 = t * t;
+    const float s = t * (1.0f + t2 * (0.333333343f + t2 * (0.2f + t2 * (0.142857149f + t2 * 0.111111112f))));
+    return e + s * 2.88539004f;
+}
+inline uint64_t fracStat(float w, float pb, float pg, float q0, int k) {
+    const float a = fracCandidate(k);
+    const float qk = a * pb + (1.0f - a) * pg;
+    float v = w * pgLog2(qk / q0) * kFracFixedScale;
+    if (v > kFracCap) v = kFracCap;
+    if (v < -kFracCap) v = -kFracCap;
+    return (uint64_t)(int64_t)v;
+}
+
 struct DTreeW {
     std::vector<QNode> sampling{QNode{}};
     float samplingTotal = 0;
+    float alpha = 0;  // learned fraction (0: not learned, pg_config.bsdf_sampling_fraction)
     std::vector<BNode> building{BNode{}};
     uint32_t count = 0;
+    uint64_t frac[kFracStats] = {};
 };
 
 inline void dirToCanonical(V3 d, float &u, float &v) {
@@ -225,6 +262,8 @@ struct SDTree {
         fixed = (uint64_t)s;
         return true;
     }
+    bool learned = false;  // PG_FRACTION_LEARNED: splat also gathers the fraction statistics
+    float alpha0 = 0.5f;   // pg_config.bsdf_sampling_fraction
     void splat(const pg_record *recs, size_t n) {
         for (size_t i = 0; i < n; ++i) {
             const pg_record &r = recs[i];
@@ -232,6 +271,12 @@ struct SDTree {
             if (!recordValue(r, fx)) continue;
             DTreeW &dt = dtrees[lookup(V3(r.pos[0], r.pos[1], r.pos[2]))];
             dt.count += 1;
+            if (learned && r.weight >= 0.0f && r.product > 0.0f && r.product < 1e30f) {
+                const float a0 = dt.alpha > 0 ? dt.alpha : alpha0;
+                const float pb = std::max((r.wo_pdf - (1.0f - a0) * r.weight) / a0, 0.0f);
+                for (int k = 0; k < kFracCandidates; ++k) dt.frac[k] += fracStat(r.product, pb, r.weight, r.wo_pdf, k);
+                dt.frac[kFracCandidates] += 1;
+            }
             float u, v;
             unpackCanonical(r.dir, u, v);
             uint32_t nidx = 0;
@@ -288,11 +333,18 @@ struct SDTree {
         for (size_t i = 0; i < tmp.size(); ++i)
             for (int q = 0; q < 4; ++q) dt.building[i].child[q] = tmp[i].child[q];
         dt.count = 0;
+        for (uint64_t &f : dt.frac) f = 0;
     }
 
     void refit(uint32_t iter, float sThreshold, float rho, int maxDepth) {
-        // 1. build: building -> sampling
+        // 1. build: building -> sampling; the learned fraction from this iteration's statistics
         for (auto &dt : dtrees) {
+            if (learned && dt.frac[kFracCandidates] >= kFracMinRecords) {
+                int best = 0;
+                for (int k = 1; k < kFracCandidates; ++k)
+                    if ((int64_t)dt.frac[k] >= (int64_t)dt.frac[best]) best = k;
+                dt.alpha = fracCandidate(best);
+            }
             buildSums(dt.building, 0);
             dt.sampling.assign(dt.building.size(), QNode{});
             for (size_t i = 0; i < dt.building.size(); ++i)
@@ -341,7 +393,7 @@ struct SDTree {
             nsamp += (uint32_t)dt.sampling.size();
             nbuild += (uint32_t)dt.building.size();
         }
-        uint32_t hdr[4] = {kSdMagic, 1u, built ? 1u : 0u, 0u};
+        uint32_t hdr[4] = {kSdMagic, 2u, built ? 1u : 0u, 0u};
         put(hdr, sizeof hdr);
         float box[8] = {lo.x, lo.y, lo.z, extent, hi.x, hi.y, hi.z, 0};
         put(box, sizeof box);
@@ -352,6 +404,7 @@ struct SDTree {
         for (auto &dt : dtrees) {
             uint32_t meta[8] = {sbase, bbase, (uint32_t)dt.sampling.size(), (uint32_t)dt.building.size(), 0, dt.count, 0, 0};
             std::memcpy(&meta[4], &dt.samplingTotal, 4);
+            std::memcpy(&meta[6], &dt.alpha, 4);
             put(meta, sizeof meta);
             sbase += (uint32_t)dt.sampling.size();
             bbase += (uint32_t)dt.building.size();
@@ -376,6 +429,7 @@ struct SDTree {
             }
             bbase += (uint32_t)dt.building.size();
         }
+        for (auto &dt : dtrees) put(dt.frac, 8 * kFracStats);
         return out;
     }
     bool deserialize(const uint8_t *p, size_t n) {
@@ -389,7 +443,7 @@ struct SDTree {
         uint32_t hdr[4];
         float box[8];
         uint32_t cnt[4];
-        if (!get(hdr, 16) || hdr[0] != kSdMagic || !get(box, 32) || !get(cnt, 16)) return false;
+        if (!get(hdr, 16) || hdr[0] != kSdMagic || hdr[1] != 2 || !get(box, 32) || !get(cnt, 16)) return false;
         built = hdr[2] != 0;
         lo = V3(box[0], box[1], box[2]);
         extent = box[3];
@@ -408,6 +462,7 @@ struct SDTree {
             dtrees[i].building.resize(meta[3]);
             std::memcpy(&dtrees[i].samplingTotal, &meta[4], 4);
             dtrees[i].count = meta[5];
+            std::memcpy(&dtrees[i].alpha, &meta[6], 4);
         }
         for (uint32_t i = 0; i < cnt[1]; ++i)
             for (auto &nd : dtrees[i].sampling) {
@@ -421,6 +476,8 @@ struct SDTree {
                 for (int q = 0; q < 4; ++q)
                     if (nd.child[q]) nd.child[q] -= bb[i];
             }
+        for (uint32_t i = 0; i < cnt[1]; ++i)
+            if (!get(dtrees[i].frac, 8 * kFracStats)) return false;
         return off == n;
     }
 };

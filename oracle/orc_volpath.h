@@ -393,7 +393,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
             r.radiance = avg(loc);
             r.wo_pdf = v.woPdf;
             r.product = 0.0f;
-            r.weight = 1.0f;
+            r.weight = -1.0f;  // no learned-fraction statistics from the volumetric path
             recs->push_back(r);
         }
         cnt.records += (uint64_t)nv;

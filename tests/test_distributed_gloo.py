@@ -65,9 +65,12 @@ class OracleShardDevice:
     def splat_local(self):
         self.tree.splat_bytes(self.pending)
 
-    # building statistics through the wire format: header 16 B, box 32 B, counts (snodes, dtrees,
-    # sampling nodes, building nodes), snodes 8 B, D-tree meta 32 B (record count at word 5),
-    # sampling nodes 32 B, building nodes 48 B (u64 sum[4] + u32 child[4])
+    # building statistics through the wire format (v2): header 16 B, box 32 B, counts (snodes,
+    # dtrees, sampling nodes, building nodes), snodes 8 B, D-tree meta 32 B (record count at word 5),
+    # sampling nodes 32 B, building nodes 48 B (u64 sum[4] + u32 child[4]), then FRAC u64 learned-
+    # fraction statistics per D-tree -- pg_get_tree_stats' order: sums, counts, fraction statistics
+    FRAC = 11
+
     def _layout(self, blob):
         ns, nd, nsamp, nb = np.frombuffer(blob[48:64].tobytes(), np.uint32)
         meta = 64 + 8 * int(ns)
@@ -76,22 +79,26 @@ class OracleShardDevice:
 
     def tree_stats_words(self):
         nd, nb, _, _ = self._layout(self.tree.serialize())
-        return 4 * nb + nd
+        return 4 * nb + nd + self.FRAC * nd
 
     def get_tree_stats(self):
         blob = self.tree.serialize()
         nd, nb, meta, build = self._layout(blob)
         sums = np.frombuffer(blob[build:build + 48 * nb].tobytes(), np.uint8).reshape(nb, 48)[:, :32]
         cnt = np.frombuffer(blob[meta:meta + 32 * nd].tobytes(), np.uint32).reshape(nd, 8)[:, 5]
-        return np.concatenate([sums.copy().view(np.uint64).reshape(-1), cnt.astype(np.uint64)])
+        frac = np.frombuffer(blob[build + 48 * nb:].tobytes(), np.uint64)
+        assert len(frac) == self.FRAC * nd
+        return np.concatenate([sums.copy().view(np.uint64).reshape(-1), cnt.astype(np.uint64), frac])
 
     def put_tree_stats(self, stats):
         blob = np.array(self.tree.serialize(), np.uint8)
         nd, nb, meta, build = self._layout(blob)
+        stats = np.asarray(stats, np.uint64)
         b = blob[build:build + 48 * nb].reshape(nb, 48)
-        b[:, :32] = np.asarray(stats[:4 * nb], np.uint64).reshape(nb, 4).view(np.uint8)
+        b[:, :32] = stats[:4 * nb].reshape(nb, 4).view(np.uint8)
         m = blob[meta:meta + 32 * nd].reshape(nd, 32)
-        m[:, 20:24] = np.asarray(stats[4 * nb:], np.uint64).astype(np.uint32).reshape(nd, 1).view(np.uint8)
+        m[:, 20:24] = stats[4 * nb:4 * nb + nd].astype(np.uint32).reshape(nd, 1).view(np.uint8)
+        blob[build + 48 * nb:] = stats[4 * nb + nd:].view(np.uint8)
         self.tree.deserialize(blob)
 
 

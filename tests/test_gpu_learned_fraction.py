@@ -1,0 +1,86 @@
+"""GPU side of the learned BSDF-sampling fraction (PG_FRACTION_LEARNED): the k_splat statistics and
+the refit's choice are bit-identical with the oracle on the same records, and the GPU's learned
+guided render is unbiased."""
+import numpy as np
+import pytest
+
+from test_learned_fraction import CANDIDATES, learned_cfg, synthetic_records, tree_alphas
+
+pytestmark = pytest.mark.gpu
+
+
+def make_dev(pg, scene, cfg):
+    from mitsuba_path_guiding_amd.integrator import Device
+    d = Device(cfg)
+    d.upload(scene)
+    return d
+
+
+def test_gpu_learns_mixture_optimum(pg, O):
+    sc = pg.scenes.cornell(16, 16)
+    cfg = learned_cfg(pg)
+    lo, hi = sc.bounds()
+    recs = synthetic_records(pg.capi, tuple(((lo + hi) / 2).tolist()), 500, 0.3, 0.7)
+    dev = make_dev(pg, sc, cfg)
+    dev.splat_records(recs)
+    dev.refit(0)
+    tree = O.OracleSDTree(O.OracleScene(pg.capi, sc))
+    tree.configure(cfg)
+    tree.splat_bytes(recs)
+    tree.refit(0, cfg)
+    g = dev.get_sdtree()
+    assert np.array_equal(g, tree.serialize())
+    assert tree_alphas(g)[0] == np.float32(0.35)
+    dev.close()
+
+
+def test_learned_splat_refit_bitexact(pg, O):
+    """Oracle records of learned-mode training passes (guided vertices carry p_guide and f L_i / q0)
+    splatted into the GPU and oracle trees: identical statistics, fractions and trees each iteration."""
+    sc = pg.scenes.cornell(48, 48)
+    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=400.0, bsdf_fraction_bound=pg.capi.PG_FRACTION_LEARNED)
+    osc = O.OracleScene(pg.capi, sc)
+    otree = O.OracleSDTree(osc)
+    dev = make_dev(pg, sc, cfg)
+    off = 0
+    for it in range(4):
+        O.render(osc, cfg, 2 ** it, off, record=True, sdtree=otree)
+        off += 2 ** it
+        recs = otree.take_records(pg.capi)
+        dev.splat_records(recs)
+        otree.splat_bytes(recs)
+        assert np.array_equal(dev.get_tree_stats(), _oracle_stats(otree)), it
+        dev.refit(it)
+        otree.refit(it, cfg)
+        assert np.array_equal(dev.get_sdtree(), otree.serialize()), it
+    a = tree_alphas(dev.get_sdtree())
+    assert (a > 0).mean() > 0.5 and np.isin(a[a > 0], CANDIDATES).all()
+    dev.close()
+
+
+def _oracle_stats(tree):
+    """pg_get_tree_stats' vector from the oracle's wire format: building sums, counts, fraction stats."""
+    blob = tree.serialize()
+    ns, nd, nsamp, nb = (int(x) for x in np.frombuffer(blob[48:64].tobytes(), np.uint32))
+    meta = 64 + 8 * ns
+    build = meta + 32 * nd + 32 * nsamp
+    sums = np.frombuffer(blob[build:build + 48 * nb].tobytes(), np.uint8).reshape(nb, 48)[:, :32]
+    cnt = np.frombuffer(blob[meta:meta + 32 * nd].tobytes(), np.uint32).reshape(nd, 8)[:, 5]
+    frac = np.frombuffer(blob[build + 48 * nb:].tobytes(), np.uint64)
+    return np.concatenate([sums.copy().view(np.uint64).reshape(-1), cnt.astype(np.uint64), frac])
+
+
+def test_gpu_learned_guided_image_unbiased(pg, O):
+    from mitsuba_path_guiding_amd.integrator import GuidedPathTracer
+    from test_gpu_parity import _zstats
+    sc = pg.scenes.cornell(64, 64)
+    integ = GuidedPathTracer({"trainingIterations": 5, "sTreeThreshold": 400.0, "bsdfSamplingFractionBound": "learned"})
+    integ.preprocess(sc)
+    rgbw, sq = integ.render(256)
+    a = tree_alphas(integ.dev.get_sdtree())
+    integ.postprocess()
+    assert (a > 0).mean() > 0.5
+    c = O.render(O.OracleScene(pg.capi, sc), pg.capi.default_config(), 512)[:2]
+    m1, m2, z = _zstats((rgbw, sq), c)
+    assert (np.abs(z) < 5).mean() > 0.995
+    assert abs(m1.mean() - m2.mean()) / m2.mean() < 0.01
