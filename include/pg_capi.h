@@ -226,6 +226,12 @@ typedef struct pg_config {
                                      their device times into pg_stats trace_ms / shade_ms / shadow_ms.  Six event
                                      records per bounce cost ~2 % on C3, so 0 (the default) leaves
                                      those three statistics at 0. */
+    int32_t volpath_exact_mis;    /* volpath: 0 (default) = the reference's MIS weight for an emitter reached through
+                                     index-matched surfaces, whose emitter pdf uses the LAST segment's length
+                                     (rayIntersectAndLookForEmitter + DirectSamplingRecord::setQuery,
+                                     progressive_volpath.cpp:401-460, records.inl:170-178): biased, +34 % on
+                                     data/tests/test_bidir_2.xml.  1 = the whole ray length: the MIS
+                                     weights sum to one and the estimator is unbiased. */
 } pg_config;
 enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2, PG_FRACTION_LEARNED = 3 };
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };

@@ -86,7 +86,7 @@ class pg_config(C.Structure):
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
                 ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
                 ("distance_guiding", C.c_float), ("aovs", C.c_int32), ("bsdf_fraction_bound", C.c_int32),
-                ("kernel_timing", C.c_int32)]
+                ("kernel_timing", C.c_int32), ("volpath_exact_mis", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -131,6 +131,7 @@ def default_config(**overrides):
     c.aovs = 0
     c.bsdf_fraction_bound = PG_FRACTION_FIXED
     c.kernel_timing = 0
+    c.volpath_exact_mis = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")

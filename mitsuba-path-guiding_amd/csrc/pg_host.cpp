@@ -118,6 +118,8 @@ struct Lane {
     int vtx_slots = 0;
     uint32_t vtxP = 0;  // slot stride of vtx (recording passes only allocate it)
     DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
+    DevBuf qkey, qsorted, rsort_hist;  // ray-sorted trace queues (PG_RAY_SORT): keys, sorted entries, histograms
+    bool sorted = false;               // the queue of the next trace launch is qsorted
     DevBuf aov;  // denoiser features per slot (pg_config.aovs), 2 x float4
     uint32_t *h_counts = nullptr;  // pinned: per-bounce class counts of the running chunk
     uint32_t *h_stats = nullptr;   // pinned: counters of the last finished chunk
@@ -426,6 +428,17 @@ EventPair nextEvents(Lane *l, LaunchKind kind) {
     return pool[l->evused[l->evcur]++];
 }
 
+// ray-sorted trace queues (A/B switch PG_RAY_SORT=1): k_shade writes a ray order key per queued path and
+// a counting sort groups every shard of the next closest-hit queue by direction octant + origin cell
+bool raySortEnabled() {
+    static const bool on = [] {
+        const char *e = std::getenv("PG_RAY_SORT");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+constexpr uint32_t kRaySortMinShard = 1024;  // smaller bounces trace unsorted (the sort's launches cost more)
+
 // training-vertex slots per path of a pass (only recording passes write training vertices)
 int vertexSlots(const Ctx *c, bool rec) { return rec ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0; }
 
@@ -434,7 +447,7 @@ void releasePaths(Ctx *c) {
     for (int li = 0; li < c->nlanes; ++li) {
         Lane &l = c->lanes[li];
         for (DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo, &l.sh_o, &l.sh_d, &l.sh_c,
-                          &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov})
+                          &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov, &l.qkey, &l.qsorted})
             b->release();
         l.P = 0;
         l.vtx_slots = 0;
@@ -485,6 +498,11 @@ pg_status ensurePaths(Ctx *c, uint32_t want, bool rec) {
         HIPC(c, l.qs.alloc(qbytes));
         HIPC(c, l.class_q.alloc((size_t)PG_NUM_CLASSES * qbytes));
         if (c->cfg.aovs) HIPC(c, l.aov.alloc((size_t)P * 16));
+        if (raySortEnabled()) {
+            HIPC(c, l.qkey.alloc(qbytes / 2));
+            HIPC(c, l.qsorted.alloc(qbytes));
+            HIPC(c, l.rsort_hist.alloc((size_t)PG_QSHARDS * PG_RAY_SORT_BINS * 4));
+        }
         l.P = P;
     }
     return PG_OK;
@@ -609,6 +627,7 @@ pg_status pg_config_default(pg_config *c) {
     c->distance_guiding = 0.25f;
     c->bsdf_fraction_bound = PG_FRACTION_FIXED;
     c->kernel_timing = 0;
+    c->volpath_exact_mis = 0;
     return PG_OK;
 }
 
@@ -1043,6 +1062,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     g.guiding = c->cfg.guiding;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
     g.fraction_bound = c->cfg.bsdf_fraction_bound;
+    g.exact_mis = c->cfg.volpath_exact_mis;
     g.record = rec && maxV > 0;
     g.max_vertices = maxV;
     const SceneDev sc = sceneView(c);
@@ -1239,7 +1259,8 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         EventPair et{};
         if (evt) et = nextEvents(&l, shq ? KT_RAYS : KT_TRACE);
         if (evt) HIPC(c, hipEventRecord(et.a, l.stream));
-        const Queue tq = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb);
+        const Queue tq = lqueue(l, l.sorted ? l.qsorted.as<uint32_t>() : (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(),
+                                cb);
         if (shq) pg_launch_rays(l.stream, g, sc, pathView(&l), tq, l.bound, cls, *shq, l.bound);
         else pg_launch_trace(l.stream, g, sc, pathView(&l), tq, l.bound, cls, l.b == 0);
         if (evt) HIPC(c, hipEventRecord(et.b, l.stream));
@@ -1300,6 +1321,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             nextLayer += nl;
         }
         l.b = 0;
+        l.sorted = false;  // camera rays: their queue order is already coherent
         l.bound = pg_camera_shard_count(l.n, 0);
         l.active = true;
         l.traced = false;
@@ -1392,8 +1414,11 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         Queue cls[PG_NUM_CLASSES + 1];
         classQueues(l, cb, cls);
         const PathDev pv = pathView(&l);
-        const Queue next = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb + kBounceWords);
+        Queue next = lqueue(l, (l.b & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(), cb + kBounceWords);
         const Queue shq = lqueue(l, l.qs.as<uint32_t>(), cb + kShadowCounts);
+        const uint32_t nextBound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
+        const bool sortNext = raySortEnabled() && nextBound >= kRaySortMinShard;
+        if (sortNext) next.keys = l.qkey.as<uint16_t>();
         EventPair es{}, ew{};
         if (evt) es = nextEvents(&l, KT_SHADE);
         if (evt) HIPC(c, hipEventRecord(es.a, l.stream));
@@ -1407,7 +1432,10 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             }
         }
         if (evt) HIPC(c, hipEventRecord(es.b, l.stream));
-        l.bound = *std::max_element(shardLive, shardLive + PG_QSHARDS);
+        l.bound = nextBound;
+        if (sortNext)  // group every shard of the next closest-hit queue by ray order key
+            pg_launch_ray_sort(l.stream, next, l.bound, l.qsorted.as<uint32_t>(), l.rsort_hist.as<uint32_t>());
+        l.sorted = sortNext;
         // without per-launch timing the shadow rays share the next trace's launch
         if (fuseRays) return launchTrace(l, &shq);
         if (evt) ew = nextEvents(&l, KT_SHADOW);

@@ -80,7 +80,11 @@ struct Queue {
     uint32_t *items;
     uint32_t *counts;  // PG_QSHARDS
     uint32_t stride;
+    uint16_t *keys = nullptr;  // ray order keys of the entries (k_shade's output queue when rays are sorted)
 };
+// Ray order for the next closest-hit launch (pg_config: PG_RAY_SORT): key = direction octant (3 bits,
+// major) then the Morton code of the origin's cell in an 8^3 grid over the SD-tree cube (9 bits)
+#define PG_RAY_SORT_BINS 4096
 // camera layout: slot -> shard (slot >> 6) & 63, entry ((slot >> 12) << 6) | (slot & 63)
 __host__ __device__ inline uint32_t pg_queue_stride(uint32_t capacity) { return 64u * ((capacity + 4095u) / 4096u); }
 __host__ __device__ inline uint32_t pg_camera_shard_count(uint32_t n, uint32_t s) {
@@ -108,6 +112,9 @@ void pg_launch_shade_all(hipStream_t s, const GParams &g, const SceneDev &sc, co
 void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
                     const Queue *class_queues, Queue shq, uint32_t max_shadow_shard);
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);
+// counting sort of every shard of `q` by its keys into sorted_items (same shard layout and counts):
+// histogram, per-shard scan, scatter; hist: PG_QSHARDS * PG_RAY_SORT_BINS u32 of scratch (zeroed here)
+void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist);
 // aov_albedo / aov_normal: per-pixel feature sums, read when p.aov is set
 void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels,
                     uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq,

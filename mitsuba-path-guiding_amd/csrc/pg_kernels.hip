@@ -236,6 +236,36 @@ __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))
                                 threadStack(stack, p.stack_ovf), nullptr, 0);
 }
 
+// ray order key of a new extension ray (PG_RAY_SORT): direction octant, then the Morton code of the
+// origin's cell in an 8^3 grid over the SD-tree cube (the scene bounds)
+__device__ __forceinline__ uint32_t rayOrderKey(const SDDev &sd, f3 o, f3 d) {
+    const float inv = 8.0f / sd.extent;
+    const int cx = min(max((int)((o.x - sd.lo[0]) * inv), 0), 7);
+    const int cy = min(max((int)((o.y - sd.lo[1]) * inv), 0), 7);
+    const int cz = min(max((int)((o.z - sd.lo[2]) * inv), 0), 7);
+    uint32_t m = 0;
+    for (int b = 0; b < 3; ++b)
+        m |= (((cx >> b) & 1) << (3 * b)) | (((cy >> b) & 1) << (3 * b + 1)) | (((cz >> b) & 1) << (3 * b + 2));
+    const uint32_t oct = (d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u);
+    return (oct << 9) | m;
+}
+// waveAppend that also stores each entry's ray order key
+__device__ __forceinline__ void waveAppendKey(bool pred, uint32_t value, uint16_t key, uint32_t *q, uint16_t *keys,
+                                              uint32_t *count) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0) return;
+    int lane = threadIdx.x & 63;
+    int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (pred) {
+        const uint32_t at = base + __popcll(m & ((1ull << lane) - 1ull));
+        q[at] = value;
+        keys[at] = key;
+    }
+}
+
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
 // MODEL >= 0 compiles only that BSDF model's code (material-class queues filled by k_trace);
 // CAN_GUIDE = false drops the SD-tree code for classes that are never guided (delta lobes).
@@ -253,7 +283,7 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
     if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
     bool alive = false, shadow = false, dirtyL = false;
-    uint32_t slot = 0;
+    uint32_t slot = 0, rkey = 0;
     f3 L = mk1(0.f);
     if (i < n) slot = in.items[(size_t)s * in.stride + i];
     // the material table, staged in LDS once per block (the material read sits on the dependent chain
@@ -437,6 +467,7 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
                     flags = (flags & ~(PF_EMITTED_QUERY | PF_PREV_DELTA)) | ((bs.type & EDelta) ? PF_PREV_DELTA : 0u);
                     stS(&p.pinfo[slot], make_uint4(pix, sample, (depth + 1) | (flags << 16), nv));
                     alive = true;
+                    if (out.keys) rkey = rayOrderKey(sd, h.p, wo);
                 }
             }
             if (shadow) {
@@ -449,7 +480,11 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
         } while (false);
         if (dirtyL) stS(&p.rad[slot], f4(L, 0.0f));
     }
-    waveAppend(alive, slot, out.items + (size_t)s * out.stride, out.counts + s);
+    if (out.keys)
+        waveAppendKey(alive, slot, (uint16_t)rkey, out.items + (size_t)s * out.stride, out.keys + (size_t)s * out.stride,
+                      out.counts + s);
+    else
+        waveAppend(alive, slot, out.items + (size_t)s * out.stride, out.counts + s);
     waveAppend(shadow, slot, shq.items + (size_t)s * shq.stride, shq.counts + s);
     }
 }
@@ -476,6 +511,81 @@ __global__ __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(4))
     else if (b < r.end[3]) shadeBlock<PG_BSDF_PLASTIC, false, false>(g, sc, sd, p, in.q[3], out, shq, b - r.end[2]);
     else if (b < r.end[4]) shadeBlock<PG_BSDF_ROUGHPLASTIC, true, false>(g, sc, sd, p, in.q[4], out, shq, b - r.end[3]);
     else shadeBlock<-1, false, false>(g, sc, sd, p, in.q[5], out, shq, b - r.end[4]);
+}
+
+// ---- counting sort of a queue's shards by ray order key (PG_RAY_SORT): the next closest-hit launch
+// then traces each shard's rays grouped by direction octant and origin cell.  Within a key the order
+// follows LDS/global atomics (nondeterministic), which is harmless: every path is a pure function of
+// (pixel, sample), whatever the order its bounces are traced in.
+#define RSORT_TILE 4096  // queue entries per block (256 threads x 16)
+__global__ __launch_bounds__(256) void k_rsort_hist(Queue q, uint32_t *hist) {
+    __shared__ uint32_t h[PG_RAY_SORT_BINS];
+    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1), tile = blockIdx.x / PG_QSHARDS;
+    const uint32_t n = q.counts[s], b0 = tile * RSORT_TILE;
+    if (b0 >= n) return;
+    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256) h[k] = 0;
+    __syncthreads();
+    const uint16_t *keys = q.keys + (size_t)s * q.stride;
+    const uint32_t e = min(n, b0 + RSORT_TILE);
+    for (uint32_t i = b0 + threadIdx.x; i < e; i += 256) atomicAdd(&h[keys[i]], 1u);
+    __syncthreads();
+    uint32_t *g = hist + (size_t)s * PG_RAY_SORT_BINS;
+    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256)
+        if (h[k]) atomicAdd(&g[k], h[k]);
+}
+// exclusive scan of every shard's histogram in place (one block per shard)
+__global__ __launch_bounds__(256) void k_rsort_scan(uint32_t *hist) {
+    __shared__ uint32_t part[256];
+    uint32_t *g = hist + (size_t)blockIdx.x * PG_RAY_SORT_BINS;
+    constexpr int PER = PG_RAY_SORT_BINS / 256;
+    uint32_t v[PER], sum = 0;
+    for (int j = 0; j < PER; ++j) {
+        v[j] = g[threadIdx.x * PER + j];
+        sum += v[j];
+    }
+    part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int off = 1; off < 256; off <<= 1) {  // Hillis-Steele inclusive scan of the thread sums
+        const uint32_t x = threadIdx.x >= (uint32_t)off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[threadIdx.x] - sum;
+    for (int j = 0; j < PER; ++j) {
+        g[threadIdx.x * PER + j] = run;
+        run += v[j];
+    }
+}
+__global__ __launch_bounds__(256) void k_rsort_scatter(Queue q, uint32_t *hist, uint32_t *sorted) {
+    __shared__ uint32_t cnt[PG_RAY_SORT_BINS];
+    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1), tile = blockIdx.x / PG_QSHARDS;
+    const uint32_t n = q.counts[s], b0 = tile * RSORT_TILE;
+    if (b0 >= n) return;
+    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256) cnt[k] = 0;
+    __syncthreads();
+    const uint16_t *keys = q.keys + (size_t)s * q.stride;
+    const uint32_t *items = q.items + (size_t)s * q.stride;
+    const uint32_t e = min(n, b0 + RSORT_TILE);
+    constexpr int PER = RSORT_TILE / 256;
+    uint32_t rank[PER], key[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {  // fixed trip count: the per-thread arrays stay in registers
+        const uint32_t i = b0 + threadIdx.x + 256u * j;
+        key[j] = i < e ? keys[i] : 0u;
+        rank[j] = i < e ? atomicAdd(&cnt[key[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    uint32_t *g = hist + (size_t)s * PG_RAY_SORT_BINS;
+    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256)  // this tile's range of every key
+        if (cnt[k]) cnt[k] = atomicAdd(&g[k], cnt[k]);
+    __syncthreads();
+    uint32_t *out = sorted + (size_t)s * q.stride;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+        const uint32_t i = b0 + threadIdx.x + 256u * j;
+        if (i < e) out[cnt[key[j]] + rank[j]] = items[i];
+    }
 }
 
 // film: box-filtered accumulation of every layer's sample into its pixel, in sample order
@@ -865,6 +975,14 @@ void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue
     if (!max_shard) return;
     hipLaunchKernelGGL(k_shadow, shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS), dim3(TRACE_BLOCK), 0,
                        s, sc, p, q);
+}
+void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist) {
+    if (!max_shard) return;
+    (void)hipMemsetAsync(hist, 0, (size_t)PG_QSHARDS * PG_RAY_SORT_BINS * 4, s);
+    const dim3 grid(PG_QSHARDS * blocks(max_shard, RSORT_TILE));
+    hipLaunchKernelGGL(k_rsort_hist, grid, dim3(256), 0, s, q, hist);
+    hipLaunchKernelGGL(k_rsort_scan, dim3(PG_QSHARDS), dim3(256), 0, s, hist);
+    hipLaunchKernelGGL(k_rsort_scatter, grid, dim3(256), 0, s, q, hist, sorted_items);
 }
 void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
                     uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq, float4 *aov_albedo,

@@ -411,16 +411,17 @@ struct ItsRef {  // the caller's intersection record: closest hit of the current
 // walk through null surfaces is done once without the medium; only when it ends on a lit emitter
 // is it walked again to estimate the transmittance of its segments (the reference estimates it
 // on every walk and discards it otherwise: same estimator, oracle/orc_volpath.h "lazy").
+// exact: qdist = the whole walk's length (pg_config.volpath_exact_mis) instead of the last segment's
 __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev &v, int medium, int maxInteractions, f3 o0, f3 d,
                                float mint0, ItsRef &its, f3 &value, f3 &qn, float &qdist, int &qem, VRng &rng,
-                               const TStack &stk, uint32_t &segs) {
+                               const TStack &stk, uint32_t &segs, bool exact) {
     value = mk1(0.f);
     qem = -1;
     f3 o = o0;
     float mint = mint0;
     int m = medium, interactions = 0;
     bool anyMedium = false;
-    float t = 0, u = 0, w = 0;
+    float t = 0, u = 0, w = 0, walked = 0;
     uint32_t tri = 0;
     uint32_t bits = 0;
     for (;;) {
@@ -438,6 +439,7 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
             m = targetMedium(tm, d, h.geoN);
         }
         o = o + d * t;
+        walked += t;
         mint = itsMinT(o);
         if (++interactions > 100) return;
     }
@@ -473,7 +475,7 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
     }
     value = mk(E.radiance[0], E.radiance[1], E.radiance[2]) * T;
     qn = h.shN;
-    qdist = t;  // setQuery: the LAST segment's length (records.inl:170-178)
+    qdist = exact ? walked + t : t;  // setQuery: the LAST segment's length (records.inl:170-178)
     qem = em;
 }
 
@@ -609,7 +611,7 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         f3 value, qn;
         float qdist;
         int qem;
-        lookForEmitter(sc, v, P.medium, maxInter, mp, wo, 0.0f, P.its, value, qn, qdist, qem, rng, stk, segs);
+        lookForEmitter(sc, v, P.medium, maxInter, mp, wo, 0.0f, P.its, value, qn, qdist, qem, rng, stk, segs, g.exact_mis != 0);
         if (!isZero(value) && fminf(value.x, fminf(value.y, value.z)) > 0.f) {
             const float emitterPdf = g.use_nee ? pdfEmitter(g, sc, qem, mk1(0.f), wo, qn, qdist) : 0.0f;
             P.L = P.L + P.T * value * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
@@ -731,7 +733,8 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         f3 value, qn;
         float qdist;
         int qem;
-        lookForEmitter(sc, v, P.medium, maxInter, h.p, wo, itsMinT(h.p), P.its, value, qn, qdist, qem, rng, stk, segs);
+        lookForEmitter(sc, v, P.medium, maxInter, h.p, wo, itsMinT(h.p), P.its, value, qn, qdist, qem, rng, stk, segs,
+                       g.exact_mis != 0);
         if (!isZero(value)) {
             const float emitterPdf =
                 (g.use_nee && !(bs.type & EDelta)) ? pdfEmitter(g, sc, qem, refN, wo, qn, qdist) : 0.0f;

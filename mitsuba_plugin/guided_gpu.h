@@ -50,6 +50,9 @@ public:
         m_cfg.d_tree_threshold = props.getFloat("dTreeThreshold", 0.01f);
         m_cfg.distance_guiding = props.getFloat("distanceGuiding", m_cfg.distance_guiding);  // volpath only
         m_cfg.aovs = props.getBoolean("aovs", false);
+        // volpath: MIS of emitters behind index-matched surfaces with the whole ray length (unbiased)
+        // instead of the reference's last segment
+        m_cfg.volpath_exact_mis = props.getBoolean("exactMis", false);
         std::string bound = boost::to_lower_copy(props.getString("bsdfSamplingFractionBound", "fixed"));
         m_cfg.bsdf_fraction_bound = bound == "albedo" ? PG_FRACTION_ALBEDO : bound == "learned" ? PG_FRACTION_LEARNED
                                     : bound == "throughput" ? PG_FRACTION_THROUGHPUT : PG_FRACTION_FIXED;

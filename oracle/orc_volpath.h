@@ -83,13 +83,15 @@ struct EmitterQuery {
 
 // rayIntersectAndLookForEmitter: `its` receives the FIRST intersection; the walk continues through
 // null surfaces (updating the medium) to find an emitter behind them
+// exact: q.dist = the whole walk's length (pg_config.volpath_exact_mis; unbiased MIS) instead of the
+// reference's last segment
 inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInteractions, Ray ray, Its &its,
-                           EmitterQuery &q, bool lazy, bool grid, VolCounters &cnt) {
+                           EmitterQuery &q, bool lazy, bool grid, VolCounters &cnt, bool exact = false) {
     q.value = V3(0.f);
     q.emitter = -1;
     Its its2;
     Its *cur = &its;
-    float T = 1.0f;
+    float T = 1.0f, walked = 0.0f;
     bool surface = false;
     int interactions = 0;
     struct Seg {
@@ -111,6 +113,7 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
         if (interactions == maxInteractions || !(S.mats[sh.material].type & ENull) || sh.emitter >= 0) break;
         if (!lazy && T == 0) return;
         if (isMediumTransition(sh)) medium = targetMedium(sh, ray.d, cur->geoN);
+        walked += cur->t;
         ray.o = ray.o + ray.d * cur->t;
         ray.mint = kEpsilon;
         cur = &its2;
@@ -129,7 +132,7 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
     q.value = Le * T;
     q.n = cur->sh.n;
     q.d = ray.d;
-    q.dist = cur->t;
+    q.dist = exact ? walked + cur->t : cur->t;
     q.emitter = sh.emitter;
 }
 
@@ -269,7 +272,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
             T *= pw;
             ray = Ray{mp, wo, 0.0f, kInf};
             EmitterQuery q;
-            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, grid, cnt);
+            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, grid, cnt, cfg.volpath_exact_mis != 0);
             if (!its.valid) its.t = kInf;
             if (!isZero(q.value) && std::min(q.value.x, std::min(q.value.y, q.value.z)) > 0.f) {
                 const float emitterPdf = cfg.use_nee ? pdfEmitterDirect(S, q.emitter, V3(0.f), q.d, q.n, q.dist) : 0.0f;
@@ -359,7 +362,7 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 continue;
             }
             EmitterQuery q;
-            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, grid, cnt);
+            lookForEmitter(S, rng, medium, maxInter(depth), ray, its, q, lazy, grid, cnt, cfg.volpath_exact_mis != 0);
             if (!its.valid) its.t = kInf;
             if (!isZero(q.value)) {
                 const float emitterPdf = (cfg.use_nee && !(bs.sampledType & EDelta))

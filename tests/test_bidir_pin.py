@@ -65,31 +65,33 @@ def test_fixture_matches_closed_forms():
     assert 0 < z["bidir0_reflected"][0] < 0.01 * d0
 
 
-# (scene, NEE, expected image): test_bidir_2 with NEE is compared with the expectation of the
-# reference's own estimator, whose MIS weights do not sum to one for an emitter reached through an
-# index-matched surface (rayIntersectAndLookForEmitter hands setQuery the LAST segment's length,
-# progressive_volpath.cpp:401-460 + records.inl:170-178): +34 % on this scene, reproduced exactly
-# (make_bidir_fixture.direct_medium, mis="reference").  Without NEE the estimator is unbiased.
-PIN_CASES = [("bidir_0", 1, "bidir0_image"), ("bidir_0", 0, "bidir0_image"),
-             ("bidir_2", 0, "bidir2_image"), ("bidir_2", 1, "bidir2_refmis_image")]
+# (scene, NEE, volpath_exact_mis, expected image): test_bidir_2 with NEE is compared with the
+# expectation of the reference's own estimator, whose MIS weights do not sum to one for an emitter
+# reached through an index-matched surface (rayIntersectAndLookForEmitter hands setQuery the LAST
+# segment's length, progressive_volpath.cpp:401-460 + records.inl:170-178): +34 % on this scene,
+# reproduced exactly (make_bidir_fixture.direct_medium, mis="reference").  Without NEE, or with
+# pg_config.volpath_exact_mis = 1 (the whole ray length), the estimator is unbiased.
+PIN_CASES = [("bidir_0", 1, 0, "bidir0_image"), ("bidir_0", 0, 0, "bidir0_image"),
+             ("bidir_2", 0, 0, "bidir2_image"), ("bidir_2", 1, 0, "bidir2_refmis_image"),
+             ("bidir_2", 1, 1, "bidir2_image")]
 
 
 def expected_image(key):
     return np.load(os.path.join(GOLDEN, "bidir_analytic.npz"))[key]
 
 
-@pytest.mark.parametrize("name,nee,key", PIN_CASES)
-def test_oracle_pinned_by_bidir_scene(pg, O, name, nee, key):
+@pytest.mark.parametrize("name,nee,exact,key", PIN_CASES)
+def test_oracle_pinned_by_bidir_scene(pg, O, name, nee, exact, key):
     sc, _ = bidir_scene(pg, name)
     vol = name == "bidir_2"
     if vol:
         assert len(sc.media) == 1 and abs(sc.media[0].scale - 1.0) < 1e-7 and sc.media[0].albedo[0] == 0.0
     cfg = pg.capi.default_config(integrator=pg.capi.PG_INTEGRATOR_VOLPATH if vol else pg.capi.PG_INTEGRATOR_PATH,
-                                 use_nee=nee)
+                                 use_nee=nee, volpath_exact_mis=exact)
     spp = 1024 if nee else 4096
     rgbw, sq, _ = O.render(O.OracleScene(pg.capi, sc), cfg, spp)
     zmean, rel = check(rgbw, sq, expected_image(key), spp)
-    print(f"{name} nee={nee}: image mean {rel:+.2e} relative to {key}, z = {zmean:+.2f}")
+    print(f"{name} nee={nee} exact={exact}: image mean {rel:+.2e} relative to {key}, z = {zmean:+.2f}")
     assert abs(rel) < 0.01
 
 

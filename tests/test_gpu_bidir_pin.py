@@ -11,18 +11,18 @@ from test_bidir_pin import PIN_CASES, bidir_scene, check, expected_image
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("name,nee,key", PIN_CASES)
-def test_gpu_pinned_by_bidir_scene(pg, name, nee, key):
+@pytest.mark.parametrize("name,nee,exact,key", PIN_CASES)
+def test_gpu_pinned_by_bidir_scene(pg, name, nee, exact, key):
     from mitsuba_path_guiding_amd.integrator import ProgressivePathTracer, ProgressiveVolumetricPathTracer
     sc, _ = bidir_scene(pg, name)
     T = ProgressiveVolumetricPathTracer if name == "bidir_2" else ProgressivePathTracer
     spp = 4096 if nee else 16384
-    t = T({"useNee": bool(nee), "samplesPerProgression": spp})
+    t = T({"useNee": bool(nee), "samplesPerProgression": spp, "exactMis": bool(exact)})
     t.preprocess(sc)
     rgbw, sq = t.render(spp)
     t.postprocess()
     zmean, rel = check(rgbw, sq, expected_image(key), spp)
-    print(f"gpu {name} nee={nee}: image mean {rel:+.2e} relative to {key}, z = {zmean:+.2f}")
+    print(f"gpu {name} nee={nee} exact={exact}: image mean {rel:+.2e} relative to {key}, z = {zmean:+.2f}")
     assert abs(rel) < 5e-3
 
 
