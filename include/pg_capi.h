@@ -232,6 +232,10 @@ typedef struct pg_config {
                                      progressive_volpath.cpp:401-460, records.inl:170-178): biased, +34 % on
                                      data/tests/test_bidir_2.xml.  1 = the whole ray length: the MIS
                                      weights sum to one and the estimator is unbiased. */
+    int32_t tail_paths;           /* path integrator: a chunk with at most this many live paths finishes in one launch
+                                     (k_tail: each thread loops shade -> shadow -> closest hit) instead of one
+                                     launch pair + count readback per bounce; bit-identical results.  0 = the
+                                     default (65536, or the PG_TAIL_PATHS environment variable), < 0 = off. */
 } pg_config;
 enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2, PG_FRACTION_LEARNED = 3 };
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };
@@ -271,6 +275,7 @@ typedef struct pg_stats {
     double rays_ms;           /* device time of the fused shadow + closest-hit launches (k_rays; kernel_timing) */
     uint64_t rays_launches;   /* k_rays launches (a bounce's shadow rays + the next bounce's closest hits) */
     uint64_t shadow_launches; /* unfused shadow-ray launches (PG_NO_RAYS_FUSION) */
+    uint64_t tail_launches;   /* chunk tails finished in one launch (k_tail) */
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

@@ -86,7 +86,8 @@ class pg_config(C.Structure):
                 ("tile_size", C.c_uint32), ("max_paths_in_flight", C.c_uint32), ("gpu_depth_cap", C.c_int32),
                 ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
                 ("distance_guiding", C.c_float), ("aovs", C.c_int32), ("bsdf_fraction_bound", C.c_int32),
-                ("kernel_timing", C.c_int32), ("volpath_exact_mis", C.c_int32)]
+                ("kernel_timing", C.c_int32), ("volpath_exact_mis", C.c_int32),
+                ("tail_paths", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -100,7 +101,7 @@ class pg_stats(C.Structure):
                 ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
                 ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64),
                 ("density_lookups", C.c_uint64), ("escaped", C.c_uint64), ("rays_ms", C.c_double),
-                ("rays_launches", C.c_uint64), ("shadow_launches", C.c_uint64)]
+                ("rays_launches", C.c_uint64), ("shadow_launches", C.c_uint64), ("tail_launches", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -132,6 +133,7 @@ def default_config(**overrides):
     c.bsdf_fraction_bound = PG_FRACTION_FIXED
     c.kernel_timing = 0
     c.volpath_exact_mis = 0
+    c.tail_paths = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")

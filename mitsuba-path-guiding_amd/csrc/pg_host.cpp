@@ -120,6 +120,8 @@ struct Lane {
     DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
     DevBuf qkey, qsorted, rsort_hist;  // ray-sorted trace queues (PG_RAY_SORT): keys, sorted entries, histograms
     bool sorted = false;               // the queue of the next trace launch is qsorted
+    DevBuf tail_stats;                 // k_tail counters of the running chunk (3 u64), copied to h_tail
+    uint64_t *h_tail = nullptr;        // pinned: k_tail counters of the last finished chunk
     DevBuf aov;  // denoiser features per slot (pg_config.aovs), 2 x float4
     uint32_t *h_counts = nullptr;  // pinned: per-bounce class counts of the running chunk
     uint32_t *h_stats = nullptr;   // pinned: counters of the last finished chunk
@@ -439,6 +441,16 @@ bool raySortEnabled() {
 }
 constexpr uint32_t kRaySortMinShard = 1024;  // smaller bounces trace unsorted (the sort's launches cost more)
 
+// the tail of a chunk (k_tail): at most this many live paths left -> one launch finishes them all
+// instead of one launch pair + count readback per bounce (PG_TAIL_PATHS overrides; 0 = off)
+uint32_t tailPaths() {
+    static const uint32_t n = [] {
+        const char *e = std::getenv("PG_TAIL_PATHS");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 16;
+    }();
+    return n;
+}
+
 // training-vertex slots per path of a pass (only recording passes write training vertices)
 int vertexSlots(const Ctx *c, bool rec) { return rec ? std::max(0, std::min(c->cfg.record_max_vertices, 64)) : 0; }
 
@@ -470,6 +482,8 @@ pg_status ensurePaths(Ctx *c, uint32_t want, bool rec) {
             HIPC(c, hipHostMalloc((void **)&l.h_stats, kCounterWords * 4, hipHostMallocDefault));
             HIPC(c, l.counters.alloc(kCounterWords * 4));
             HIPC(c, l.stack_ovf.alloc(2 * pg_stack_overflow_words(0) * 4));  // k_rays: two launches' worth
+            HIPC(c, l.tail_stats.alloc(32));
+            HIPC(c, hipHostMalloc((void **)&l.h_tail, 32, hipHostMallocDefault));
         }
         const bool aovMissing = c->cfg.aovs && !l.aov.p;
         if (vslots > 0 && (vslots > l.vtx_slots || want > l.vtxP)) {
@@ -628,6 +642,7 @@ pg_status pg_config_default(pg_config *c) {
     c->bsdf_fraction_bound = PG_FRACTION_FIXED;
     c->kernel_timing = 0;
     c->volpath_exact_mis = 0;
+    c->tail_paths = 0;
     return PG_OK;
 }
 
@@ -705,6 +720,7 @@ pg_status pg_destroy(void *ctx) {
         if (l.done) (void)hipEventDestroy(l.done);
         if (l.h_counts) (void)hipHostFree(l.h_counts);
         if (l.h_stats) (void)hipHostFree(l.h_stats);
+        if (l.h_tail) (void)hipHostFree(l.h_tail);
         if (l.stream) (void)hipStreamDestroy(l.stream);
     }
     if (c->timing.a) (void)hipEventDestroy(c->timing.a);
@@ -1276,6 +1292,9 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         for (uint32_t k = 0; k < l.stats_bounces; ++k)
             for (int sh = 0; sh < PG_QSHARDS; ++sh)
                 c->stats.shadow_rays += l.h_stats[(size_t)kBounceWords * k + kShadowCounts + sh];
+        c->stats.segments += l.h_tail[0];  // the chunk's tail (k_tail)
+        c->stats.escaped += l.h_tail[1];
+        c->stats.shadow_rays += l.h_tail[2];
         if (std::getenv("PG_DEBUG_COUNTS")) {
             for (uint32_t k = 0; k < l.stats_bounces && k < l.used_prev.size(); ++k) {
                 uint64_t t = 0;
@@ -1328,6 +1347,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         l.chunk = nextChunk++;
         HIPC(c, hipStreamWaitEvent(l.stream, c->pass_start, 0));
         HIPC(c, hipMemsetAsync(l.counters.p, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, l.stream));
+        HIPC(c, hipMemsetAsync(l.tail_stats.p, 0, 24, l.stream));
         pg_launch_camera(l.stream, g, pathView(&l), c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl,
                          sample_offset + l.layer0, lqueue(l, l.q0.as<uint32_t>(), l.counters.as<uint32_t>()));
         return launchTrace(l, nullptr);
@@ -1338,6 +1358,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         if ((st = collectStats(l))) return st;
         const PathDev pv = pathView(&l);
         HIPC(c, hipMemcpyAsync(l.h_stats, l.counters.p, (size_t)kBounceWords * l.b * 4, hipMemcpyDeviceToHost, l.stream));
+        HIPC(c, hipMemcpyAsync(l.h_tail, l.tail_stats.p, 24, hipMemcpyDeviceToHost, l.stream));
         HIPC(c, hipStreamWaitEvent(l.stream, c->film_order, 0));
         pg_launch_film(l.stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
                        c->film_sq.as<float4>(), c->aov_albedo.as<float4>(), c->aov_normal.as<float4>());
@@ -1396,7 +1417,17 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             l.used_cur.push_back(t);
         }
         ++l.b;
-        if (nlive == 0 || l.b >= maxBounces) {
+        const uint32_t tailMax = c->cfg.tail_paths < 0 ? 0u : c->cfg.tail_paths > 0 ? (uint32_t)c->cfg.tail_paths : tailPaths();
+        const bool tail = nlive > 0 && nlive <= tailMax && l.b < maxBounces;
+        if (tail) {  // one launch finishes every remaining path (shading starts at the hits just traced)
+            const uint32_t *cbt = l.counters.as<uint32_t>() + (size_t)kBounceWords * (l.b - 1);
+            const Queue tq = lqueue(l, l.sorted ? l.qsorted.as<uint32_t>()
+                                                : ((l.b - 1) & 1) ? l.q1.as<uint32_t>() : l.q0.as<uint32_t>(),
+                                    const_cast<uint32_t *>(cbt));
+            pg_launch_tail(l.stream, g, sc, sd, pathView(&l), tq, l.bound, l.tail_stats.as<unsigned long long>());
+            c->stats.tail_launches += 1;
+        }
+        if (nlive == 0 || tail || l.b >= maxBounces) {
             l.traced = true;
             // finish this lane and every waiting lane whose turn comes after it, in chunk order
             for (bool progress = true; progress;) {

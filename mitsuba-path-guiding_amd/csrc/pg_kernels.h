@@ -112,6 +112,10 @@ void pg_launch_shade_all(hipStream_t s, const GParams &g, const SceneDev &sc, co
 void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard,
                     const Queue *class_queues, Queue shq, uint32_t max_shadow_shard);
 void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue q, uint32_t max_shard);
+// every remaining path of the queue `q` (its hits already traced) to its end in one launch, each thread
+// looping shade -> shadow ray -> closest hit (k_tail); stats: 3 u64 (segments, escaped, shadow rays)
+void pg_launch_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p, Queue q,
+                    uint32_t max_shard, unsigned long long *stats);
 // counting sort of every shard of `q` by its keys into sorted_items (same shard layout and counts):
 // histogram, per-shard scan, scatter; hist: PG_QSHARDS * PG_RAY_SORT_BINS u32 of scratch (zeroed here)
 void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist);

@@ -271,6 +271,200 @@ __device__ __forceinline__ void waveAppendKey(bool pred, uint32_t value, uint16_
 // CAN_GUIDE = false drops the SD-tree code for classes that are never guided (delta lobes).
 // ENV compiles in environment-emitter sampling for NEE (kept out of the other instantiations: it
 // costs 4-8 VGPRs).
+// one bounce of Li for the path in `slot` (progressive_path.cpp:149-306 + guiding): reads its state,
+// writes the next one; alive = an extension ray was written, shadow = a shadow ray was written (sh_*)
+// mats: the material table (global memory, or a block's LDS copy); wantKey: compute rkey (PG_RAY_SORT)
+template <int MODEL, bool CAN_GUIDE, bool ENV>
+__device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
+                                         uint32_t slot, const GMat *mats, bool wantKey, bool &alive, bool &shadow,
+                                         uint32_t &rkey) {
+    bool dirtyL = false;
+    f3 L = mk1(0.f);
+    do {
+        uint4 pi = ldS(&p.pinfo[slot]);
+        const uint32_t pix = pi.x, sample = pi.y;
+        uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16, nv = pi.w;
+        float4 hv = ldS(&p.hit[slot]);
+        float4 T4 = ldS(&p.thr[slot]);
+        float4 L4 = ldS(&p.rad[slot]);
+        f3 T = xyz(T4);
+        L = xyz(L4);
+        float eta = T4.w;
+        uint32_t tri = __float_as_uint(hv.y);
+        if (tri == 0xFFFFFFFFu) break;  // escaped: no environment emitter
+        const uint32_t key = rngKey(pix, g.seed);
+        f3 rd = xyz(ldS(&p.ray_d[slot]));
+        Hit h;
+        fetchHit(sc, tri, hv.z, hv.w, rd, h);
+        f3 Le = mk1(0.f);
+        if (h.emitter >= 0 && dot(h.shN, -rd) > 0) {  // AreaLight::eval (area.cpp)
+            const GEmitter &em = sc.ems[h.emitter];
+            Le = mk(em.radiance[0], em.radiance[1], em.radiance[2]);
+        }
+        // ---- finish the previous bounce: emitter hit by the sampled direction (MIS), then RR
+        if (depth > 1) {
+            if (h.emitter >= 0) {
+                float4 pv = ldS(&p.prev[slot]);
+                float lumPdf = 0.0f;
+                if (g.use_nee && !(flags & PF_PREV_DELTA)) {
+                    f3 prevRefN = xyz(pv);
+                    if (dot(rd, prevRefN) >= 0 && dot(rd, h.shN) < 0) {
+                        const GEmitter &em = sc.ems[h.emitter];
+                        lumPdf = em.inv_area * (hv.x * hv.x) / absDot(rd, h.shN) * (1.0f / (float)g.num_emitters);
+                    }
+                }
+                float w = g.use_nee ? miWeight(pv.w, lumPdf) : 1.0f;
+                L = L + T * Le * w;
+                dirtyL = true;
+            }
+            if (depth - 1 >= (uint32_t)g.rr_depth) {
+                float q = fminf(maxc(T) * eta * eta, 0.95f);
+                if (rng1(key, sample, dimOf(depth - 1, SLOT_RR)) >= q) break;
+                T = T / q;
+            }
+        }
+        if (depth > g.depth_cap) break;
+        const GMat M = mats[h.mat];
+        if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
+            L = L + T * Le;
+            dirtyL = true;
+        }
+        if ((g.max_depth > 0 && (int)depth >= g.max_depth) ||
+            (g.strict_normals && dot(rd, h.geoN) * h.wi.z >= 0))
+            break;
+        const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
+        const bool guide = CAN_GUIDE && g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
+        const SDView sv = sdv(sd);
+        uint4 meta = make_uint4(0, 0, 0, 0);
+        if (guide) meta = sd.meta[sdLookup(sv, h.p)];
+        // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction):
+        // PG_FRACTION_LEARNED reads the leaf's learned fraction (meta.z; 0 = not learned yet)
+        const float leafAlpha = __uint_as_float(meta.z);
+        const float alpha = g.fraction_bound == PG_FRACTION_LEARNED ? (leafAlpha > 0 ? leafAlpha : g.bsdf_fraction)
+                                                                     : guideFraction(g.fraction_bound, g.bsdf_fraction,
+                                                                                     M.wbound, maxc(T));
+        float pgWo = -1.0f;  // p_guide of the sampled direction at a guided vertex (training record)
+
+        // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow.  With
+        // guiding, the D-tree pdf of the light direction is resolved below, in one lockstep walk
+        // with the direction-sampling descent (sdDual).
+        f3 neeC = mk1(0.f), neeD = mk1(0.f), neeV = mk1(0.f);
+        float neeDist = 0, neeEmPdf = 0, neeBp = 0;
+        bool neePending = false;
+        if (g.use_nee && (M.type & ESmooth)) {
+            float s0, s1;
+            rng2(key, sample, dimOf(depth, SLOT_NEE), s0, s1);
+            float emPdf;
+            f3 value = sampleEmitter<ENV>(g, sc, h.p, refN, s0, s1, neeD, neeDist, emPdf);
+            if (!isZero(value)) {
+                f3 woL = h.sh.toLocal(neeD);
+                f3 bsdfVal = bsdfEval<MODEL>(M, h.wi, woL);
+                if (!isZero(bsdfVal) && (!g.strict_normals || dot(h.geoN, neeD) * woL.z > 0)) {
+                    neeBp = bsdfPdf<MODEL>(M, h.wi, woL);
+                    neeEmPdf = emPdf;
+                    neeV = T * value * bsdfVal;
+                    shadow = true;
+                    if (guide) neePending = true;
+                    else neeC = neeV * miWeight(emPdf, neeBp);
+                }
+            }
+        }
+
+        // ---- direction sampling: BSDF, or one-sample MIS between BSDF and the D-tree
+        BS bs;
+        f3 weight;
+        float woPdf;
+        bool ok = true;
+        {
+            float b0, b1;
+            rng2(key, sample, dimOf(depth, SLOT_BSDF), b0, b1);
+            float b2 = rng1(key, sample, dimOf(depth, SLOT_COMP));
+            int mode = 0;  // D-tree walk of the sampled direction: 0 none, 1 pdf (BSDF sample), 2 sample
+            float bu = 0, bw = 0;
+            if (!guide) {
+                weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
+                woPdf = bs.pdf;
+            } else if (rng1(key, sample, dimOf(depth, SLOT_GUIDE_CHOICE)) < alpha) {
+                weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
+                if (isZero(weight)) {
+                    ok = false;
+                } else {
+                    mode = 1;
+                    dirToCanonical(h.sh.toWorld(bs.wo), bu, bw);
+                }
+            } else {
+                mode = 2;
+                rng2(key, sample, dimOf(depth, SLOT_GUIDE), bu, bw);
+            }
+            if (guide) {
+                float au = 0, aw = 0, aPdf, dPdf, cu, cv;
+                if (neePending) dirToCanonical(neeD, au, aw);
+                sdDual(sv, meta, neePending, au, aw, aPdf, mode != 0, mode == 2, bu, bw, cu, cv, dPdf);
+                if (neePending) neeC = neeV * miWeight(neeEmPdf, alpha * neeBp + (1 - alpha) * aPdf);
+                pgWo = dPdf;
+                if (mode == 1) {
+                    woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
+                    weight = weight * (bs.pdf / woPdf);
+                } else if (mode == 2) {
+                    f3 dW = canonicalToDir(cu, cv);
+                    f3 woL = h.sh.toLocal(dW);
+                    f3 f = bsdfEval<MODEL>(M, h.wi, woL);
+                    float bp = bsdfPdf<MODEL>(M, h.wi, woL);
+                    woPdf = alpha * bp + (1 - alpha) * dPdf;
+                    if (!(woPdf > 0) || isZero(f)) {
+                        ok = false;
+                    } else {
+                        weight = f / woPdf;
+                        bs.wo = woL;
+                        bs.pdf = bp;
+                        bool refl = h.wi.z * woL.z > 0;
+                        bs.type = refl ? ((M.type & EDiffuseReflection) ? EDiffuseReflection : EGlossyReflection)
+                                       : EGlossyTransmission;
+                        bs.eta = refl ? 1.0f : (h.wi.z > 0 ? M.eta : M.invEta);
+                    }
+                }
+            }
+        }
+        uint32_t vtxIndex = 0xFFFFFFFFu;
+        if (ok && !isZero(weight)) {
+            if (bs.type != ENull) flags |= PF_SCATTERED;
+            f3 wo = h.sh.toWorld(bs.wo);
+            if (!(g.strict_normals && dot(h.geoN, wo) * bs.wo.z <= 0)) {
+                f3 Tn = T * weight;
+                // training vertex: (x, wo, woPdf, T after this bounce, L snapshot)
+                if (g.record && !(bs.type & EDelta) && nv < (uint32_t)g.max_vertices) {
+                    float cu, cv;
+                    dirToCanonical(wo, cu, cv);
+                    float4 *vb = p.vtx + ((size_t)nv * p.vtxP + slot) * PG_VTX_F4;
+                    stS(vb + 0, f4(h.p, woPdf));
+                    stS(vb + 1, f4(Tn, __uint_as_float(packCanonical(cu, cv))));
+                    stS(vb + 2, f4(L, 0.0f));
+                    stS(vb + 3, f4(T, guide ? pgWo : -1.0f));
+                    vtxIndex = nv;
+                    nv++;
+                }
+                float tmin = kEpsilon * fmaxf(fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z)), kEpsilon);
+                stS(&p.ray_o[slot], f4(h.p, tmin));
+                stS(&p.ray_d[slot], f4(wo, __int_as_float(0x7f800000)));
+                stS(&p.thr[slot], f4(Tn, eta * bs.eta));
+                stS(&p.prev[slot], f4(refN, woPdf));
+                flags = (flags & ~(PF_EMITTED_QUERY | PF_PREV_DELTA)) | ((bs.type & EDelta) ? PF_PREV_DELTA : 0u);
+                stS(&p.pinfo[slot], make_uint4(pix, sample, (depth + 1) | (flags << 16), nv));
+                alive = true;
+                if (wantKey) rkey = rayOrderKey(sd, h.p, wo);
+            }
+        }
+        if (shadow) {
+            float tmin = kEpsilon * fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z));
+            stS(&p.sh_o[slot], f4(h.p, tmin));
+            stS(&p.sh_d[slot], f4(neeD, neeDist * (1 - kShadowEpsilon)));
+            stS(&p.sh_c[slot], f4(neeC, __uint_as_float(vtxIndex)));
+        }
+        if (!alive && nv != pi.w) stS(&p.pinfo[slot], make_uint4(pix, sample, pi.z, nv));
+    } while (false);
+    if (dirtyL) stS(&p.rad[slot], f4(L, 0.0f));
+}
+
 template <int MODEL, bool CAN_GUIDE, bool ENV>
 __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
                                            const Queue &in, const Queue &out, const Queue &shq, uint32_t bid) {
@@ -282,9 +476,8 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
     const uint32_t base = (bid / PG_QSHARDS) * SHADE_BLOCK;
     if (base >= n) return;
     const uint32_t i = base + threadIdx.x;
-    bool alive = false, shadow = false, dirtyL = false;
+    bool alive = false, shadow = false;
     uint32_t slot = 0, rkey = 0;
-    f3 L = mk1(0.f);
     if (i < n) slot = in.items[(size_t)s * in.stride + i];
     // the material table, staged in LDS once per block (the material read sits on the dependent chain
     // hit -> triangle -> material of every shaded vertex); larger tables stay in global memory
@@ -295,191 +488,9 @@ __device__ __forceinline__ void shadeBlock(const GParams &g, const SceneDev &sc,
         for (uint32_t k = threadIdx.x; k < g.num_materials * (uint32_t)(sizeof(GMat) / 16); k += SHADE_BLOCK) smat[k] = src[k];
         __syncthreads();
     }
-    if (i < n) {
-        do {
-            uint4 pi = ldS(&p.pinfo[slot]);
-            const uint32_t pix = pi.x, sample = pi.y;
-            uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16, nv = pi.w;
-            float4 hv = ldS(&p.hit[slot]);
-            float4 T4 = ldS(&p.thr[slot]);
-            float4 L4 = ldS(&p.rad[slot]);
-            f3 T = xyz(T4);
-            L = xyz(L4);
-            float eta = T4.w;
-            uint32_t tri = __float_as_uint(hv.y);
-            if (tri == 0xFFFFFFFFu) break;  // escaped: no environment emitter
-            const uint32_t key = rngKey(pix, g.seed);
-            f3 rd = xyz(ldS(&p.ray_d[slot]));
-            Hit h;
-            fetchHit(sc, tri, hv.z, hv.w, rd, h);
-            f3 Le = mk1(0.f);
-            if (h.emitter >= 0 && dot(h.shN, -rd) > 0) {  // AreaLight::eval (area.cpp)
-                const GEmitter &em = sc.ems[h.emitter];
-                Le = mk(em.radiance[0], em.radiance[1], em.radiance[2]);
-            }
-            // ---- finish the previous bounce: emitter hit by the sampled direction (MIS), then RR
-            if (depth > 1) {
-                if (h.emitter >= 0) {
-                    float4 pv = ldS(&p.prev[slot]);
-                    float lumPdf = 0.0f;
-                    if (g.use_nee && !(flags & PF_PREV_DELTA)) {
-                        f3 prevRefN = xyz(pv);
-                        if (dot(rd, prevRefN) >= 0 && dot(rd, h.shN) < 0) {
-                            const GEmitter &em = sc.ems[h.emitter];
-                            lumPdf = em.inv_area * (hv.x * hv.x) / absDot(rd, h.shN) * (1.0f / (float)g.num_emitters);
-                        }
-                    }
-                    float w = g.use_nee ? miWeight(pv.w, lumPdf) : 1.0f;
-                    L = L + T * Le * w;
-                    dirtyL = true;
-                }
-                if (depth - 1 >= (uint32_t)g.rr_depth) {
-                    float q = fminf(maxc(T) * eta * eta, 0.95f);
-                    if (rng1(key, sample, dimOf(depth - 1, SLOT_RR)) >= q) break;
-                    T = T / q;
-                }
-            }
-            if (depth > g.depth_cap) break;
-            const GMat M = ldsMats ? reinterpret_cast<const GMat *>(smat)[h.mat] : sc.mats[h.mat];
-            if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
-                L = L + T * Le;
-                dirtyL = true;
-            }
-            if ((g.max_depth > 0 && (int)depth >= g.max_depth) ||
-                (g.strict_normals && dot(rd, h.geoN) * h.wi.z >= 0))
-                break;
-            const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
-            const bool guide = CAN_GUIDE && g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
-            const SDView sv = sdv(sd);
-            uint4 meta = make_uint4(0, 0, 0, 0);
-            if (guide) meta = sd.meta[sdLookup(sv, h.p)];
-            // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction):
-            // PG_FRACTION_LEARNED reads the leaf's learned fraction (meta.z; 0 = not learned yet)
-            const float leafAlpha = __uint_as_float(meta.z);
-            const float alpha = g.fraction_bound == PG_FRACTION_LEARNED ? (leafAlpha > 0 ? leafAlpha : g.bsdf_fraction)
-                                                                         : guideFraction(g.fraction_bound, g.bsdf_fraction,
-                                                                                         M.wbound, maxc(T));
-            float pgWo = -1.0f;  // p_guide of the sampled direction at a guided vertex (training record)
-
-            // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow.  With
-            // guiding, the D-tree pdf of the light direction is resolved below, in one lockstep walk
-            // with the direction-sampling descent (sdDual).
-            f3 neeC = mk1(0.f), neeD = mk1(0.f), neeV = mk1(0.f);
-            float neeDist = 0, neeEmPdf = 0, neeBp = 0;
-            bool neePending = false;
-            if (g.use_nee && (M.type & ESmooth)) {
-                float s0, s1;
-                rng2(key, sample, dimOf(depth, SLOT_NEE), s0, s1);
-                float emPdf;
-                f3 value = sampleEmitter<ENV>(g, sc, h.p, refN, s0, s1, neeD, neeDist, emPdf);
-                if (!isZero(value)) {
-                    f3 woL = h.sh.toLocal(neeD);
-                    f3 bsdfVal = bsdfEval<MODEL>(M, h.wi, woL);
-                    if (!isZero(bsdfVal) && (!g.strict_normals || dot(h.geoN, neeD) * woL.z > 0)) {
-                        neeBp = bsdfPdf<MODEL>(M, h.wi, woL);
-                        neeEmPdf = emPdf;
-                        neeV = T * value * bsdfVal;
-                        shadow = true;
-                        if (guide) neePending = true;
-                        else neeC = neeV * miWeight(emPdf, neeBp);
-                    }
-                }
-            }
-
-            // ---- direction sampling: BSDF, or one-sample MIS between BSDF and the D-tree
-            BS bs;
-            f3 weight;
-            float woPdf;
-            bool ok = true;
-            {
-                float b0, b1;
-                rng2(key, sample, dimOf(depth, SLOT_BSDF), b0, b1);
-                float b2 = rng1(key, sample, dimOf(depth, SLOT_COMP));
-                int mode = 0;  // D-tree walk of the sampled direction: 0 none, 1 pdf (BSDF sample), 2 sample
-                float bu = 0, bw = 0;
-                if (!guide) {
-                    weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
-                    woPdf = bs.pdf;
-                } else if (rng1(key, sample, dimOf(depth, SLOT_GUIDE_CHOICE)) < alpha) {
-                    weight = bsdfSample<MODEL>(M, h.wi, b0, b1, b2, bs);
-                    if (isZero(weight)) {
-                        ok = false;
-                    } else {
-                        mode = 1;
-                        dirToCanonical(h.sh.toWorld(bs.wo), bu, bw);
-                    }
-                } else {
-                    mode = 2;
-                    rng2(key, sample, dimOf(depth, SLOT_GUIDE), bu, bw);
-                }
-                if (guide) {
-                    float au = 0, aw = 0, aPdf, dPdf, cu, cv;
-                    if (neePending) dirToCanonical(neeD, au, aw);
-                    sdDual(sv, meta, neePending, au, aw, aPdf, mode != 0, mode == 2, bu, bw, cu, cv, dPdf);
-                    if (neePending) neeC = neeV * miWeight(neeEmPdf, alpha * neeBp + (1 - alpha) * aPdf);
-                    pgWo = dPdf;
-                    if (mode == 1) {
-                        woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
-                        weight = weight * (bs.pdf / woPdf);
-                    } else if (mode == 2) {
-                        f3 dW = canonicalToDir(cu, cv);
-                        f3 woL = h.sh.toLocal(dW);
-                        f3 f = bsdfEval<MODEL>(M, h.wi, woL);
-                        float bp = bsdfPdf<MODEL>(M, h.wi, woL);
-                        woPdf = alpha * bp + (1 - alpha) * dPdf;
-                        if (!(woPdf > 0) || isZero(f)) {
-                            ok = false;
-                        } else {
-                            weight = f / woPdf;
-                            bs.wo = woL;
-                            bs.pdf = bp;
-                            bool refl = h.wi.z * woL.z > 0;
-                            bs.type = refl ? ((M.type & EDiffuseReflection) ? EDiffuseReflection : EGlossyReflection)
-                                           : EGlossyTransmission;
-                            bs.eta = refl ? 1.0f : (h.wi.z > 0 ? M.eta : M.invEta);
-                        }
-                    }
-                }
-            }
-            uint32_t vtxIndex = 0xFFFFFFFFu;
-            if (ok && !isZero(weight)) {
-                if (bs.type != ENull) flags |= PF_SCATTERED;
-                f3 wo = h.sh.toWorld(bs.wo);
-                if (!(g.strict_normals && dot(h.geoN, wo) * bs.wo.z <= 0)) {
-                    f3 Tn = T * weight;
-                    // training vertex: (x, wo, woPdf, T after this bounce, L snapshot)
-                    if (g.record && !(bs.type & EDelta) && nv < (uint32_t)g.max_vertices) {
-                        float cu, cv;
-                        dirToCanonical(wo, cu, cv);
-                        float4 *vb = p.vtx + ((size_t)nv * p.vtxP + slot) * PG_VTX_F4;
-                        stS(vb + 0, f4(h.p, woPdf));
-                        stS(vb + 1, f4(Tn, __uint_as_float(packCanonical(cu, cv))));
-                        stS(vb + 2, f4(L, 0.0f));
-                        stS(vb + 3, f4(T, guide ? pgWo : -1.0f));
-                        vtxIndex = nv;
-                        nv++;
-                    }
-                    float tmin = kEpsilon * fmaxf(fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z)), kEpsilon);
-                    stS(&p.ray_o[slot], f4(h.p, tmin));
-                    stS(&p.ray_d[slot], f4(wo, __int_as_float(0x7f800000)));
-                    stS(&p.thr[slot], f4(Tn, eta * bs.eta));
-                    stS(&p.prev[slot], f4(refN, woPdf));
-                    flags = (flags & ~(PF_EMITTED_QUERY | PF_PREV_DELTA)) | ((bs.type & EDelta) ? PF_PREV_DELTA : 0u);
-                    stS(&p.pinfo[slot], make_uint4(pix, sample, (depth + 1) | (flags << 16), nv));
-                    alive = true;
-                    if (out.keys) rkey = rayOrderKey(sd, h.p, wo);
-                }
-            }
-            if (shadow) {
-                float tmin = kEpsilon * fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z));
-                stS(&p.sh_o[slot], f4(h.p, tmin));
-                stS(&p.sh_d[slot], f4(neeD, neeDist * (1 - kShadowEpsilon)));
-                stS(&p.sh_c[slot], f4(neeC, __uint_as_float(vtxIndex)));
-            }
-            if (!alive && nv != pi.w) stS(&p.pinfo[slot], make_uint4(pix, sample, pi.z, nv));
-        } while (false);
-        if (dirtyL) stS(&p.rad[slot], f4(L, 0.0f));
-    }
+    if (i < n)
+        shadeOne<MODEL, CAN_GUIDE, ENV>(g, sc, sd, p, slot, ldsMats ? reinterpret_cast<const GMat *>(smat) : sc.mats,
+                                        out.keys != nullptr, alive, shadow, rkey);
     if (out.keys)
         waveAppendKey(alive, slot, (uint16_t)rkey, out.items + (size_t)s * out.stride, out.keys + (size_t)s * out.stride,
                       out.counts + s);
@@ -585,6 +596,97 @@ __global__ __launch_bounds__(256) void k_rsort_scatter(Queue q, uint32_t *hist, 
     for (int j = 0; j < PER; ++j) {
         const uint32_t i = b0 + threadIdx.x + 256u * j;
         if (i < e) out[cnt[key[j]] + rank[j]] = items[i];
+    }
+}
+
+// ---- the tail of a chunk: once few paths are alive, the host stops the per-bounce launches and
+// count readbacks and one launch finishes every remaining path, each thread looping shade (the
+// class's specialised body) -> shadow ray -> closest hit until its path ends.  Every step is the
+// wavefront's own code on the path's own state and random numbers, in the same order (a path's NEE
+// is added before its next vertex is shaded), so films, records and trees are bit-identical with
+// the bounce-by-bounce loop.  Input: the queue of the bounce just traced (hits already in p.hit).
+// stats: [0] traced segments, [1] escaped segments, [2] shadow rays (u64, device atomics).
+template <bool ENV>
+__device__ __forceinline__ void tailShade(const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
+                                          uint32_t slot, uint32_t tri, bool &alive, bool &shadow) {
+    uint32_t rk = 0;
+    switch (sc.tclass[tri]) {
+        case PG_CLASS_DIFFUSE: shadeOne<PG_BSDF_DIFFUSE, true, ENV>(g, sc, sd, p, slot, sc.mats, false, alive, shadow, rk); break;
+        case PG_CLASS_ROUGHCONDUCTOR:
+            shadeOne<PG_BSDF_ROUGHCONDUCTOR, true, ENV>(g, sc, sd, p, slot, sc.mats, false, alive, shadow, rk);
+            break;
+        case PG_CLASS_ROUGHDIELECTRIC:
+            shadeOne<PG_BSDF_ROUGHDIELECTRIC, true, ENV>(g, sc, sd, p, slot, sc.mats, false, alive, shadow, rk);
+            break;
+        case PG_CLASS_PLASTIC: shadeOne<PG_BSDF_PLASTIC, false, ENV>(g, sc, sd, p, slot, sc.mats, false, alive, shadow, rk); break;
+        case PG_CLASS_ROUGHPLASTIC:
+            shadeOne<PG_BSDF_ROUGHPLASTIC, true, ENV>(g, sc, sd, p, slot, sc.mats, false, alive, shadow, rk);
+            break;
+        default: shadeOne<-1, false, ENV>(g, sc, sd, p, slot, sc.mats, false, alive, shadow, rk);
+    }
+}
+template <bool ENV>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_tail(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue q,
+                                                      unsigned long long *stats) {
+    __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
+    const TStack stk = threadStack(stack, p.stack_ovf);
+    const WStack wstk = threadWideStack(stack, p.stack_ovf);
+    const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
+    const uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x;
+    uint32_t segs = 0, esc = 0, shadows = 0;
+    if (i < q.counts[s]) {
+        const uint32_t slot = q.items[(size_t)s * q.stride + i];
+        uint32_t tri = __float_as_uint(ldS(&p.hit[slot]).y);
+        while (tri != 0xFFFFFFFFu) {
+            bool alive = false, shadow = false;
+            tailShade<ENV>(g, sc, sd, p, slot, tri, alive, shadow);
+            if (shadow) {  // shadowRows for this path
+                ++shadows;
+                const float4 o = ldS(&p.sh_o[slot]), d = ldS(&p.sh_d[slot]);
+                float tmax = d.w, u, v;
+                uint32_t t2 = 0xFFFFFFFFu;
+                if (!traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), o.w, tmax, t2, u, v, wstk)) {
+                    const float4 c = ldS(&p.sh_c[slot]);
+                    const float4 L = ldS(&p.rad[slot]);
+                    stS(&p.rad[slot], make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w));
+                    const uint32_t vi = __float_as_uint(c.w);
+                    if (vi != 0xFFFFFFFFu) {
+                        float4 *vl = p.vtx + ((size_t)vi * p.vtxP + slot) * PG_VTX_F4 + 2;
+                        const float4 a = *vl;
+                        *vl = make_float4(a.x + c.x, a.y + c.y, a.z + c.z, a.w);
+                    }
+                }
+            }
+            if (!alive) break;
+            // traceRows for this path
+            const float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.ray_d[slot]);
+            float tmax = d.w, u = 0, v = 0;
+            tri = 0xFFFFFFFFu;
+            const bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+            float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
+            if (ENV && !h) {
+                const f3 e = envEscapeRadiance(g, sc, p, slot, xyz(d));
+                hr = make_float4(e.x, hr.y, e.y, e.z);
+            }
+            stS(&p.hit[slot], hr);
+            ++segs;
+            if (!h) {
+                ++esc;
+                tri = 0xFFFFFFFFu;
+            }
+        }
+    }
+    // wave-summed counters
+    unsigned long long a = segs, b = esc, c = shadows;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+        c += __shfl_xor(c, off);
+    }
+    if ((threadIdx.x & 63) == 0 && (a | b | c)) {
+        atomicAdd(stats + 0, a);
+        atomicAdd(stats + 1, b);
+        atomicAdd(stats + 2, c);
     }
 }
 
@@ -975,6 +1077,13 @@ void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue
     if (!max_shard) return;
     hipLaunchKernelGGL(k_shadow, shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS), dim3(TRACE_BLOCK), 0,
                        s, sc, p, q);
+}
+void pg_launch_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p, Queue q,
+                    uint32_t max_shard, unsigned long long *stats) {
+    if (!max_shard) return;
+    const dim3 grid(PG_QSHARDS * blocks(max_shard, TRACE_BLOCK));
+    if (sc.env) hipLaunchKernelGGL(k_tail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, sd, p, q, stats);
+    else hipLaunchKernelGGL(k_tail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, sd, p, q, stats);
 }
 void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist) {
     if (!max_shard) return;

@@ -322,6 +322,7 @@ class ProgressivePathTracer:
             distance_guiding=float(props.get("distanceGuiding", 0.25)),
             aovs=int(bool(props.get("aovs", False))),
             volpath_exact_mis=int(bool(props.get("exactMis", False))),
+            tail_paths=int(props.get("tailPaths", 0)),
             bsdf_fraction_bound=_FRACTION_BOUNDS[str(props.get("bsdfSamplingFractionBound", "fixed")).lower()])
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         # maxRenderTime (progressiveintegrator.cpp:296-300): > 0 renders whole progressions until this
