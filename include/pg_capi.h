@@ -236,6 +236,12 @@ typedef struct pg_config {
                                      (k_tail: each thread loops shade -> shadow -> closest hit) instead of one
                                      launch pair + count readback per bounce; bit-identical results.  0 = the
                                      default (65536, or the PG_TAIL_PATHS environment variable), < 0 = off. */
+    int32_t glossy_prior;         /* guided path integrator: 1 = the BSDF's glossy sampling rate r
+                                     (BSDF::getGlossySamplingRate, bsdf.h:365-381: 1 for roughconductor and
+                                     roughdielectric, the glossy lobe's probability for roughplastic,
+                                     roughplastic.cpp:323-345, 0 otherwise) raises the vertex's BSDF fraction
+                                     to r + (1 - r) alpha; vertices with r = 1 are not guided, and only vertices
+                                     with r = 0 feed the learned-fraction statistics.  0 = off (Mueller 2017). */
 } pg_config;
 enum { PG_FRACTION_FIXED = 0, PG_FRACTION_ALBEDO = 1, PG_FRACTION_THROUGHPUT = 2, PG_FRACTION_LEARNED = 3 };
 enum { PG_INTEGRATOR_PATH = 0, PG_INTEGRATOR_VOLPATH = 1 };

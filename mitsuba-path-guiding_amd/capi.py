@@ -87,7 +87,7 @@ class pg_config(C.Structure):
                 ("path_lanes", C.c_int32), ("integrator", C.c_int32), ("volume_majorant", C.c_int32),
                 ("distance_guiding", C.c_float), ("aovs", C.c_int32), ("bsdf_fraction_bound", C.c_int32),
                 ("kernel_timing", C.c_int32), ("volpath_exact_mis", C.c_int32),
-                ("tail_paths", C.c_int32)]
+                ("tail_paths", C.c_int32), ("glossy_prior", C.c_int32)]
 
 
 class pg_record(C.Structure):
@@ -134,6 +134,7 @@ def default_config(**overrides):
     c.kernel_timing = 0
     c.volpath_exact_mis = 0
     c.tail_paths = 0
+    c.glossy_prior = 0
     for k, v in overrides.items():
         if not hasattr(c, k):
             raise AttributeError(f"pg_config has no field {k!r}")

@@ -657,6 +657,20 @@ PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
     }
 }
 
+// BSDF::getGlossySamplingRate (bsdf.h:365-381; roughplastic.cpp:323-345; twosided.cpp:221-235): 1 for
+// the all-glossy models, the glossy lobe's sampling probability for roughplastic, 0 for the rest (the
+// delta models are never guided).  pg_config.glossy_prior; oracle glossyRate (orc_bsdf.h).
+template <int MODEL = -1>
+PGD float glossyRate(const GMat &M, float cosThetaI) {
+    switch (MODEL >= 0 ? MODEL : (int)M.model) {
+        case PG_BSDF_ROUGHCONDUCTOR:
+        case PG_BSDF_ROUGHDIELECTRIC: return 1.0f;
+        case PG_BSDF_ROUGHPLASTIC:
+            return roughPlasticProbSpec(M, (M.flags & PG_MAT_TWOSIDED) ? fabsf(cosThetaI) : cosThetaI);
+        default: return 0.0f;
+    }
+}
+
 // twosided adapter (twosided.cpp:116-190)
 template <int MODEL = -1>
 PGD f3 bsdfEval(const GMat &M, f3 wi, f3 wo) {

@@ -643,6 +643,7 @@ pg_status pg_config_default(pg_config *c) {
     c->kernel_timing = 0;
     c->volpath_exact_mis = 0;
     c->tail_paths = 0;
+    c->glossy_prior = 0;
     return PG_OK;
 }
 
@@ -1235,6 +1236,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     g.max_component_value = c->cfg.max_component_value;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
     g.fraction_bound = c->cfg.bsdf_fraction_bound;
+    g.glossy_prior = c->cfg.glossy_prior;
     g.seed = c->cfg.seed;
     g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
     const SceneDev sc = sceneView(c);

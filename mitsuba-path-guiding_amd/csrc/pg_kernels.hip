@@ -333,16 +333,22 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
             (g.strict_normals && dot(rd, h.geoN) * h.wi.z >= 0))
             break;
         const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
-        const bool guide = CAN_GUIDE && g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta);
+        // glossy prior (pg_config.glossy_prior): r = BSDF::getGlossySamplingRate; r = 1 is not guided
+        const float gRate = (CAN_GUIDE && g.glossy_prior) ? glossyRate<MODEL>(M, h.wi.z) : 0.0f;
+        const bool guide = CAN_GUIDE && g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta) && gRate < 1.0f;
         const SDView sv = sdv(sd);
         uint4 meta = make_uint4(0, 0, 0, 0);
         if (guide) meta = sd.meta[sdLookup(sv, h.p)];
         // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction):
         // PG_FRACTION_LEARNED reads the leaf's learned fraction (meta.z; 0 = not learned yet)
         const float leafAlpha = __uint_as_float(meta.z);
-        const float alpha = g.fraction_bound == PG_FRACTION_LEARNED ? (leafAlpha > 0 ? leafAlpha : g.bsdf_fraction)
-                                                                     : guideFraction(g.fraction_bound, g.bsdf_fraction,
-                                                                                     M.wbound, maxc(T));
+        float alpha = g.fraction_bound == PG_FRACTION_LEARNED ? (leafAlpha > 0 ? leafAlpha : g.bsdf_fraction)
+                                                               : guideFraction(g.fraction_bound, g.bsdf_fraction,
+                                                                               M.wbound, maxc(T));
+        if (gRate > 0.0f) {
+#pragma clang fp contract(off)
+            alpha = gRate + (1.0f - gRate) * alpha;
+        }
         float pgWo = -1.0f;  // p_guide of the sampled direction at a guided vertex (training record)
 
         // ---- NEE (progressive_path.cpp:193-219); the shadow ray is deferred to k_shadow.  With
@@ -439,7 +445,8 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
                     stS(vb + 0, f4(h.p, woPdf));
                     stS(vb + 1, f4(Tn, __uint_as_float(packCanonical(cu, cv))));
                     stS(vb + 2, f4(L, 0.0f));
-                    stS(vb + 3, f4(T, guide ? pgWo : -1.0f));
+                    // learned-fraction statistics only from vertices whose fraction is the leaf's (r = 0)
+                    stS(vb + 3, f4(T, guide && gRate == 0.0f ? pgWo : -1.0f));
                     vtxIndex = nv;
                     nv++;
                 }

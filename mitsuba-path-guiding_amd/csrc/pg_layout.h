@@ -147,4 +147,5 @@ struct GParams {
     uint32_t seed, num_emitters, num_materials, depth_cap;  // num_emitters counts the environment emitter
     int32_t fraction_bound;  // pg_config.bsdf_fraction_bound (PG_FRACTION_*)
     int32_t exact_mis;       // pg_config.volpath_exact_mis
+    int32_t glossy_prior;    // pg_config.glossy_prior
 };

@@ -323,6 +323,7 @@ class ProgressivePathTracer:
             aovs=int(bool(props.get("aovs", False))),
             volpath_exact_mis=int(bool(props.get("exactMis", False))),
             tail_paths=int(props.get("tailPaths", 0)),
+            glossy_prior=int(bool(props.get("glossyPrior", False))),
             bsdf_fraction_bound=_FRACTION_BOUNDS[str(props.get("bsdfSamplingFractionBound", "fixed")).lower()])
         self.spp_per_progression = int(props.get("samplesPerProgression", 1))
         # maxRenderTime (progressiveintegrator.cpp:296-300): > 0 renders whole progressions until this

@@ -53,6 +53,10 @@ public:
         // volpath: MIS of emitters behind index-matched surfaces with the whole ray length (unbiased)
         // instead of the reference's last segment
         m_cfg.volpath_exact_mis = props.getBoolean("exactMis", false);
+        // a chunk with at most this many live paths finishes in one launch (k_tail); 0 = library default
+        m_cfg.tail_paths = props.getInteger("tailPaths", 0);
+        // BSDF::getGlossySamplingRate as a prior on the BSDF fraction (glossy lobes are not guided)
+        m_cfg.glossy_prior = props.getBoolean("glossyPrior", m_cfg.glossy_prior != 0);
         std::string bound = boost::to_lower_copy(props.getString("bsdfSamplingFractionBound", "fixed"));
         m_cfg.bsdf_fraction_bound = bound == "albedo" ? PG_FRACTION_ALBEDO : bound == "learned" ? PG_FRACTION_LEARNED
                                     : bound == "throughput" ? PG_FRACTION_THROUGHPUT : PG_FRACTION_FIXED;

@@ -82,11 +82,15 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
             break;
 
         V3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? its.sh.n : V3(0.f);
-        const bool guidable = guiding && (M.type & ESmooth) && !(M.type & EDelta);
+        // glossy prior (pg_config.glossy_prior): vertices with glossy rate r = 1 are not guided, the rest
+        // sample the BSDF with probability r + (1 - r) alpha
+        const float gRate = cfg.glossy_prior ? glossyRate(M, its.wi.z) : 0.0f;
+        const bool guidable = guiding && (M.type & ESmooth) && !(M.type & EDelta) && gRate < 1.0f;
         const DTreeW *dt = guidable ? &tree->dtrees[tree->lookup(its.p)] : nullptr;
-        const float alpha = cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED
-                                ? ((dt && dt->alpha > 0) ? dt->alpha : cfg.bsdf_sampling_fraction)
-                                : guideFraction(cfg.bsdf_fraction_bound, cfg.bsdf_sampling_fraction, M, maxc(T));
+        float alpha = cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED
+                          ? ((dt && dt->alpha > 0) ? dt->alpha : cfg.bsdf_sampling_fraction)
+                          : guideFraction(cfg.bsdf_fraction_bound, cfg.bsdf_sampling_fraction, M, maxc(T));
+        if (gRate > 0.0f) alpha = gRate + (1.0f - gRate) * alpha;
         float pgWo = -1.0f;  // p_guide of the sampled direction (guided vertex)
 
         // ---- direct illumination (NEE)
@@ -164,7 +168,7 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
             vtx[nv].Lat = L;
             vtx[nv].woPdf = woPdf;
             vtx[nv].Tpre = T;
-            vtx[nv].pg = dt ? pgWo : -1.0f;
+            vtx[nv].pg = dt && gRate == 0.0f ? pgWo : -1.0f;  // learned statistics: r = 0 vertices only
             nv++;
         }
 

@@ -396,6 +396,17 @@ inline V3 sample1(const Material &M, V3 wi, float u0, float u1, float u2, BSampl
 
 }  // namespace detail
 
+// BSDF::getGlossySamplingRate (bsdf.h:365-381; roughplastic.cpp:323-345; twosided.cpp:221-235): 1 for
+// all-glossy models, the glossy lobe's probability for roughplastic, else 0 (kernels: glossyRate)
+inline float glossyRate(const Material &M, float cosThetaI) {
+    switch (M.m.type) {
+        case PG_BSDF_ROUGHCONDUCTOR:
+        case PG_BSDF_ROUGHDIELECTRIC: return 1.0f;
+        case PG_BSDF_ROUGHPLASTIC: return detail::roughPlasticProbSpec(M, M.twosided() ? std::fabs(cosThetaI) : cosThetaI);
+        default: return 0.0f;
+    }
+}
+
 // ---- public interface with the twosided adapter -------------------------------------------
 inline V3 bsdfEval(const Material &M, V3 wi, V3 wo) {
     if (M.twosided() && !(wi.z > 0)) {

@@ -11,7 +11,7 @@ world = int(sys.argv[1]) if len(sys.argv) > 1 else 1  # emulate rank 0 of `world
 integ = GuidedPathTracer({"trainingIterations": 5, "samplesPerProgression": 1024}, rank=0, world_size=world)
 integ.preprocess(sc)
 d = integ.dev
-for rep in range(2):
+for rep in range(int(os.environ.get("PG_TRAIN_REPS", 2))):
     T = {}
     def tm(k, f, *a, **kw):
         t = time.perf_counter(); r = f(*a, **kw); T[k] = T.get(k, 0) + time.perf_counter() - t; return r
@@ -24,7 +24,8 @@ for rep in range(2):
         tm(f"splat{it}", d.splat_local)
         tm(f"refit{it}", d.refit, it)
     tm("reset_film", d.reset_film)
-    tm("final", d.render_pass, 1024, off, False)
+    if not os.environ.get("PG_TRAIN_ONLY"):
+        tm("final", d.render_pass, 1024, off, False)
     print(f"world {world} rep {rep}: total {time.perf_counter()-t0:.3f} s  " + "  ".join(f"{k} {v*1e3:.1f}" for k, v in T.items()), flush=True)
     st = d.stats()
     print("  stree", st["stree_nodes"], "dtree", st["dtree_nodes"], flush=True)
