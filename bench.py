@@ -283,7 +283,8 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
     from mitsuba_path_guiding_amd.integrator import Device
     cfg = pg.capi.default_config(guiding=1, device=local, path_lanes=1, kernel_timing=1, rank=integ.dev.cfg.rank,
                                  world_size=integ.dev.cfg.world_size,
-                                 bsdf_fraction_bound=integ.cfg.bsdf_fraction_bound)
+                                 bsdf_fraction_bound=integ.cfg.bsdf_fraction_bound,
+                                 glossy_prior=integ.cfg.glossy_prior)
     dev = Device(cfg)
     dev.upload(scene)
     dev.put_sdtree(integ.dev.get_sdtree())
@@ -303,7 +304,12 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
                    + d["shadow_rays"] * BYTES_SHADOW_PER_RAY, d["rays_launches"]),
     }
     dev.close()
-    dom = max(kernels, key=lambda k: kernels[k][0])
+    # the HBM roofline is reported for the shipped kernel that carries the most algorithmic bytes
+    # (the shading launch: ~70 % of SURVEY §8d's 420 B per segment); the traversal launches (k_rays,
+    # k_trace) are latency-bound gathers of cache-resident BVH nodes, excluded from the byte model by
+    # §8d, and are listed under "kernels" with their own time share and fraction
+    dom = max(kernels, key=lambda k: kernels[k][1])
+    total_ms = sum(v[0] for v in kernels.values()) or 1.0
     ms, nbytes, launches = kernels[dom]
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     per_launch = nbytes / max(launches, 1)
@@ -323,7 +329,9 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
         e = {"ms": round(v[0], 2), "launches": int(v[2]),
              "algorithmic_bytes_per_launch": int(v[1] / max(v[2], 1)),
              "avg_launch_ms": round(v[0] / max(v[2], 1), 4),
-             "achieved_gbs": round(v[1] / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else 0.0}
+             "time_share": round(v[0] / total_ms, 3),
+             "achieved_gbs": round(v[1] / (v[0] / 1e3) / 1e9, 2) if v[0] > 0 else 0.0,
+             "frac": round(v[1] / (v[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if v[0] > 0 else 0.0}
         t = measured.get(k, {}).get("hbm_bytes_per_launch")
         if t and v[2]:
             e["traffic_bytes_per_launch"] = t
@@ -332,7 +340,8 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
             "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
-            "kernel": dom, "algorithmic_bytes_per_launch": int(per_launch),
+            "kernel": dom, "dominant_by": "algorithmic bytes per pass (time shares under kernels)",
+            "algorithmic_bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(ms / max(launches, 1), 4),
             "bytes_model": {"k_trace": f"{BYTES_TRACE_PER_RAY} B/camera ray",
                             shade_name: f"{BYTES_SHADE_PER_VERTEX} B/shaded vertex (+{BYTES_SHADE_RECORD} B when "
@@ -407,11 +416,14 @@ def quality_block(pg, scene, final, job_s, a):
     dev.upload(scene)
     dev.render_pass(a.spp, 0)  # warm-up + equal-spp image (independent of the guided streams' offsets)
     ug = image(dev.read_film()[0])
-    dev.reset_film()
-    t = time.perf_counter()
-    dev.render_pass(a.spp, 0)
-    dev.read_film()
-    rate = a.spp / (time.perf_counter() - t)
+    best = float("inf")  # best of two warm runs, like the timed job's steady state
+    for _ in range(2):
+        dev.reset_film()
+        t = time.perf_counter()
+        dev.render_pass(a.spp, 0)
+        dev.read_film()
+        best = min(best, time.perf_counter() - t)
+    rate = a.spp / best
     out["unguided_equal_spp"] = dict(errors(ug, gt), spp=a.spp)
     spp_eq = max(1, int(round(job_s * rate)))
     dev.reset_film()

@@ -7,6 +7,7 @@
 // contribution).  Camera rays, film accumulation, record commit and SD-tree splat are separate
 // kernels.  Path state is SoA float4/uint4 arrays indexed by path slot.
 #include <algorithm>
+#include <cstdlib>
 
 #include "pg_trace.h"
 
@@ -907,6 +908,110 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
     waveKeyedFracAdd(sd.frac, dt, w, pb, pg, q0, stat);
 }
 
+// Block-private splat (PG_SPLAT_LDS, default): a grid of at most ~1k blocks walks the records in
+// block-strided rounds and sums the per-D-tree record counts and per-leaf-quadrant fixed-point values
+// in two LDS hash tables (open addressing, 8 probes); keys that find no slot go straight to the global
+// atomics.  Each block then adds its table entries to the global sums once.  A hot D-tree (one near
+// the camera gets ~10 % of an iteration's records) thus costs one global atomic per block instead of
+// one per wave.  Integer sums: the trees are bit-identical to the wave-aggregated k_splat.
+#define SPLAT_CNT_SLOTS 512
+#define SPLAT_SUM_SLOTS 2048
+#define SPLAT_EMPTY 0xFFFFFFFFu
+__device__ __forceinline__ bool ldsTableAdd(uint32_t *keys, unsigned long long *vals, uint32_t mask, uint32_t key,
+                                            unsigned long long v) {
+    uint32_t h = (key * 2654435761u) >> 7;
+    for (int probe = 0; probe < 8; ++probe, ++h) {
+        h &= mask;
+        uint32_t k = __atomic_load_n(&keys[h], __ATOMIC_RELAXED);
+        if (k == SPLAT_EMPTY) k = atomicCAS(&keys[h], SPLAT_EMPTY, key);
+        if (k == SPLAT_EMPTY || k == key) {
+            atomicAdd(&vals[h], v);
+            return true;
+        }
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(256) void k_splat_lds(SDDev sd, const pg_record *__restrict__ recs, unsigned long long n) {
+    __shared__ uint32_t ckey[SPLAT_CNT_SLOTS], skey[SPLAT_SUM_SLOTS];
+    __shared__ unsigned long long cval[SPLAT_CNT_SLOTS], sval[SPLAT_SUM_SLOTS];
+    for (uint32_t e = threadIdx.x; e < SPLAT_SUM_SLOTS; e += blockDim.x) {
+        skey[e] = SPLAT_EMPTY;
+        sval[e] = 0;
+        if (e < SPLAT_CNT_SLOTS) {
+            ckey[e] = SPLAT_EMPTY;
+            cval[e] = 0;
+        }
+    }
+    __syncthreads();
+    const SDView sv = sdv(sd);
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    // uniform trip count per block (waveKeyedFracAdd needs the whole wave)
+    for (unsigned long long base = (unsigned long long)blockIdx.x * blockDim.x; base < n; base += stride) {
+        const unsigned long long i = base + threadIdx.x;
+        bool valid = i < n, found = false;
+        unsigned long long fx = 0;
+        uint32_t dt = 0, slot = 0;
+        float4 b = make_float4(0, 0, 0, 0);
+        if (valid) {
+            const float4 *src = reinterpret_cast<const float4 *>(recs + i);
+            const float4 a = src[0];
+            b = src[1];
+            const float woPdf = b.y;
+            float val = 0.0f;
+            {
+#pragma clang fp contract(off)
+                if (woPdf > 0) val = b.x / woPdf;
+            }
+            valid = woPdf > 0 && val >= 0 && val < 1e30f;
+            if (valid) {
+                float s = val * 16777216.0f;
+                if (s >= 281474976710656.0f) s = 281474976710656.0f;  // cap 2^48, as k_splat
+                fx = (unsigned long long)s;
+                dt = sdLookup(sv, mk(a.x, a.y, a.z));
+                const uint32_t dirw = __float_as_uint(a.w);
+                float u = ((float)(dirw & 0xFFFFu) + 0.5f) * (1.0f / 65536.0f);
+                float v = ((float)(dirw >> 16) + 0.5f) * (1.0f / 65536.0f);
+                uint32_t node = sd.meta[dt].y;
+                for (int guard = 0; guard < 64; ++guard) {
+                    const int q = childIndex(u, v);
+                    const uint32_t c = c4(sd.bchild[node], q);
+                    if (c == 0) {
+                        slot = 4 * node + q;
+                        found = true;
+                        break;
+                    }
+                    node = c;
+                }
+            }
+        }
+        if (valid && !ldsTableAdd(ckey, cval, SPLAT_CNT_SLOTS - 1, dt, 1ull)) atomicAdd(sd.count + dt, 1ull);
+        if (found && fx && !ldsTableAdd(skey, sval, SPLAT_SUM_SLOTS - 1, slot, fx)) atomicAdd(sd.bsum + slot, fx);
+        if (sd.learned) {  // learned-fraction statistics as in k_splat (wave-aggregated global atomics)
+            bool stat = false;
+            float w = 0, pb = 0, pg = 0, q0 = 0;
+            if (valid) {
+                pg = b.w;
+                w = b.z;
+                q0 = b.y;
+                if (pg >= 0.0f && w > 0.0f && w < 1e30f) {
+#pragma clang fp contract(off)
+                    const float la = __uint_as_float(sd.meta[dt].z);
+                    const float a0 = la > 0 ? la : sd.alpha0;
+                    pb = fmaxf((q0 - (1.0f - a0) * pg) / a0, 0.0f);
+                    stat = true;
+                }
+            }
+            waveKeyedFracAdd(sd.frac, dt, w, pb, pg, q0, stat);
+        }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < SPLAT_SUM_SLOTS; e += blockDim.x) {
+        if (skey[e] != SPLAT_EMPTY && sval[e]) atomicAdd(sd.bsum + skey[e], sval[e]);
+        if (e < SPLAT_CNT_SLOTS && ckey[e] != SPLAT_EMPTY) atomicAdd(sd.count + ckey[e], cval[e]);
+    }
+}
+
 // ---- unit-level kernels used by the parity tests ---------------------------------------------
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const float *__restrict__ rays, uint32_t n,
                                                             int any, float *__restrict__ hits, uint32_t *ovf) {
@@ -1148,7 +1253,16 @@ void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_
 }
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n) {
     if (!n) return;
-    hipLaunchKernelGGL(k_splat, dim3(blocks(n, 256)), dim3(256), 0, s, sd, recs, n);
+    static const bool lds = [] {
+        const char *e = std::getenv("PG_SPLAT_LDS");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (lds) {  // ~16 records per thread, at most 1024 blocks (4 per CU)
+        const unsigned long long nb = std::min<unsigned long long>(1024, std::max<unsigned long long>(1, n / 4096));
+        hipLaunchKernelGGL(k_splat_lds, dim3((uint32_t)nb), dim3(256), 0, s, sd, recs, n);
+    } else {
+        hipLaunchKernelGGL(k_splat, dim3(blocks(n, 256)), dim3(256), 0, s, sd, recs, n);
+    }
 }
 void pg_launch_trace_rays(hipStream_t s, const SceneDev &sc, const float *rays, uint32_t n, int any, float *hits,
                           uint32_t *ovf) {

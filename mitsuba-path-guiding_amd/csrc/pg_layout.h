@@ -65,7 +65,9 @@ static_assert(sizeof(GEnv) == 128, "GEnv layout");
 // With PG_DENSITY_BRICKS = 1 the density is stored in 4x4x4-voxel bricks of 256 B (bricks x fastest,
 // bx * by bricks per z layer; inside a brick x, then y, then z): the 2x2x2 corners of a trilinear
 // lookup then touch ~2.3 cache lines instead of 4 rows of the linear layout.
-#define PG_MAJORANT_CELL 8
+#ifndef PG_MAJORANT_CELL
+#define PG_MAJORANT_CELL 8  // voxels per majorant cell and axis (oracle: orc_medium.h kCell)
+#endif
 #ifndef PG_DENSITY_BRICKS
 #define PG_DENSITY_BRICKS 0  // measured: no gain over the linear layout (DESIGN.md "Volumes")
 #endif

@@ -398,10 +398,12 @@ def cornell(width=512, height=512, short_material=None, tall_material=None):
 # y up in [0, 3]; z in [0, 5].  Doorway in the separating wall at z in [2.0, 3.0], y < 2.2; the
 # door is hinged at (5.0, z=2.0) and opened by `door_deg` into room A: light reaches room A only
 # through the narrow gap.  The only emitter is a ceiling panel in room B.
-def ajar_door(width=1280, height=720, door_deg=7.0, sphere_res=(96, 48), seed=7):
+def ajar_door(width=1280, height=720, door_deg=7.0, sphere_res=(96, 48), seed=7, diffuse_objects=False):
+    """diffuse_objects: the table, spheres, torus and pebbles diffuse (grey 0.5) instead of rough
+    metals and glass -- the camera room is then lit only indirectly, without specular chains."""
     rng = np.random.default_rng(seed)
     s = Scene()
-    s.name = "ajar_door"
+    s.name = "ajar_diffuse" if diffuse_objects else "ajar_door"
     wallm = s.add_material(material("diffuse", reflectance=(0.6, 0.58, 0.55)))
     floorm = s.add_material(material("diffuse", reflectance=(0.35, 0.28, 0.22)))
     doorm = s.add_material(material("diffuse", reflectance=(0.45, 0.40, 0.35), twosided=True))
@@ -411,6 +413,8 @@ def ajar_door(width=1280, height=720, door_deg=7.0, sphere_res=(96, 48), seed=7)
     glass = s.add_material(material("dielectric", int_ior=1.5, ext_ior=1.0))
     rglass = s.add_material(material("roughdielectric", int_ior=1.5, ext_ior=1.0, alpha=0.2, distribution="ggx"))
     lightm = s.add_material(material("diffuse", reflectance=(0.0, 0.0, 0.0)))
+    if diffuse_objects:
+        tablem = cu = au = glass = rglass = s.add_material(material("diffuse", reflectance=(0.5, 0.5, 0.5)))
     H = 3.0
     xa, xw, xb, Z = 5.0, 5.15, 9.0, 5.0
     ins_a = (2.5, 1.5, 2.5)
@@ -665,4 +669,5 @@ def smoke(width=1024, height=1024, res=256, seed=7, scale=40.0, albedo=0.9, g=0.
     return s.finalize()
 
 
-SCENES = {"cornell": cornell, "ajar_door": ajar_door, "kitchen": kitchen, "smoke": smoke, "sky_courtyard": sky_courtyard}
+SCENES = {"cornell": cornell, "ajar_door": ajar_door,
+          "ajar_diffuse": lambda w=1280, h=720: ajar_door(w, h, diffuse_objects=True), "kitchen": kitchen, "smoke": smoke, "sky_courtyard": sky_courtyard}
