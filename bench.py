@@ -76,7 +76,9 @@ def parse():
                     help="launcher self-test: every rank joins the process group and reports (rank, world); no GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU budget of the final-render sample")
     ap.add_argument("--quick", action="store_true", help="small smoke configuration (not a bench line)")
-    ap.add_argument("--props", default="{}", help="extra integrator properties (JSON), for A/B runs")
+    ap.add_argument("--props", default=None,
+                    help="integrator properties (JSON); default: the guided configuration DESIGN.md §8a measured best "
+                         "on C3 (albedo-bounded BSDF fraction + glossy prior)")
     return ap.parse_args()
 
 
@@ -169,6 +171,8 @@ def main():
         exchange = None
     # one progression for the final render (the device chunks it into 2^25-path chunks, 3 in flight)
     Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
+    if a.props is None:
+        a.props = "{}" if vol else json.dumps(BENCH_GUIDING)
     integ = Tracer({"trainingIterations": a.train, "samplesPerProgression": a.spp, "pathLanes": a.lanes,
                     "maxPathsInFlight": a.paths_in_flight, **json.loads(a.props)}, device=device,
                    rank=rank, world_size=world, exchange=exchange,
@@ -256,6 +260,7 @@ def main():
                                    f"iterations (1..{2 ** (a.train - 1)} spp) + {a.spp} spp render",
                        "scene": a.scene, "triangles": scene.num_triangles, "width": a.width, "height": a.height,
                        "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
+                       "integrator_props": json.loads(a.props),
                        "parallelism": f"tile-shard x{world}, RCCL {a.exchange} per training iteration"
                                       + (", film reduce to rank 0" if world > 1 else "")},
             "roofline": roofline,
@@ -269,6 +274,11 @@ def main():
     integ.postprocess()
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+# C3's guided configuration: the BSDF-sampling fraction bounded below by the BSDF's
+# albedo, and the glossy prior (BSDF::getGlossySamplingRate) -- rough metals and glass are not guided
+BENCH_GUIDING = {"bsdfSamplingFractionBound": "albedo", "glossyPrior": True}
 
 
 def kernel_roofline(pg, scene, integ, local, a, spp=32):

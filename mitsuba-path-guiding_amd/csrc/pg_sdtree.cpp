@@ -52,9 +52,12 @@ uint64_t propagate(std::vector<SdNodeB> &b, uint32_t n) {
 // exceeds rho, below max_depth; quadrants of leaves keep refining with sum/4 estimates.
 void rebuildTopology(SdLeaf &L, int maxDepth, float rho) {
     struct Tmp { float s[4]; uint32_t c[4]; };
-    std::vector<Tmp> nodes(1, Tmp{{0, 0, 0, 0}, {0, 0, 0, 0}});
     struct Item { uint32_t dst; uint32_t src; bool prev; int depth; };
-    std::vector<Item> stack{{0, 0, true, 1}};
+    // per-thread scratch reused across leaves (no allocation per D-tree)
+    thread_local std::vector<Tmp> nodes;
+    thread_local std::vector<Item> stack;
+    nodes.assign(1, Tmp{{0, 0, 0, 0}, {0, 0, 0, 0}});
+    stack.assign(1, Item{0, 0, true, 1});
     const float total = L.total;
     while (!stack.empty()) {
         Item it = stack.back();

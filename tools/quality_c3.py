@@ -158,7 +158,13 @@ def main():
         "relmse_ratio_equal_spp": round(g["relmse"] / out["unguided_equal_spp"]["relmse"], 4),
         "relmse_ratio_equal_time": round(g["relmse"] / out["unguided_equal_time"]["relmse"], 4),
         "rel_rmse_ratio_equal_spp": round(g["rel_rmse"] / out["unguided_equal_spp"]["rel_rmse"], 4),
-        "rel_rmse_ratio_equal_time": round(g["rel_rmse"] / out["unguided_equal_time"]["rel_rmse"], 4)}
+        "rel_rmse_ratio_equal_time": round(g["rel_rmse"] / out["unguided_equal_time"]["rel_rmse"], 4),
+        "exposed_ratio_equal_spp": round(g["relmse_exposed"] / out["unguided_equal_spp"]["relmse_exposed"], 4),
+        "exposed_ratio_equal_time": round(g["relmse_exposed"] / out["unguided_equal_time"]["relmse_exposed"], 4)}
+    iv = out["guided_inversevar"]  # every iteration's film, inverse-variance weighted (same wall clock + combine)
+    out["inversevar_vs_unguided"] = {
+        "relmse_ratio_equal_time": round(iv["relmse"] / out["unguided_equal_time"]["relmse"], 4),
+        "exposed_ratio_equal_time": round(iv["relmse_exposed"] / out["unguided_equal_time"]["relmse_exposed"], 4)}
     print(json.dumps(out), flush=True)
     if a.dump:
         np.savez_compressed(a.dump, **{k: v.astype(np.float16) for k, v in dumps.items()})
