@@ -890,23 +890,37 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         return s;
     // densities: one buffer, each grid 256-B aligned (bricked, see pg_layout.h GMedium)
     {
-        size_t words = 0;
+        size_t words = 0, linMax = 0;
         std::vector<size_t> at;
         std::vector<float> stage;
+        // corner-packed grids (pg_layout.h PG_DENSITY_CORNERS); a grid with a dimension of 1 has no
+        // cell (every lookup is 0) and keeps no density
         for (uint32_t m = 0; m < d->num_media; ++m) {
             const pg_medium &pm = d->media[m];
             at.push_back(words);
             gmed[m].bx = (pm.res[0] + 3) / 4;
             gmed[m].by = (pm.res[1] + 3) / 4;
+            const size_t lin = (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+            const size_t cells = (size_t)(pm.res[0] - 1) * (pm.res[1] - 1) * (pm.res[2] - 1);
+            gmed[m].corners = PG_DENSITY_CORNERS ? 1u : 0u;
             const size_t n = PG_DENSITY_BRICKS ? (size_t)gmed[m].bx * gmed[m].by * ((pm.res[2] + 3) / 4) * 64
-                                               : (size_t)pm.res[0] * pm.res[1] * pm.res[2];
+                             : PG_DENSITY_CORNERS ? cells * 8 : lin;
+            if (PG_DENSITY_CORNERS && cells) linMax = std::max(linMax, lin);
             words += (n + 63) & ~(size_t)63;
         }
         HIPC(c, c->density.grow(std::max<size_t>(words * 4, 256)));
+        DevBuf linTmp;  // the linear grid of a corner-packed medium, expanded on the device
+        if (linMax) HIPC(c, linTmp.alloc(linMax * 4));
         for (uint32_t m = 0; m < d->num_media; ++m) {
             const pg_medium &pm = d->media[m];
             const size_t n = (size_t)pm.res[0] * pm.res[1] * pm.res[2];
-            if (PG_DENSITY_BRICKS) {
+            if (PG_DENSITY_CORNERS) {
+                HIPC(c, hipMemcpyAsync(linTmp.p, pm.density, n * 4, hipMemcpyHostToDevice, c->stream));
+                pg_launch_density_corners(c->stream, linTmp.as<float>(), pm.res[0], pm.res[1], pm.res[2],
+                                          c->density.as<float>() + at[m]);
+                HIPC(c, hipGetLastError());
+                HIPC(c, hipStreamSynchronize(c->stream));  // linTmp is reused by the next medium
+            } else if (PG_DENSITY_BRICKS) {
                 const uint32_t bx = gmed[m].bx, by = gmed[m].by, bz = (pm.res[2] + 3) / 4;
                 stage.assign((size_t)bx * by * bz * 64, 0.0f);
                 for (uint32_t z = 0; z < pm.res[2]; ++z)

@@ -68,8 +68,15 @@ static_assert(sizeof(GEnv) == 128, "GEnv layout");
 #ifndef PG_MAJORANT_CELL
 #define PG_MAJORANT_CELL 8  // voxels per majorant cell and axis (oracle: orc_medium.h kCell)
 #endif
+#ifndef PG_DENSITY_CORNERS
+#define PG_DENSITY_CORNERS 1  // corner-packed density (below); 0: linear voxels (or bricks)
+#endif
 #ifndef PG_DENSITY_BRICKS
 #define PG_DENSITY_BRICKS 0  // measured: no gain over the linear layout (DESIGN.md "Volumes")
+#endif
+#if PG_DENSITY_BRICKS  // bricks replace the corner packing
+#undef PG_DENSITY_CORNERS
+#define PG_DENSITY_CORNERS 0
 #endif
 struct GMedium {
     const float *density;
@@ -87,9 +94,15 @@ struct GMedium {
     float albedo[3];
     uint32_t by;  // bricks along y
     const float *maj;
-    uint32_t pad5[2];
+    uint32_t corners;  // 1: density holds the 8 trilinear corners of every cell (below), 0: linear voxels
+    uint32_t pad5;
 };
 static_assert(sizeof(GMedium) == 128, "GMedium layout");
+// Corner-packed density (default when it fits, see pg_host.cpp kCornerBudget): cell (x, y, z) of the
+// (rx-1)(ry-1)(rz-1) cells between voxel centres stores its 8 corner voxels, 32 B in lookup order
+// (z, y, x bits: d000 d001 d010 d011 | d100 d101 d110 d111), so a trilinear lookup is two aligned
+// 16-B loads instead of eight scattered 4-B loads over four cache lines.  8x the memory of the grid
+// (530 MB for 256^3): a trade the 288 GB of HBM3E affords.
 
 // Per-triangle shading record (5 x float4 = 80 B), indexed by BVH-order triangle id:
 //   [0] p0.xyz, bits(material | (emitter + 1) << 16)

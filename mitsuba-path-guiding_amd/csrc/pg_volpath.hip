@@ -107,6 +107,12 @@ __device__ __forceinline__ float lookupDensity(const MedView &M, f3 p) {
     const float *D = M.density;
     const float d000 = D[az1 + ay1 + ax1], d001 = D[az1 + ay1 + ax2], d010 = D[az1 + ay2 + ax1], d011 = D[az1 + ay2 + ax2];
     const float d100 = D[az2 + ay1 + ax1], d101 = D[az2 + ay1 + ax2], d110 = D[az2 + ay2 + ax1], d111 = D[az2 + ay2 + ax2];
+#elif PG_DENSITY_CORNERS
+    const size_t cell = ((size_t)z1 * (size_t)(M.ry - 1) + (size_t)y1) * (size_t)(M.rx - 1) + (size_t)x1;
+    const float4 *cp = reinterpret_cast<const float4 *>(M.density) + 2 * cell;
+    const float4 lo = cp[0], hi = cp[1];
+    const float d000 = lo.x, d001 = lo.y, d010 = lo.z, d011 = lo.w;
+    const float d100 = hi.x, d101 = hi.y, d110 = hi.z, d111 = hi.w;
 #else
     const size_t sy = (size_t)M.rx, sz = (size_t)M.rx * M.ry;
     const float *b = M.density + (size_t)z1 * sz + (size_t)y1 * sy + x1;
@@ -829,6 +835,25 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
         atomicAdd(v.stats + 1, s1);
         atomicAdd(v.stats + 2, s2);
     }
+}
+
+// corner-packed density (pg_layout.h): one thread per cell, 8 gathers -> two 16-B stores
+__global__ __launch_bounds__(256) void k_density_corners(const float *__restrict__ lin, uint32_t rx, uint32_t ry,
+                                                        uint32_t rz, float4 *__restrict__ out) {
+    const size_t cx = rx - 1, cy = ry - 1, n = cx * cy * (size_t)(rz - 1);
+    const size_t cell = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= n) return;
+    const size_t x = cell % cx, y = (cell / cx) % cy, z = cell / (cx * cy);
+    const size_t sy = rx, sz = (size_t)rx * ry;
+    const float *b = lin + z * sz + y * sy + x;
+    out[2 * cell] = make_float4(b[0], b[1], b[sy], b[sy + 1]);
+    out[2 * cell + 1] = make_float4(b[sz], b[sz + 1], b[sz + sy], b[sz + sy + 1]);
+}
+void pg_launch_density_corners(hipStream_t s, const float *lin, uint32_t rx, uint32_t ry, uint32_t rz, float *out) {
+    const size_t n = (size_t)(rx - 1) * (ry - 1) * (rz - 1);
+    if (!n) return;
+    hipLaunchKernelGGL(k_density_corners, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, lin, rx, ry, rz,
+                       reinterpret_cast<float4 *>(out));
 }
 
 // ---- unit-level queries (pg_phase_query / pg_medium_query) --------------------------------------

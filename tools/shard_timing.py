@@ -17,7 +17,9 @@ sc = pg.scenes.ajar_door(1280, 720)
 worlds = [int(w) for w in (sys.argv[1].split(",") if len(sys.argv) > 1 else ["1", "2", "4", "8"])]
 base = None
 for W in worlds:
-    integ = GuidedPathTracer({"trainingIterations": 5, "samplesPerProgression": 1024}, rank=0, world_size=W)
+    # the bench's guided configuration (bench.py BENCH_GUIDING)
+    integ = GuidedPathTracer({"trainingIterations": 5, "samplesPerProgression": 1024,
+                              "bsdfSamplingFractionBound": "albedo", "glossyPrior": True}, rank=0, world_size=W)
     integ.preprocess(sc)
     d = integ.dev
     best = None
