@@ -235,7 +235,7 @@ typedef struct pg_config {
     int32_t tail_paths;           /* path integrator: a chunk with at most this many live paths finishes in one launch
                                      (k_tail: each thread loops shade -> shadow -> closest hit) instead of one
                                      launch pair + count readback per bounce; bit-identical results.  0 = the
-                                     default (65536, or the PG_TAIL_PATHS environment variable), < 0 = off. */
+                                     default (131072, or the PG_TAIL_PATHS environment variable), < 0 = off. */
     int32_t glossy_prior;         /* guided path integrator: 1 = the BSDF's glossy sampling rate r
                                      (BSDF::getGlossySamplingRate, bsdf.h:365-381: 1 for roughconductor and
                                      roughdielectric, the glossy lobe's probability for roughplastic,

@@ -446,7 +446,7 @@ constexpr uint32_t kRaySortMinShard = 1024;  // smaller bounces trace unsorted (
 uint32_t tailPaths() {
     static const uint32_t n = [] {
         const char *e = std::getenv("PG_TAIL_PATHS");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 16;
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 17;  // profiles/r03n_*: 2^17 vs 2^16 +0.3 %
     }();
     return n;
 }

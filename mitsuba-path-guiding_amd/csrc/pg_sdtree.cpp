@@ -5,7 +5,11 @@
 #include <atomic>
 #include <cmath>
 #include <cstring>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
+#include <vector>
 
 namespace pgh {
 namespace {
@@ -17,23 +21,79 @@ inline float fixedToFloat(uint64_t x) { return (float)std::ldexp((double)x, -24)
 
 // f(i) for i in [0, n) on up to 16 host threads, in blocks of 8 leaves.  Every D-tree is refit,
 // rebuilt and flattened independently of the others, so the result does not depend on the split.
+// The workers persist across calls (a refit makes four parallel passes; spawning 15 threads per pass
+// cost ~1 ms); a caller that finds the pool busy (another context refitting concurrently) runs inline.
+class Pool {
+public:
+    static Pool &get() {
+        static Pool p;
+        return p;
+    }
+    template <class F>
+    bool run(size_t n, size_t threads, F &f) {
+        std::unique_lock<std::mutex> own(use_, std::try_to_lock);
+        if (!own.owns_lock()) return false;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            while (workers_.size() + 1 < threads) workers_.emplace_back([this] { loop(); });
+            job_ = [&f](size_t i) { f(i); };
+            n_ = n;
+            next_.store(0);
+            active_ = std::min(threads, workers_.size() + 1) - 1;
+            pending_ = active_;
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        job_ = nullptr;
+        return true;
+    }
+    ~Pool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+
+private:
+    void work() {
+        for (size_t b; (b = next_.fetch_add(8)) < n_;)
+            for (size_t i = b, e = std::min(n_, b + 8); i < e; ++i) job_(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            std::unique_lock<std::mutex> lk(m_);
+            cv_.wait(lk, [&] { return stop_ || (gen_ != seen && active_ > 0); });
+            if (stop_) return;
+            seen = gen_;
+            --active_;  // this worker takes part in generation gen_
+            lk.unlock();
+            work();
+            lk.lock();
+            if (--pending_ == 0) done_.notify_one();
+        }
+    }
+    std::mutex use_, m_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    std::function<void(size_t)> job_;
+    std::atomic<size_t> next_{0};
+    size_t n_ = 0, active_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
 template <class F>
 void parallelFor(size_t n, F &&f) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     const size_t T = std::min<size_t>(std::min(hw, 16u), (n + 63) / 64);
-    if (T <= 1) {
+    if (T <= 1 || !Pool::get().run(n, T, f))
         for (size_t i = 0; i < n; ++i) f(i);
-        return;
-    }
-    std::atomic<size_t> next{0};
-    auto work = [&] {
-        for (size_t b; (b = next.fetch_add(8)) < n;)
-            for (size_t i = b, e = std::min(n, b + 8); i < e; ++i) f(i);
-    };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < T; ++t) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
 }
 inline float total4(const float *s) { return ((s[0] + s[1]) + s[2]) + s[3]; }
 
