@@ -1111,6 +1111,10 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     v.vtx = g.record ? c->vol_vtx.as<float4>() : nullptr;
     v.vtx_P = want;
     v.dist_beta = c->cfg.distance_guiding;
+    {  // refill threshold of the persistent volumetric kernel (A/B: PG_VOL_REFILL, 1 = every idle lane)
+        const char *e = std::getenv("PG_VOL_REFILL");
+        v.refill_min = e ? (uint32_t)std::max(1, std::min(64, std::atoi(e))) : 1u;
+    }
     PathDev pv{};
     pv.rad = v.rad;
     pv.vtx = v.vtx;

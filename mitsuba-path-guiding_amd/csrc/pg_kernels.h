@@ -68,6 +68,7 @@ struct VolDev {
     float4 *vtx;               // guided training vertices [max_vertices][vtx_P][PG_VTX_F4] (PathDev::vtx layout)
     uint32_t vtx_P;            // slot stride of vtx (>= items per launch)
     float dist_beta;           // pg_config.distance_guiding
+    uint32_t refill_min;       // k_volpath refills a wave's finished lanes once at least this many are idle
 };
 
 // Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).

@@ -773,9 +773,11 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
     VPath P;
     VRng rng{0, 0, 0, 0};
     for (;;) {
-        // refill finished lanes from the work counter (one atomic per wave)
+        // refill finished lanes from the work counter (one atomic per wave); with refill_min > 1 a wave
+        // waits until that many lanes are idle (or none is alive), so the lanes it restarts together
+        // run their camera rays and first hits in one pass instead of one refill per finished path
         const unsigned long long need = __ballot(!alive && !done);
-        if (need) {
+        if (need && (__popcll(need) >= v.refill_min || !__any(alive))) {
             const int leader = __ffsll((long long)need) - 1;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(v.next, (uint32_t)__popcll(need));

@@ -214,3 +214,22 @@ def test_guided_volpath_same_tree_parity(pg, O, beta):
     assert abs(nrec_gpu - nrec_cpu) <= 0.01 * nrec_cpu, (nrec_gpu, nrec_cpu)
     r = np.frombuffer(recs.tobytes(), np.float32).reshape(-1, 8)
     assert np.all(np.isfinite(r[:, [0, 1, 2, 4, 5]])) and np.all(r[:, 5] > 0)
+
+
+def test_volpath_refill_threshold_bit_identical(pg, monkeypatch):
+    """k_volpath refills a wave's idle lanes in batches (VolDev.refill_min, PG_VOL_REFILL): every
+    work item draws from its own stream and writes its own slots, so films and trees must not depend
+    on when lanes are refilled."""
+    from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer
+    sc = pg.scenes.smoke(96, 96, res=48)
+    out = []
+    for r in ("1", "24", "64"):
+        monkeypatch.setenv("PG_VOL_REFILL", r)
+        t = GuidedVolumetricPathTracer({"trainingIterations": 3, "samplesPerProgression": 8})
+        t.preprocess(sc)
+        rgbw, sq = t.render(8)
+        out.append((rgbw, sq, t.dev.get_sdtree()))
+        t.postprocess()
+    for o in out[1:]:
+        assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
+        assert np.array_equal(o[2], out[0][2])
