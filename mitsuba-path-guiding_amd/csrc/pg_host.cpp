@@ -1111,9 +1111,11 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     v.vtx = g.record ? c->vol_vtx.as<float4>() : nullptr;
     v.vtx_P = want;
     v.dist_beta = c->cfg.distance_guiding;
-    {  // refill threshold of the persistent volumetric kernel (A/B: PG_VOL_REFILL, 1 = every idle lane)
+    {  // refill threshold of the persistent volumetric kernel: C5 198 / 212 / 227 / 243 / 248 / 247 / 242 /
+       // 211 Mpaths/s at 1 / 8 / 16 / 32 / 40 / 48 / 56 / 64 idle lanes (profiles/r03p_vol_refill/);
+       // PG_VOL_REFILL overrides (A/B)
         const char *e = std::getenv("PG_VOL_REFILL");
-        v.refill_min = e ? (uint32_t)std::max(1, std::min(64, std::atoi(e))) : 1u;
+        v.refill_min = e ? (uint32_t)std::max(1, std::min(64, std::atoi(e))) : 40u;
     }
     PathDev pv{};
     pv.rad = v.rad;
