@@ -117,7 +117,7 @@ struct Lane {
     uint32_t P = 0;
     int vtx_slots = 0;
     uint32_t vtxP = 0;  // slot stride of vtx (recording passes only allocate it)
-    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_o, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
+    DevBuf ray_o, ray_d, hit, thr, rad, prev, pinfo, sh_d, sh_c, vtx, q0, q1, qs, class_q, counters, stack_ovf;
     DevBuf qkey, qsorted, rsort_hist;  // ray-sorted trace queues (PG_RAY_SORT): keys, sorted entries, histograms
     bool sorted = false;               // the queue of the next trace launch is qsorted
     DevBuf tail_stats;                 // k_tail counters of the running chunk (3 u64), copied to h_tail
@@ -186,8 +186,15 @@ struct Ctx {
     DevBuf ext_records;
     // sd-tree
     pgh::SdTree sd;
-    DevBuf sd_snodes, sd_meta, sd_qnode, sd_bchild, sd_bsum, sd_count, sd_jump;  // sd_qnode: {energies, children}
-    DevBuf sd_frac;  // learned-fraction statistics, pgh::kFracStats u64 per leaf
+    // the device SD-tree lives in one allocation (uploadSd): snodes | meta | qnode {energies, children} |
+    // bchild | bsum | count | frac | jump.  bsum, count and frac are contiguous -- the pg_get_tree_stats
+    // vector -- so the statistics move in one copy (download, all-reduce in place), the host-built
+    // part in one upload, and the jump grid is built on the device from the S-tree.
+    DevBuf sd_blob;
+    struct {
+        uint32_t *snodes = nullptr, *meta = nullptr, *qnode = nullptr, *bchild = nullptr, *jump = nullptr;
+        uint64_t *bsum = nullptr, *count = nullptr, *frac = nullptr;  // frac: pgh::kFracStats u64 per leaf
+    } sdp;
     int sd_jump_bits = 0;
     PinnedBuf sd_stage;
     bool sd_dirty = true;
@@ -345,15 +352,15 @@ SceneDev sceneView(const Ctx *c) {
 }
 SDDev sdView(const Ctx *c) {
     SDDev s{};
-    s.snodes = c->sd_snodes.as<uint2>();
-    s.meta = c->sd_meta.as<uint4>();
-    s.qsum = c->sd_qnode.as<float4>();
-    s.qchild = reinterpret_cast<const uint4 *>(c->sd_qnode.as<float4>() + 1);
-    s.bchild = c->sd_bchild.as<uint4>();
-    s.bsum = c->sd_bsum.as<unsigned long long>();
-    s.count = c->sd_count.as<unsigned long long>();
-    s.jump = c->sd_jump.as<uint32_t>();
-    s.frac = c->sd_frac.as<unsigned long long>();
+    s.snodes = reinterpret_cast<const uint2 *>(c->sdp.snodes);
+    s.meta = reinterpret_cast<const uint4 *>(c->sdp.meta);
+    s.qsum = reinterpret_cast<const float4 *>(c->sdp.qnode);
+    s.qchild = reinterpret_cast<const uint4 *>(reinterpret_cast<const float4 *>(c->sdp.qnode) + 1);
+    s.bchild = reinterpret_cast<const uint4 *>(c->sdp.bchild);
+    s.bsum = reinterpret_cast<unsigned long long *>(c->sdp.bsum);
+    s.count = reinterpret_cast<unsigned long long *>(c->sdp.count);
+    s.jump = c->sdp.jump;
+    s.frac = reinterpret_cast<unsigned long long *>(c->sdp.frac);
     s.jump_bits = c->sd_jump_bits;
     s.learned = c->cfg.bsdf_fraction_bound == PG_FRACTION_LEARNED ? 1 : 0;
     s.alpha0 = c->cfg.bsdf_sampling_fraction;
@@ -364,32 +371,39 @@ SDDev sdView(const Ctx *c) {
 }
 PathDev pathView(const Lane *c) {
     return PathDev{c->ray_o.as<float4>(), c->ray_d.as<float4>(), c->hit.as<float4>(), c->thr.as<float4>(),
-                   c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(), c->sh_o.as<float4>(),
+                   c->rad.as<float4>(),   c->prev.as<float4>(),  c->pinfo.as<uint4>(),
                    c->sh_d.as<float4>(),  c->sh_c.as<float4>(),  c->vtx.as<float4>(), c->stack_ovf.as<uint32_t>(),
                    c->P,                  c->vtxP,               c->aov.as<float4>()};
 }
 
 pg_status uploadSd(Ctx *c) {
-    // the device layout is written straight into the pinned staging buffer (no intermediate
-    // arrays), then copied part by part
+    // the device layout (Ctx::sd_blob) is written straight into the pinned staging buffer at the same
+    // offsets, then copied in one piece; the jump grid is derived on the device from the S-tree
     const pgh::SdTree &t = c->sd;
     const size_t R = (size_t)1 << pgh::SdTree::kJumpBits;
     const size_t nl = t.leaves.size(), ns = t.samplingNodes(), nb = t.buildingNodes();
-    DevBuf *dst[] = {&c->sd_snodes, &c->sd_meta, &c->sd_qnode, &c->sd_bchild, &c->sd_bsum, &c->sd_count, &c->sd_jump,
-                     &c->sd_frac};
-    const size_t bytes[] = {4 * t.snode.size(), 16 * nl, 32 * ns, 16 * nb, 32 * nb, 8 * nl, 4 * R * R * R,
-                            8 * pgh::kFracStats * nl};
-    size_t off[9] = {0};
-    for (int k = 0; k < 8; ++k) off[k + 1] = off[k] + ((bytes[k] + 255) & ~(size_t)255);
-    HIPC(c, c->sd_stage.reserve(off[8]));
+    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t oMeta = up(4 * t.snode.size()), oQ = oMeta + up(16 * nl), oB = oQ + up(32 * ns);
+    const size_t oStats = oB + up(16 * nb), statBytes = 32 * nb + 8 * nl + 8 * pgh::kFracStats * nl;
+    const size_t oJump = oStats + up(statBytes), total = oJump + 4 * R * R * R;
+    HIPC(c, c->sd_stage.reserve(oJump));
     uint8_t *h = (uint8_t *)c->sd_stage.p;
-    t.flattenInto(pgh::SdTree::Layout{(uint32_t *)(h + off[0]), (uint32_t *)(h + off[1]), (uint32_t *)(h + off[2]),
-                                      (uint32_t *)(h + off[3]), (uint64_t *)(h + off[4]), (uint64_t *)(h + off[5]),
-                                      (uint32_t *)(h + off[6]), (uint64_t *)(h + off[7])});
-    for (int k = 0; k < 8; ++k) {
-        HIPC(c, dst[k]->grow(std::max<size_t>(bytes[k], 16)));
-        if (bytes[k]) HIPC(c, hipMemcpyAsync(dst[k]->p, h + off[k], bytes[k], hipMemcpyHostToDevice, c->stream));
-    }
+    uint64_t *hs = (uint64_t *)(h + oStats);
+    t.flattenInto(pgh::SdTree::Layout{(uint32_t *)h, (uint32_t *)(h + oMeta), (uint32_t *)(h + oQ),
+                                      (uint32_t *)(h + oB), hs, hs + 4 * nb, nullptr, hs + 4 * nb + nl});
+    HIPC(c, c->sd_blob.grow(total));
+    uint8_t *d = (uint8_t *)c->sd_blob.p;
+    c->sdp.snodes = (uint32_t *)d;
+    c->sdp.meta = (uint32_t *)(d + oMeta);
+    c->sdp.qnode = (uint32_t *)(d + oQ);
+    c->sdp.bchild = (uint32_t *)(d + oB);
+    c->sdp.bsum = (uint64_t *)(d + oStats);
+    c->sdp.count = c->sdp.bsum + 4 * nb;
+    c->sdp.frac = c->sdp.count + nl;
+    c->sdp.jump = (uint32_t *)(d + oJump);
+    HIPC(c, hipMemcpyAsync(d, h, oJump, hipMemcpyHostToDevice, c->stream));
+    pg_launch_sd_jump(c->stream, c->sdp.snodes, pgh::SdTree::kJumpBits, c->sdp.jump);
+    HIPC(c, hipGetLastError());
     HIPC(c, hipStreamSynchronize(c->stream));
     c->stats.stree_nodes = t.snode.size() / 2;
     c->stats.dtree_nodes = ns;
@@ -398,17 +412,13 @@ pg_status uploadSd(Ctx *c) {
     return PG_OK;
 }
 
-// pull device-side building sums + counts into the host tree
+// pull device-side building sums + counts (+ fraction statistics) into the host tree: one copy
 pg_status downloadSd(Ctx *c) {
-    size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
-    const size_t sb = (32 * nb + 255) & ~(size_t)255, sc = (8 * nl + 255) & ~(size_t)255;
-    HIPC(c, c->sd_stage.reserve(sb + sc + 8 * pgh::kFracStats * nl));
-    uint64_t *bsum = (uint64_t *)c->sd_stage.p;
-    uint64_t *cnt = (uint64_t *)((uint8_t *)c->sd_stage.p + sb);
-    uint64_t *frac = (uint64_t *)((uint8_t *)c->sd_stage.p + sb + sc);
-    HIPC(c, hipMemcpyAsync(bsum, c->sd_bsum.p, 32 * nb, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(cnt, c->sd_count.p, 8 * nl, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipMemcpyAsync(frac, c->sd_frac.p, 8 * pgh::kFracStats * nl, hipMemcpyDeviceToHost, c->stream));
+    const size_t nb = c->sd.buildingNodes(), nl = c->sd.leaves.size();
+    const size_t bytes = 32 * nb + 8 * nl + 8 * pgh::kFracStats * nl;
+    HIPC(c, c->sd_stage.reserve(bytes));
+    uint64_t *bsum = (uint64_t *)c->sd_stage.p, *cnt = bsum + 4 * nb, *frac = cnt + nl;
+    HIPC(c, hipMemcpyAsync(bsum, c->sdp.bsum, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     std::vector<uint32_t> cnt32(nl);
     for (size_t i = 0; i < nl; ++i) cnt32[i] = (uint32_t)std::min<uint64_t>(cnt[i], 0xFFFFFFFFu);
@@ -458,7 +468,7 @@ int vertexSlots(const Ctx *c, bool rec) { return rec ? std::max(0, std::min(c->c
 void releasePaths(Ctx *c) {
     for (int li = 0; li < c->nlanes; ++li) {
         Lane &l = c->lanes[li];
-        for (DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo, &l.sh_o, &l.sh_d, &l.sh_c,
+        for (DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo, &l.sh_d, &l.sh_c,
                           &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov, &l.qkey, &l.qsorted})
             b->release();
         l.P = 0;
@@ -503,7 +513,6 @@ pg_status ensurePaths(Ctx *c, uint32_t want, bool rec) {
         HIPC(c, l.rad.alloc(f4));
         HIPC(c, l.prev.alloc(f4));
         HIPC(c, l.pinfo.alloc(f4));
-        HIPC(c, l.sh_o.alloc(f4));
         HIPC(c, l.sh_d.alloc(f4));
         HIPC(c, l.sh_c.alloc(f4));
         const size_t qbytes = (size_t)PG_QSHARDS * pg_queue_stride(P) * 4;
@@ -1206,12 +1215,12 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
             size_t held = 0;
             for (int li = 0; li < c->nlanes; ++li) {
                 const Lane &l = c->lanes[li];
-                for (const DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo, &l.sh_o,
+                for (const DevBuf *b : {&l.ray_o, &l.ray_d, &l.hit, &l.thr, &l.rad, &l.prev, &l.pinfo,
                                         &l.sh_d, &l.sh_c, &l.vtx, &l.q0, &l.q1, &l.qs, &l.class_q, &l.aov})
                     held += b->bytes;
             }
             const int vs = vertexSlots(c, rec);
-            const double perPath = 10.0 * 16 + (3 + PG_NUM_CLASSES) * 4.0 + vs * 16.0 * PG_VTX_F4 + (c->cfg.aovs ? 16.0 : 0.0);
+            const double perPath = 9.0 * 16 + (3 + PG_NUM_CLASSES) * 4.0 + vs * 16.0 * PG_VTX_F4 + (c->cfg.aovs ? 16.0 : 0.0);
             const double fit = 0.7 * (double)(freeB + held) / (perPath * c->nlanes);
             if (fit < (double)cap) cap = std::max<uint32_t>(1u << 20, (uint32_t)fit & ~4095u);
         }
@@ -1668,9 +1677,7 @@ pg_status pg_get_tree_stats(void *ctx, void *dst, uint64_t capacity_words, int32
     if (!dst) return PG_OK;
     if (capacity_words < *words) return fail(c, PG_ERR_INVALID, "pg_get_tree_stats: buffer too small");
     const hipMemcpyKind k = dst_is_device ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    HIPC(c, hipMemcpyAsync(dst, c->sd_bsum.p, 32 * nb, k, c->stream));
-    HIPC(c, hipMemcpyAsync((uint64_t *)dst + 4 * nb, c->sd_count.p, 8 * nl, k, c->stream));
-    HIPC(c, hipMemcpyAsync((uint64_t *)dst + 4 * nb + nl, c->sd_frac.p, 8 * pgh::kFracStats * nl, k, c->stream));
+    HIPC(c, hipMemcpyAsync(dst, c->sdp.bsum, 8 * *words, k, c->stream));  // bsum | count | frac, contiguous
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }
@@ -1684,9 +1691,7 @@ pg_status pg_put_tree_stats(void *ctx, const void *src, uint64_t words, int32_t 
     if (words != 4 * nb + nl + pgh::kFracStats * nl)
         return fail(c, PG_ERR_INVALID, "pg_put_tree_stats: size does not match the tree");
     const hipMemcpyKind k = src_is_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    HIPC(c, hipMemcpyAsync(c->sd_bsum.p, src, 32 * nb, k, c->stream));
-    HIPC(c, hipMemcpyAsync(c->sd_count.p, (const uint64_t *)src + 4 * nb, 8 * nl, k, c->stream));
-    HIPC(c, hipMemcpyAsync(c->sd_frac.p, (const uint64_t *)src + 4 * nb + nl, 8 * pgh::kFracStats * nl, k, c->stream));
+    HIPC(c, hipMemcpyAsync(c->sdp.bsum, src, 8 * words, k, c->stream));  // bsum | count | frac, contiguous
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }
@@ -1731,18 +1736,16 @@ pg_status pg_comm_allreduce_tree_stats(void *ctx) {
     if (!c->comm) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_tree_stats: no communicator (pg_comm_init)");
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_comm_allreduce_tree_stats: no scene");
     HIPC(c, hipSetDevice(c->cfg.device));
-    // the reduced vector IS the pg_get_tree_stats vector (u64 quadrant sums, then per-D-tree record
-    // counts): gathered with pg_get_tree_stats into one device buffer, summed over ranks, put back
-    // with pg_put_tree_stats -- so the multi-rank arithmetic is the one the torch.distributed /
-    // gloo exchange tests check.  Integer sums: every rank ends with identical statistics.
+    // the reduced vector IS the pg_get_tree_stats vector (u64 quadrant sums, per-D-tree record counts,
+    // fraction statistics), which the device keeps contiguous: summed over ranks in place -- the
+    // multi-rank arithmetic the torch.distributed / gloo exchange tests check.  Integer sums: every
+    // rank ends with identical statistics.
     uint64_t words = 0;
     pg_status st;
     if ((st = pg_get_tree_stats(ctx, nullptr, 0, 1, &words))) return st;
-    DevBuf v;
-    HIPC(c, v.alloc(std::max<uint64_t>(words, 1) * 8));
-    if ((st = pg_get_tree_stats(ctx, v.p, words, 1, &words))) return st;
-    NCCLC(c, ncclAllReduce(v.p, v.p, words, ncclUint64, ncclSum, c->comm, c->stream));
-    return pg_put_tree_stats(ctx, v.p, words, 1);
+    if (words) NCCLC(c, ncclAllReduce(c->sdp.bsum, c->sdp.bsum, words, ncclUint64, ncclSum, c->comm, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
 }
 
 pg_status pg_comm_reduce_film(void *ctx, int32_t root) {

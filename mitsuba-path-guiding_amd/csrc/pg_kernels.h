@@ -26,7 +26,7 @@ struct SceneDev {
 struct PathDev {
     float4 *ray_o, *ray_d, *hit, *thr, *rad, *prev;
     uint4 *pinfo;
-    float4 *sh_o, *sh_d, *sh_c;
+    float4 *sh_d, *sh_c;  // shadow ray (direction, tmax) and contribution; its origin is ray_o
     float4 *vtx;       // [max_vertices][P][PG_VTX_F4]
     uint32_t *stack_ovf;  // traversal-stack overflow ring, pg_stack_overflow_words(0) words
     uint32_t P;        // path-state capacity
@@ -130,6 +130,9 @@ void pg_launch_envmap_query(hipStream_t s, const SceneDev &sc, int op, const flo
 // env_hits: surface path with an environment emitter (escape radiance in the hit record)
 void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_vertices, pg_record *records,
                       unsigned long long *rec_count, unsigned long long rec_capacity, int env_hits);
+// S-tree jump grid (SDDev::jump) of the device S-tree: cell (x, y, z) of the 2^bits grid -> the node
+// reached after 3 * bits axis-cycling midpoint decisions from the root (or the leaf met before)
+void pg_launch_sd_jump(hipStream_t s, const uint32_t *snodes, int bits, uint32_t *jump);
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n);
 // one volpath sample per (pixel, layer) item of the chunk, written to v.rad[item]
 void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,

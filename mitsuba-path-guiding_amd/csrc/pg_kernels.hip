@@ -188,6 +188,12 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
                                           top, ntop);
 }
 
+// shadow-ray mint at the shading point o (the extension ray's origin): Epsilon * max |o_i|
+// (progressive_path.cpp via DirectSamplingRecord / Scene::sampleEmitterDirect's shadow ray)
+__device__ __forceinline__ float shadowTmin(float4 o) {
+    return kEpsilon * fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+}
+
 // any hit for queued shadow rays; unoccluded -> add the NEE contribution to L (and to the
 // training vertex's radiance snapshot, so its record excludes light arriving from elsewhere)
 __device__ __forceinline__ void shadowRows(const SceneDev &sc, const PathDev &p, const Queue &q, uint32_t bid,
@@ -197,11 +203,12 @@ __device__ __forceinline__ void shadowRows(const SceneDev &sc, const PathDev &p,
     const uint32_t *items = q.items + (size_t)s * q.stride;
     for (uint32_t i = (bid / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += nblk / PG_QSHARDS * TRACE_BLOCK) {
         uint32_t slot = items[i];
-        float4 o = ldS(&p.sh_o[slot]), d = ldS(&p.sh_d[slot]);
+        // the shadow ray starts at the shading point, which is also the extension ray's origin
+        float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.sh_d[slot]);
         float tmax = d.w;
         uint32_t tri = 0xFFFFFFFFu;
         float u, v;
-        bool occ = traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+        bool occ = traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), shadowTmin(o), tmax, tri, u, v, stk);
         if (!occ) {
             float4 c = ldS(&p.sh_c[slot]);
             float4 L = ldS(&p.rad[slot]);
@@ -462,9 +469,8 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
                 if (wantKey) rkey = rayOrderKey(sd, h.p, wo);
             }
         }
-        if (shadow) {
-            float tmin = kEpsilon * fmaxf(fmaxf(fabsf(h.p.x), fabsf(h.p.y)), fabsf(h.p.z));
-            stS(&p.sh_o[slot], f4(h.p, tmin));
+        if (shadow) {  // origin: ray_o (the extension ray's, written above when the path goes on)
+            if (!alive) stS(&p.ray_o[slot], f4(h.p, 0.0f));
             stS(&p.sh_d[slot], f4(neeD, neeDist * (1 - kShadowEpsilon)));
             stS(&p.sh_c[slot], f4(neeC, __uint_as_float(vtxIndex)));
         }
@@ -650,10 +656,10 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_tail(GParams g, SceneDev sc, SD
             tailShade<ENV>(g, sc, sd, p, slot, tri, alive, shadow);
             if (shadow) {  // shadowRows for this path
                 ++shadows;
-                const float4 o = ldS(&p.sh_o[slot]), d = ldS(&p.sh_d[slot]);
+                const float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.sh_d[slot]);
                 float tmax = d.w, u, v;
                 uint32_t t2 = 0xFFFFFFFFu;
-                if (!traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), o.w, tmax, t2, u, v, wstk)) {
+                if (!traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), shadowTmin(o), tmax, t2, u, v, wstk)) {
                     const float4 c = ldS(&p.sh_c[slot]);
                     const float4 L = ldS(&p.rad[slot]);
                     stS(&p.rad[slot], make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w));
@@ -1250,6 +1256,25 @@ void pg_launch_commit(hipStream_t s, const PathDev &p, uint32_t nslots, int max_
     if (!nslots) return;
     hipLaunchKernelGGL(k_commit, dim3(blocks(nslots, 256)), dim3(256), 0, s, p, nslots, max_vertices, records, rec_count,
                        rec_capacity, env_hits);
+}
+// the host's fillJump (pg_sdtree.cpp) per cell: level d splits axis d % 3 by bit (bits - 1 - d / 3) of
+// the cell's coordinate on that axis
+__global__ __launch_bounds__(256) void k_sd_jump(const uint2 *__restrict__ snodes, int bits, uint32_t *__restrict__ jump) {
+    const uint32_t R = 1u << bits, cell = blockIdx.x * blockDim.x + threadIdx.x;
+    if (cell >= R * R * R) return;
+    const uint32_t xyz[3] = {cell % R, (cell / R) % R, cell / (R * R)};
+    uint32_t n = 0;
+    for (int d = 0; d < 3 * bits; ++d) {
+        const uint2 nd = snodes[n];
+        if (nd.x == 0xFFFFFFFFu) break;
+        n = ((xyz[d % 3] >> (bits - 1 - d / 3)) & 1u) ? nd.y : nd.x;
+    }
+    jump[cell] = n;
+}
+void pg_launch_sd_jump(hipStream_t s, const uint32_t *snodes, int bits, uint32_t *jump) {
+    const uint32_t n = 1u << (3 * bits);
+    hipLaunchKernelGGL(k_sd_jump, dim3((n + 255) / 256), dim3(256), 0, s, reinterpret_cast<const uint2 *>(snodes), bits,
+                       jump);
 }
 void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsigned long long n) {
     if (!n) return;

@@ -258,7 +258,7 @@ static void fillJump(const std::vector<uint32_t> &sn, uint32_t node, int depth, 
 void SdTree::flattenInto(const Layout &d) const {
     std::memcpy(d.snodes, snode.data(), 4 * snode.size());
     const uint32_t R = 1u << kJumpBits;
-    fillJump(snode, 0, 0, kJumpBits, 0, 0, 0, R, R, R, d.jump);
+    if (d.jump) fillJump(snode, 0, 0, kJumpBits, 0, 0, 0, R, R, R, d.jump);  // nullptr: built on the device
     std::vector<uint32_t> sbase(leaves.size()), bbase(leaves.size());
     for (size_t i = 0, sb = 0, bb = 0; i < leaves.size(); ++i) {
         sbase[i] = (uint32_t)sb;
