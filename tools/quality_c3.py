@@ -104,13 +104,17 @@ def main():
     tu = float("inf")
     for _ in range(a.reps):
         dev.reset_film()
+        s0 = dev.stats()
         t = time.perf_counter()
         dev.render_pass(a.spp, 0)
         ug = img(dev.read_film())
         tu = min(tu, time.perf_counter() - t)
+        s1 = dev.stats()
     rate = a.spp * npx / tu
     dumps = {"unguided": ug}
-    out["unguided_equal_spp"] = dict(errors(ug, gt), seconds=round(tu, 3), mpaths_s=round(rate / 1e6, 1))
+    seg_u = (s1["segments"] - s0["segments"]) / max(1, s1["paths"] - s0["paths"])
+    out["unguided_equal_spp"] = dict(errors(ug, gt), seconds=round(tu, 3), mpaths_s=round(rate / 1e6, 1),
+                                     segments_per_path=round(seg_u, 4), gsegments_s=round(rate * seg_u / 1e9, 3))
     print("unguided", json.dumps(out["unguided_equal_spp"]), flush=True)
 
     # ---- guided job (training + final render), discard and inverse-variance combination
@@ -124,15 +128,19 @@ def main():
         el = float("inf")
         for _ in range(a.reps):
             integ.reset()
+            s0 = integ.dev.stats()
             t = time.perf_counter()
             rgbw, sq = integ.render(a.spp)
             el = min(el, time.perf_counter() - t)
-        st = integ.dev.stats()
+            st = integ.dev.stats()
+        seg_g = (st["segments"] - s0["segments"]) / max(1, st["paths"] - s0["paths"])
         x = rgbw[..., :3] / np.maximum(rgbw[..., 3:], 1)
         dumps[comb] = x
         r = dict(errors(x, gt), seconds=round(el, 3),
                  mpaths_s=round((2 ** a.train - 1 + a.spp) * npx / el / 1e6, 1),
-                 stree_nodes=int(st["stree_nodes"]), dtree_nodes=int(st["dtree_nodes"]))
+                 stree_nodes=int(st["stree_nodes"]), dtree_nodes=int(st["dtree_nodes"]),
+                 segments_per_path=round(seg_g, 4),
+                 gsegments_s=round((st["segments"] - s0["segments"]) / el / 1e9, 3))
         if comb == "inversevar":
             r["weights"] = [round(w, 4) for w in integ.combination_weights]
         else:
