@@ -49,6 +49,7 @@ BYTES_SHADOW_PER_RAY = 32      # shadow-queue read 32
 assert BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX + BYTES_SHADE_RECORD + BYTES_SHADOW_PER_RAY == BYTES_SEGMENT
 BYTES_DENSITY_LOOKUP = 32      # k_volpath (C5): one trilinear lookup gathers 8 f32 voxels
 GT_C3 = os.path.join(ROOT, "tests", "golden", "c3_gt.npz")
+GT_C3_CPU = os.path.join(ROOT, "tests", "golden", "c3_cpu_gt_tiles.npz")  # make_c3_cpu_gt.py
 
 
 def parse():
@@ -542,6 +543,21 @@ def cpu_baseline(pg, scene, integ, final, a):
                      "rmse_cpu_vs_gt": float(np.sqrt(se_c.sum() / c.size)),
                      "rmse_ratio_gpu_over_cpu": round(ratio, 5), "rmse_ratio_jackknife_se": round(err, 5),
                      "target": "<= 1.01 (SURVEY.md §8c(3))"})
+        # the same ratio against a ground truth the system under test did not render: the unguided
+        # CPU oracle at 8192 spp on the first tiles of the same run (tests/golden/make_c3_cpu_gt.py)
+        if os.path.exists(GT_C3_CPU):
+            z = np.load(GT_C3_CPU)
+            at = {int(p): i for i, p in enumerate(z["pixels"])}
+            if all(int(p) in at for p in pix):
+                gtc = z["mean"][[at[int(p)] for p in pix]].astype(np.float64)
+                se_g2 = ((g - gtc) ** 2).reshape(ntiles, -1).sum(1)
+                se_c2 = ((c - gtc) ** 2).reshape(ntiles, -1).sum(1)
+                jk2 = np.sqrt((se_g2.sum() - se_g2) / (se_c2.sum() - se_c2))
+                rmse["vs_cpu_ground_truth"] = {
+                    "ground_truth": f"tests/golden/c3_cpu_gt_tiles.npz: CPU oracle, unguided, {int(z['spp'])} spp",
+                    "rmse_ratio_gpu_over_cpu": round(float(np.sqrt(se_g2.sum() / se_c2.sum())), 5),
+                    "rmse_ratio_jackknife_se": round(float(np.sqrt((ntiles - 1) / ntiles *
+                                                                   ((jk2 - jk2.mean()) ** 2).sum())), 5)}
     # same-stream parity: the CPU final render of the same tiles with the GPU-trained tree
     tree.deserialize(integ.dev.get_sdtree())
     s_rgbw = O.render(osc, cfg, a.spp, off, sdtree=tree, pixels=pix, nthreads=cores)[0]

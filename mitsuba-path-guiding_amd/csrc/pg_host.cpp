@@ -108,6 +108,14 @@ enum LaunchKind { KT_TRACE = 0, KT_SHADE = 1, KT_SHADOW = 2, KT_RAYS = 3 };
 #ifndef PG_SMALL_PASS
 #define PG_SMALL_PASS (1u << 21)  // paths: passes up to this size run as one chunk (0: always one per lane)
 #endif
+// the same threshold at run time (A/B: PG_SMALL_PASS_PATHS overrides)
+uint64_t smallPass() {
+    static const uint64_t n = [] {
+        const char *e = std::getenv("PG_SMALL_PASS_PATHS");
+        return e ? (uint64_t)std::strtoull(e, nullptr, 10) : (uint64_t)PG_SMALL_PASS;
+    }();
+    return n;
+}
 #ifndef PG_PIXEL_BLOCK
 #define PG_PIXEL_BLOCK 8  // local pixel order inside a tile: 8x8 blocks (0: row-major)
 #endif
@@ -1237,7 +1245,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
         // a small pass (early training iterations, a rank's shard of them) runs as ONE chunk: three
         // lanes would each pay the whole bounce tail of launches and count readbacks for a third of
         // the paths.  Per-pixel sums keep their layer order either way.
-        if (total <= (uint64_t)PG_SMALL_PASS) chunks = 1;
+        if (total <= smallPass()) chunks = 1;
         if ((uint64_t)npix * chunks <= total) {  // whole sample layers per chunk
             const uint64_t layers = (spp + chunks - 1) / chunks;
             want = (uint32_t)std::min<uint64_t>(layers * npix, cap);
