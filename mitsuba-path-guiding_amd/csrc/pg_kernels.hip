@@ -920,8 +920,14 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
 // atomics.  Each block then adds its table entries to the global sums once.  A hot D-tree (one near
 // the camera gets ~10 % of an iteration's records) thus costs one global atomic per block instead of
 // one per wave.  Integer sums: the trees are bit-identical to the wave-aggregated k_splat.
-#define SPLAT_CNT_SLOTS 512
-#define SPLAT_SUM_SLOTS 2048
+// 1024 + 4096 entries (60 KiB, 2 blocks per CU): C3 W = 1 training 77 -> 70 ms against 512 + 2048
+// (iteration 4's splat 7.5 -> 2.9 ms); 2048 + 8192 (1 block per CU) 74 ms (profiles/r03y_splat_tables_ab/)
+#ifndef SPLAT_CNT_SLOTS
+#define SPLAT_CNT_SLOTS 1024
+#endif
+#ifndef SPLAT_SUM_SLOTS
+#define SPLAT_SUM_SLOTS 4096
+#endif
 #define SPLAT_EMPTY 0xFFFFFFFFu
 __device__ __forceinline__ bool ldsTableAdd(uint32_t *keys, unsigned long long *vals, uint32_t mask, uint32_t key,
                                             unsigned long long v) {
