@@ -518,6 +518,84 @@ static bool buildBinaryBvh(const std::vector<BNode> &bn, uint32_t maxDepth, cons
     return true;
 }
 
+// 4-wide BVH (PG_BVH4, closest hit) over the same tree: each node takes a binary inner node's two
+// children and opens the largest-area inner child until it has four; its leaves are the binary
+// leaves (same refs).  Nodes are stored in depth-first order.  Fails if a root-to-leaf walk could
+// hold more than PG_QSTACK_DEPTH stack entries (the siblings pushed at every level).
+static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_t> &posOf, BvhOut &out) {
+    auto ref = [&](int32_t n, int32_t inner) -> int32_t {
+        if (bn[n].leaf) return (int32_t)(~((posOf[bn[n].first] << 4) | bn[n].count));
+        return inner;
+    };
+    struct QTask { int32_t bnode; uint32_t qnode; uint32_t stackNeed; };
+    std::vector<float> nodes;
+    std::vector<QTask> st;
+    uint32_t maxNeed = 0;
+    auto alloc = [&]() {
+        const uint32_t q = (uint32_t)(nodes.size() / (4 * PG_QNODE_F4));
+        nodes.resize(nodes.size() + 4 * PG_QNODE_F4, 0.0f);
+        return q;
+    };
+    if (bn[0].leaf) {  // the root is a leaf: one node with one leaf slot
+        const uint32_t q = alloc();
+        float *o = &nodes[(size_t)q * 4 * PG_QNODE_F4];
+        int32_t r[4] = {ref(0, 0), PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY};
+        for (int a = 0; a < 3; ++a) {
+            o[8 * a + 0] = bn[0].box.lo[a];
+            o[8 * a + 4] = bn[0].box.hi[a];
+        }
+        std::memcpy(&o[24], r, 16);
+        out.nodes.swap(nodes);
+        return true;
+    }
+    st.push_back({0, alloc(), 1});
+    while (!st.empty()) {
+        const QTask t = st.back();
+        st.pop_back();
+        std::vector<int32_t> ch{bn[t.bnode].child[0], bn[t.bnode].child[1]};
+        while (ch.size() < 4) {
+            int best = -1;
+            float bestA = -1.0f;
+            for (size_t i = 0; i < ch.size(); ++i)
+                if (!bn[ch[i]].leaf && bn[ch[i]].box.area() > bestA) {
+                    bestA = bn[ch[i]].box.area();
+                    best = (int)i;
+                }
+            if (best < 0) break;
+            const int32_t m = ch[best];
+            ch[best] = bn[m].child[0];
+            ch.insert(ch.begin() + best + 1, bn[m].child[1]);
+        }
+        const uint32_t need = t.stackNeed + (uint32_t)ch.size() - 1;
+        maxNeed = std::max(maxNeed, need);
+        int32_t r[4] = {PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY};
+        float box[6][4];
+        for (int a = 0; a < 6; ++a)
+            for (int s = 0; s < 4; ++s) box[a][s] = 0.0f;
+        for (size_t s = 0; s < ch.size(); ++s) {
+            const BNode &c = bn[ch[s]];
+            for (int a = 0; a < 3; ++a) {
+                box[2 * a][s] = c.box.lo[a];
+                box[2 * a + 1][s] = c.box.hi[a];
+            }
+            if (c.leaf) {
+                r[s] = ref(ch[s], 0);
+            } else {
+                const uint32_t q = alloc();
+                r[s] = (int32_t)q;
+                st.push_back({ch[s], q, need});
+            }
+        }
+        float *o = &nodes[(size_t)t.qnode * 4 * PG_QNODE_F4];
+        for (int a = 0; a < 6; ++a)
+            for (int s = 0; s < 4; ++s) o[4 * a + s] = box[a][s];
+        std::memcpy(&o[24], r, 16);
+    }
+    out.nodes.swap(nodes);
+    out.top_nodes = 0;
+    return maxNeed <= PG_QSTACK_DEPTH;
+}
+
 bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_limit, BvhOut &out) {
     if (nt == 0) {  // every ray misses: an inner root with two empty far-away leaves; a childless wide node
         out.nodes.assign(16, 0.0f);
@@ -526,6 +604,11 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         int32_t empty = ~(int32_t)0;
         std::memcpy(&out.nodes[12], &empty, 4);
         std::memcpy(&out.nodes[13], &empty, 4);
+        if (PG_BVH4) {  // one node without children
+            out.nodes.assign(4 * PG_QNODE_F4, 0.0f);
+            const int32_t r[4] = {PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY};
+            std::memcpy(&out.nodes[24], r, 16);
+        }
         out.wnodes.assign(PG_WIDE_NODE_F4 * 4, 0.0f);
         out.order.clear();
         out.woop.clear();
@@ -545,7 +628,12 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         out.lo[a] = all.lo[a];
         out.hi[a] = all.hi[a];
     }
-    return buildWide(P, I, nt, stack_limit, bn, ord, out, posOf) && buildBinaryBvh(bn, maxDepth, posOf, stack_limit, out);
+    if (!buildWide(P, I, nt, stack_limit, bn, ord, out, posOf)) return false;
+    if (PG_BVH4) {
+        out.max_depth = maxDepth;
+        return buildQuadBvh(bn, posOf, out);
+    }
+    return buildBinaryBvh(bn, maxDepth, posOf, stack_limit, out);
 }
 
 }  // namespace pgh

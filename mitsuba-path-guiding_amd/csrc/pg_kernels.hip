@@ -1110,7 +1110,8 @@ static inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b
 
 size_t pg_stack_overflow_words(uint64_t max_threads) {
     if (max_threads == 0) max_threads = (uint64_t)TRACE_MAX_BLOCKS * TRACE_BLOCK;
-    const size_t words = std::max<size_t>(STACK_DEPTH - LDS_STACK, 2 * (STACK_DEPTH - WIDE_LDS_STACK));
+    const size_t words = std::max<size_t>(std::max(STACK_DEPTH, PG_BVH4 ? PG_QSTACK_DEPTH : 0) - LDS_STACK,
+                                          2 * (STACK_DEPTH - WIDE_LDS_STACK));
     return words * max_threads;
 }
 // threads k_trace_rays launches for n rays: its overflow stride is gridDim.x * TRACE_BLOCK

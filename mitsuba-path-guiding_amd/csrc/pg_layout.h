@@ -124,6 +124,20 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 #define PG_BVH_TOP_LEVELS 5
 #define PG_BVH_TOP_NODES 31
 
+// 4-wide BVH node for closest-hit rays (PG_BVH4 builds; 8 x float4 = 128 B, one L2 line), collapsed
+// from the same binary tree by opening the largest-area inner child until four slots are used:
+//   [0] lo.x[4]  [1] hi.x[4]  [2] lo.y[4]  [3] hi.y[4]  [4] lo.z[4]  [5] hi.z[4]   (slot order)
+//   [6] bits(child[4]) with the binary node's encoding (>= 0 inner, < 0 leaf), PG_QNODE_EMPTY unused
+//   [7] 0
+#ifndef PG_BVH4
+#define PG_BVH4 0
+#endif
+#define PG_QNODE_F4 8
+#define PG_QNODE_EMPTY 0x7ffffffe
+// closest-hit stack entries a 4-wide traversal may need (the builder checks its trees against it;
+// the global overflow ring already holds PG_QSTACK_DEPTH - LDS_STACK words per thread)
+#define PG_QSTACK_DEPTH 96
+
 // 8-wide BVH node for shadow rays, with quantised child boxes (5 x float4 = 80 B; after Ylitie et al. 2017):
 //   [0] p.xyz (quantisation origin = node box min), bits(ex | ey << 8 | ez << 16 | imask << 24)
 //       child box coordinate = p + q * 2^(e - 127) per axis; imask bit s: slot s is an inner node

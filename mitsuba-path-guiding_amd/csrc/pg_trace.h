@@ -205,15 +205,128 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
     return found;
 }
 
+// Postponed-leaf triangle tests shared by the binary and the 4-wide closest-hit walks: every
+// triangle of leaf ref `leaf` (< 0: ~leaf = first << 4 | count) against the ray.
+template <bool ANY>
+__device__ __forceinline__ bool leafTest(const float4 *__restrict__ woop, int leaf, f3 o, f3 d, float tmin,
+                                         float &tmax, uint32_t &hitTri, float &hu, float &hv, bool &found) {
+    const uint32_t lr = ~(uint32_t)leaf;
+    const uint32_t first = lr >> 4, cnt = lr & 15u;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const uint32_t tr = first + k;
+        const float4 w0 = woop[3 * tr + 0];
+        float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
+        float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
+        float tt = oz / dz;
+        if (tt >= tmin && tt <= tmax) {
+            const float4 w1 = woop[3 * tr + 1];
+            float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
+            if (a >= 0.0f && a <= 1.0f) {
+                const float4 w2 = woop[3 * tr + 2];
+                float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
+                // equal distances: the lower triangle index (see traverseBin)
+                if (b >= 0.0f && a + b <= 1.0f && (tt < tmax || tr < hitTri)) {
+                    found = true;
+                    if (ANY) return true;
+                    tmax = tt;
+                    hitTri = tr;
+                    hu = b;
+                    hv = 1.0f - a - b;
+                }
+            }
+        }
+    }
+    return false;
+}
+
+// ascending compare-exchange of (key, ref) pairs
+__device__ __forceinline__ void cxch(float &ka, int &ra, float &kb, int &rb) {
+    const bool s = kb < ka;
+    const float k = s ? kb : ka;
+    kb = s ? ka : kb;
+    ka = k;
+    const int r = s ? rb : ra;
+    rb = s ? ra : rb;
+    ra = r;
+}
+
+// Closest-hit walk of the 4-wide BVH (PG_BVH4): one 128-B node per visit instead of two 64-B binary
+// nodes, its hit children visited nearest first (a 5-exchange sorting network on the entry
+// distances; the others pushed far to near), with the binary walk's while-while loop, postponed
+// leaves, tie rule and widened culling distance, so it returns the same hit.
+template <bool ANY>
+__device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+                                          float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
+                                          const TStack &stk) {
+    const int DONE = 0x7fffffff;
+    const float eps = 1e-30f;
+    const float INF = __builtin_huge_valf();
+    const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
+                       1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
+                       1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+    const f3 ood = o * idir;
+    const float tslack = 1e-6f * fmaxf(fmaxf(fabsf(ood.x), fabsf(ood.y)), fabsf(ood.z));
+    int sp = 0;
+    int node = 0;
+    int leaf = 0;
+    bool found = false;
+    while (node != DONE) {
+        const float tcull = tmax * 1.000001f + tslack;
+        while (node >= 0 && node != DONE) {
+            const float4 *np = nodes + (size_t)PG_QNODE_F4 * node;
+            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+            const float4 rf = np[6];
+            float k[4];
+            int r[4];
+#define PG_Q4_SLOT(i, c)                                                                              \
+    {                                                                                                 \
+        const float x0 = fmaf(lx.c, idir.x, -ood.x), x1 = fmaf(hx.c, idir.x, -ood.x);                 \
+        const float y0 = fmaf(ly.c, idir.y, -ood.y), y1 = fmaf(hy.c, idir.y, -ood.y);                 \
+        const float z0 = fmaf(lz.c, idir.z, -ood.z), z1 = fmaf(hz.c, idir.z, -ood.z);                 \
+        const float cmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));    \
+        const float cmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcull));   \
+        r[i] = __float_as_int(rf.c);                                                                  \
+        k[i] = (cmin <= cmax && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                                 \
+    }
+            PG_Q4_SLOT(0, x) PG_Q4_SLOT(1, y) PG_Q4_SLOT(2, z) PG_Q4_SLOT(3, w)
+#undef PG_Q4_SLOT
+            cxch(k[0], r[0], k[1], r[1]);
+            cxch(k[2], r[2], k[3], r[3]);
+            cxch(k[0], r[0], k[2], r[2]);
+            cxch(k[1], r[1], k[3], r[3]);
+            cxch(k[1], r[1], k[2], r[2]);
+            if (k[0] == INF) {
+                node = sp > 0 ? (int)stk.get(--sp) : DONE;
+            } else {
+                node = r[0];
+                if (k[3] != INF && sp < PG_QSTACK_DEPTH) stk.put(sp++, (uint32_t)r[3]);
+                if (k[2] != INF && sp < PG_QSTACK_DEPTH) stk.put(sp++, (uint32_t)r[2]);
+                if (k[1] != INF && sp < PG_QSTACK_DEPTH) stk.put(sp++, (uint32_t)r[1]);
+            }
+            if (node < 0 && leaf >= 0) {
+                leaf = node;
+                node = sp > 0 ? (int)stk.get(--sp) : DONE;
+            }
+            if (!__any(leaf >= 0)) break;
+        }
+        while (leaf < 0) {
+            if (leafTest<ANY>(woop, leaf, o, d, tmin, tmax, hitTri, hu, hv, found)) return true;
+            leaf = node;
+            if (node < 0) node = sp > 0 ? (int)stk.get(--sp) : DONE;
+        }
+    }
+    return found;
+}
+
 // While-while traversal with postponed leaves (Aila & Laine 2009): lanes keep descending inner
 // nodes until every lane of the wave holds a leaf, then all lanes test triangles together.  This
 // keeps the 64-wide wave in one code path most of the time (if-if traversal measured 23 % lane
 // utilisation on gfx950).
 // LTOP: nodes [0, ntop) are read from `lnodes` (the top levels, staged in LDS by the caller).
 template <bool ANY, bool LTOP = false>
-__device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
-                                         float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                         const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
+__device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+                                            float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
+                                            const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
     const int DONE = 0x7fffffff;
     const float eps = 1e-30f;
     const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
@@ -312,6 +425,19 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
         }
     }
     return found;
+}
+
+// the closest-hit walk of this build's closest-hit BVH (SceneDev::nodes)
+template <bool ANY, bool LTOP = false>
+__device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+                                         float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
+                                         const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
+#if PG_BVH4
+    static_assert(!LTOP, "LDS-staged top levels are a binary-BVH option");
+    return traverse4<ANY>(nodes, woop, o, d, tmin, tmax, hitTri, hu, hv, stk);
+#else
+    return traverseBin<ANY, LTOP>(nodes, woop, o, d, tmin, tmax, hitTri, hu, hv, stk, lnodes, ntop);
+#endif
 }
 
 __device__ __forceinline__ float miWeight(float a, float b) {
