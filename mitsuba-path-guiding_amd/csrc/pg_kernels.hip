@@ -205,11 +205,7 @@ __device__ __forceinline__ void shadowRows(const SceneDev &sc, const PathDev &p,
         uint32_t slot = items[i];
         // the shadow ray starts at the shading point, which is also the extension ray's origin
         float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.sh_d[slot]);
-        float tmax = d.w;
-        uint32_t tri = 0xFFFFFFFFu;
-        float u, v;
-        bool occ = traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), shadowTmin(o), tmax, tri, u, v, stk);
-        if (!occ) {
+        if (!occluded(sc, xyz(o), xyz(d), shadowTmin(o), d.w, stk)) {
             float4 c = ldS(&p.sh_c[slot]);
             float4 L = ldS(&p.rad[slot]);
             stS(&p.rad[slot], make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w));
@@ -657,9 +653,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_tail(GParams g, SceneDev sc, SD
             if (shadow) {  // shadowRows for this path
                 ++shadows;
                 const float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.sh_d[slot]);
-                float tmax = d.w, u, v;
-                uint32_t t2 = 0xFFFFFFFFu;
-                if (!traverseWide<true>(sc.wnodes, sc.wwoop, xyz(o), xyz(d), shadowTmin(o), tmax, t2, u, v, wstk)) {
+                if (!occluded(sc, xyz(o), xyz(d), shadowTmin(o), d.w, wstk)) {
                     const float4 c = ldS(&p.sh_c[slot]);
                     const float4 L = ldS(&p.rad[slot]);
                     stS(&p.rad[slot], make_float4(L.x + c.x, L.y + c.y, L.z + c.z, L.w));
@@ -1039,7 +1033,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const f
     float u = 0, v = 0;
     float *h = hits + 4 * (size_t)i;
     if (any) {
-        bool occ = traverseWide<true>(sc.wnodes, sc.wwoop, o, d, r[3], tmax, tri, u, v, wstk);
+        bool occ = occluded(sc, o, d, r[3], tmax, wstk);
         h[0] = occ ? 1.0f : 0.0f;
         h[1] = h[2] = h[3] = 0.0f;
         return;

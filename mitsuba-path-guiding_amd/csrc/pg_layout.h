@@ -113,7 +113,7 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 // The same layout is used for the compact emitter-triangle array.
 #define PG_TRI_SHADE_F4 5
 
-// Binary BVH node for closest-hit rays (4 x float4 = 64 B):
+// Binary BVH node for closest-hit rays (PG_BVH4 = 0 builds; 4 x float4 = 64 B):
 //   [0] c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y   [1] c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y
 //   [2] c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z   [3] bits(child0), bits(child1), 0, 0
 // child >= 0: inner node index; child < 0: leaf, ~child = (first_tri << 4) | count (count <= 15).
@@ -124,13 +124,14 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 #define PG_BVH_TOP_LEVELS 5
 #define PG_BVH_TOP_NODES 31
 
-// 4-wide BVH node for closest-hit rays (PG_BVH4 builds; 8 x float4 = 128 B, one L2 line), collapsed
-// from the same binary tree by opening the largest-area inner child until four slots are used:
+// 4-wide BVH node for closest-hit rays (default, PG_BVH4 = 1; 8 x float4 = 128 B, one L2 line), collapsed
+// from the same binary tree by opening the largest-area inner child until four slots are used
+// (C3 +1.5 %, kitchen +6.9 %, C5 +3.1 % over the binary nodes, identical results; profiles/r03za_bvh4_ab):
 //   [0] lo.x[4]  [1] hi.x[4]  [2] lo.y[4]  [3] hi.y[4]  [4] lo.z[4]  [5] hi.z[4]   (slot order)
 //   [6] bits(child[4]) with the binary node's encoding (>= 0 inner, < 0 leaf), PG_QNODE_EMPTY unused
 //   [7] 0
 #ifndef PG_BVH4
-#define PG_BVH4 0
+#define PG_BVH4 1
 #endif
 #define PG_QNODE_F4 8
 #define PG_QNODE_EMPTY 0x7ffffffe

@@ -38,8 +38,8 @@ __device__ __forceinline__ void stS(uint4 *p, uint4 a) { *p = a; }
 // ---------------------------------------------------------------------------------------------
 // BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,
 // sahkdtree3.h:178-308) with the same contract: closest t in [tmin, tmax] (any hit for shadow
-// rays).  Closest-hit rays walk the binary BVH (64-B nodes), shadow rays the 8-wide BVH with
-// quantised boxes (80-B nodes); both test 48-B Woop unit triangles.
+// rays).  Closest-hit rays walk the 4-wide BVH (128-B nodes; the binary BVH's 64-B nodes in PG_BVH4 = 0
+// builds), shadow rays the 8-wide BVH with quantised boxes (80-B nodes); all test 48-B Woop unit triangles.
 // Stacks: entries [0, LDS) in LDS (columns per thread, stride TRACE_BLOCK: conflict-free), deeper
 // entries in a per-thread column of a global overflow ring (stride = launched threads).
 struct TStack {
@@ -437,6 +437,21 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
     return traverse4<ANY>(nodes, woop, o, d, tmin, tmax, hitTri, hu, hv, stk);
 #else
     return traverseBin<ANY, LTOP>(nodes, woop, o, d, tmin, tmax, hitTri, hu, hv, stk, lnodes, ntop);
+#endif
+}
+
+// shadow-ray any hit: the 8-wide BVH, or the 4-wide closest-hit BVH in PG_SHADOW4 builds (A/B; the
+// 4-wide walk's stack is the wide stack's storage, >= LDS_STACK LDS words + the shared overflow ring)
+#ifndef PG_SHADOW4
+#define PG_SHADOW4 0
+#endif
+__device__ __forceinline__ bool occluded(const SceneDev &sc, f3 o, f3 d, float tmin, float tmax, const WStack &w) {
+    uint32_t tri = 0xFFFFFFFFu;
+    float u, v;
+#if PG_BVH4 && PG_SHADOW4
+    return traverse4<true>(sc.nodes, sc.woop, o, d, tmin, tmax, tri, u, v, TStack{w.lds, w.ovf, w.ostride});
+#else
+    return traverseWide<true>(sc.wnodes, sc.wwoop, o, d, tmin, tmax, tri, u, v, w);
 #endif
 }
 
