@@ -518,11 +518,77 @@ static bool buildBinaryBvh(const std::vector<BNode> &bn, uint32_t maxDepth, cons
     return true;
 }
 
-// 4-wide BVH (PG_BVH4, closest hit) over the same tree: each node takes a binary inner node's two
-// children and opens the largest-area inner child until it has four; its leaves are the binary
-// leaves (same refs).  Nodes are stored in depth-first order.  Fails if a root-to-leaf walk could
-// hold more than PG_QSTACK_DEPTH stack entries (the siblings pushed at every level).
+// 4-wide BVH (PG_BVH4, closest hit) over the same tree; its leaves are the binary leaves (same refs).
+// Which binary nodes a 4-wide node absorbs is the SAH-optimal choice (the 8-wide collapse's dynamic
+// programme with 4 slots and the leaves fixed: it minimises the summed surface area of the opened
+// nodes, i.e. the expected node visits); PG_BVH4_GREEDY=1 opens the largest-area inner child
+// instead (A/B).  Siblings are stored consecutively, nodes depth first.  Fails if a root-to-leaf walk
+// could hold more than PG_QSTACK_DEPTH stack entries (the siblings pushed at every level).
 static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_t> &posOf, BvhOut &out) {
+    const bool greedy = std::getenv("PG_BVH4_GREEDY") && std::atoi(std::getenv("PG_BVH4_GREEDY")) != 0;
+    const size_t nb = bn.size();
+    constexpr float kInf = std::numeric_limits<float>::infinity();
+    // dist[n][j]: least summed area of opened nodes to spread subtree n over at most j slots
+    std::vector<std::array<float, 5>> dist(nb);
+    std::vector<std::array<uint8_t, 5>> splitK(nb);
+    {
+        std::vector<int32_t> post, s{0};
+        while (!s.empty()) {
+            const int32_t n = s.back();
+            s.pop_back();
+            post.push_back(n);
+            if (!bn[n].leaf) {
+                s.push_back(bn[n].child[0]);
+                s.push_back(bn[n].child[1]);
+            }
+        }
+        for (size_t i = post.size(); i-- > 0;) {
+            const int32_t n = post[i];
+            splitK[n].fill(0);
+            if (bn[n].leaf) {
+                dist[n].fill(0.0f);
+                continue;
+            }
+            const int32_t L = bn[n].child[0], R = bn[n].child[1];
+            float best = kInf;
+            for (int k = 1; k < 4; ++k) best = std::min(best, dist[L][k] + dist[R][4 - k]);
+            dist[n][1] = bn[n].box.area() + best;  // n as one slot: an opened 4-wide node
+            for (int j = 2; j <= 4; ++j) {
+                dist[n][j] = dist[n][1];
+                for (int k = 1; k < j; ++k) {
+                    const float c = dist[L][k] + dist[R][j - k];
+                    if (c < dist[n][j]) {
+                        dist[n][j] = c;
+                        splitK[n][j] = (uint8_t)k;
+                    }
+                }
+            }
+        }
+    }
+    // the slots of opened node n along the programme's choices
+    auto collect = [&](int32_t n, std::vector<int32_t> &ch) {
+        int bestK = 1;
+        float best = kInf;
+        for (int k = 1; k < 4; ++k) {
+            const float c = dist[bn[n].child[0]][k] + dist[bn[n].child[1]][4 - k];
+            if (c < best) {
+                best = c;
+                bestK = k;
+            }
+        }
+        std::vector<std::pair<int32_t, int>> s{{bn[n].child[1], 4 - bestK}, {bn[n].child[0], bestK}};
+        while (!s.empty()) {
+            auto [m, j] = s.back();
+            s.pop_back();
+            const int k = bn[m].leaf ? 0 : splitK[m][j];
+            if (k == 0) {
+                ch.push_back(m);
+            } else {
+                s.push_back({bn[m].child[1], j - k});
+                s.push_back({bn[m].child[0], k});
+            }
+        }
+    };
     auto ref = [&](int32_t n, int32_t inner) -> int32_t {
         if (bn[n].leaf) return (int32_t)(~((posOf[bn[n].first] << 4) | bn[n].count));
         return inner;
@@ -552,8 +618,10 @@ static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_
     while (!st.empty()) {
         const QTask t = st.back();
         st.pop_back();
-        std::vector<int32_t> ch{bn[t.bnode].child[0], bn[t.bnode].child[1]};
-        while (ch.size() < 4) {
+        std::vector<int32_t> ch;
+        if (!greedy) collect(t.bnode, ch);
+        else ch = {bn[t.bnode].child[0], bn[t.bnode].child[1]};
+        while (greedy && ch.size() < 4) {
             int best = -1;
             float bestA = -1.0f;
             for (size_t i = 0; i < ch.size(); ++i)
