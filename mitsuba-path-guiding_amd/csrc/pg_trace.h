@@ -286,7 +286,7 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
         const float cmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));    \
         const float cmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcull));   \
         r[i] = __float_as_int(rf.c);                                                                  \
-        k[i] = (cmin <= cmax && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                                 \
+        k[i] = (cmin <= cmax + tslack && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                                 \
     }
             PG_Q4_SLOT(0, x) PG_Q4_SLOT(1, y) PG_Q4_SLOT(2, z) PG_Q4_SLOT(3, w)
 #undef PG_Q4_SLOT
@@ -343,7 +343,9 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
         // boxes are culled against tmax widened by the slab-distance rounding: a triangle that ties
         // with the current hit (shared edge, coplanar) can sit in a box whose rounded entry distance
         // lands just past tmax, and skipping it would make the tie-break (lower index) depend on
-        // traversal order, i.e. on which paths share the wave
+        // traversal order, i.e. on which paths share the wave.  The same slack widens every box
+        // interval (cmin <= cmax + tslack): a ray that clips a box near an edge can see its rounded
+        // interval come out empty while it hits the triangle inside (tests/test_bvh4_build.py)
         const float tcull = tmax * 1.000001f + tslack;
         while (node >= 0 && node != DONE) {
             float4 n0, n1, n2, n3;
@@ -368,7 +370,7 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
             float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
             float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), tmin));
             float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tcull));
-            const bool h0 = c0min <= c0max, h1 = c1min <= c1max;
+            const bool h0 = c0min <= c0max + tslack, h1 = c1min <= c1max + tslack;
             const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
             if (!h0 && !h1) {
                 node = sp > 0 ? (int)stk.get(--sp) : DONE;

@@ -1,0 +1,184 @@
+// Test-only shim (tests/test_bvh4_build.py): the library's BVH builder (pg_bvh.cpp) on the CPU.
+// Checks the 4-wide closest-hit layout (pg_layout.h PG_QNODE_*) for structure -- every triangle in
+// exactly one leaf, child boxes containing their subtrees, the stack bound -- and runs a scalar
+// restatement of the device walk (traverse4: slab test widened by the rounding slack, culling distance, nearest-first
+// order, lower-index tie rule) against a brute-force loop over the same Woop records.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../mitsuba-path-guiding_amd/csrc/pg_bvh.h"
+#include "../../mitsuba-path-guiding_amd/csrc/pg_layout.h"
+
+namespace {
+pgh::BvhOut g_bvh;
+std::vector<float> g_P;
+std::vector<uint32_t> g_I;
+
+bool woopHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax, float &tt) {
+    const float *w = &g_bvh.woop[12 * (size_t)tr];
+    const float dz = d[0] * w[0] + d[1] * w[1] + d[2] * w[2];
+    const float oz = w[3] - (o[0] * w[0] + o[1] * w[1] + o[2] * w[2]);
+    tt = oz / dz;
+    if (!(tt >= tmin && tt <= tmax)) return false;
+    const float a = (w[7] + o[0] * w[4] + o[1] * w[5] + o[2] * w[6]) + tt * (d[0] * w[4] + d[1] * w[5] + d[2] * w[6]);
+    if (!(a >= 0.0f && a <= 1.0f)) return false;
+    const float b = (w[11] + o[0] * w[8] + o[1] * w[9] + o[2] * w[10]) + tt * (d[0] * w[8] + d[1] * w[9] + d[2] * w[10]);
+    return b >= 0.0f && a + b <= 1.0f;
+}
+
+const float *qnode(int32_t n) { return &g_bvh.nodes[(size_t)n * 4 * PG_QNODE_F4]; }
+int32_t qref(int32_t n, int s) {
+    int32_t r;
+    std::memcpy(&r, &qnode(n)[24 + s], 4);
+    return r;
+}
+}  // namespace
+
+extern "C" {
+
+// 1: built; 0: the builder refused (stack bound)
+int shim_build(const float *P, uint32_t nv, const uint32_t *I, uint32_t nt) {
+    g_P.assign(P, P + 3 * (size_t)nv);
+    g_I.assign(I, I + 3 * (size_t)nt);
+    g_bvh = pgh::BvhOut();
+    return pgh::buildBvh(g_P.data(), g_I.data(), nt, 48, g_bvh) ? 1 : 0;
+}
+
+// structure of the 4-wide tree: out[0] nodes, out[1] max stack need, out[2] triangles reached
+// exactly once (all: == nt), out[3] child boxes not containing their subtree's triangles, out[4] depth
+void shim_check(uint32_t nt, uint32_t *out) {
+    const uint32_t nn = (uint32_t)(g_bvh.nodes.size() / (4 * PG_QNODE_F4));
+    std::vector<uint32_t> seen(nt, 0);
+    uint32_t bad = 0, maxNeed = 0, maxDepth = 0;
+    struct T { int32_t n; uint32_t need, depth; };
+    std::vector<T> st{{0, 1, 1}};
+    while (!st.empty()) {
+        const T t = st.back();
+        st.pop_back();
+        maxDepth = std::max(maxDepth, t.depth);
+        const float *o = qnode(t.n);
+        int used = 0;
+        for (int s = 0; s < 4; ++s) used += qref(t.n, s) != PG_QNODE_EMPTY;
+        const uint32_t need = t.need + (used > 0 ? used - 1 : 0);
+        maxNeed = std::max(maxNeed, need);
+        for (int s = 0; s < 4; ++s) {
+            const int32_t r = qref(t.n, s);
+            if (r == PG_QNODE_EMPTY) continue;
+            float lo[3], hi[3];
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = o[8 * a + s];
+                hi[a] = o[8 * a + 4 + s];
+            }
+            // triangles of the child's subtree
+            std::vector<int32_t> sub{r};
+            while (!sub.empty()) {
+                const int32_t m = sub.back();
+                sub.pop_back();
+                if (m >= 0) {
+                    for (int k = 0; k < 4; ++k)
+                        if (qref(m, k) != PG_QNODE_EMPTY) sub.push_back(qref(m, k));
+                    continue;
+                }
+                const uint32_t lr = ~(uint32_t)m, first = lr >> 4, cnt = lr & 15u;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const uint32_t orig = g_bvh.order[first + k];
+                    for (int j = 0; j < 3; ++j)
+                        for (int a = 0; a < 3; ++a) {
+                            const float v = g_P[3 * (size_t)g_I[3 * (size_t)orig + j] + a];
+                            if (v < lo[a] || v > hi[a]) ++bad;
+                        }
+                }
+            }
+            if (r >= 0) {
+                st.push_back({r, need, t.depth + 1});
+            } else {
+                const uint32_t lr = ~(uint32_t)r, first = lr >> 4, cnt = lr & 15u;
+                for (uint32_t k = 0; k < cnt; ++k) seen[first + k]++;
+            }
+        }
+    }
+    uint32_t once = 0;
+    for (uint32_t i = 0; i < nt; ++i) once += seen[i] == 1;
+    out[0] = nn;
+    out[1] = maxNeed;
+    out[2] = once;
+    out[3] = bad;
+    out[4] = maxDepth;
+}
+
+// rays: 8 floats (o, tmin, d, tmax); hits: 2 words (bits(t), BVH-order triangle or ~0) per ray for the
+// walk and for brute force
+void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, uint32_t nt) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * (size_t)i;
+        const float o[3] = {r[0], r[1], r[2]}, d[3] = {r[4], r[5], r[6]};
+        // brute force, the same tie rule
+        {
+            float tmax = r[7];
+            uint32_t best = 0xFFFFFFFFu;
+            for (uint32_t tr = 0; tr < nt; ++tr) {
+                float tt;
+                if (woopHit(tr, o, d, r[3], tmax, tt) && (tt < tmax || tr < best)) {
+                    tmax = tt;
+                    best = tr;
+                }
+            }
+            std::memcpy(&brute[2 * i], &tmax, 4);
+            brute[2 * i + 1] = best;
+        }
+        // traverse4
+        const float eps = 1e-30f;
+        float idir[3], ood[3];
+        for (int a = 0; a < 3; ++a) {
+            idir[a] = 1.0f / (std::fabs(d[a]) > eps ? d[a] : std::copysign(eps, d[a]));
+            ood[a] = o[a] * idir[a];
+        }
+        const float tslack = 1e-6f * std::fmax(std::fmax(std::fabs(ood[0]), std::fabs(ood[1])), std::fabs(ood[2]));
+        float tmax = r[7];
+        uint32_t best = 0xFFFFFFFFu;
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            const int32_t node = st.back();
+            st.pop_back();
+            if (node < 0) {
+                const uint32_t lr = ~(uint32_t)node, first = lr >> 4, cnt = lr & 15u;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    float tt;
+                    if (woopHit(first + k, o, d, r[3], tmax, tt) && (tt < tmax || first + k < best)) {
+                        tmax = tt;
+                        best = first + k;
+                    }
+                }
+                continue;
+            }
+            const float tcull = tmax * 1.000001f + tslack;
+            const float *q = qnode(node);
+            float key[4];
+            int32_t ref[4];
+            for (int s = 0; s < 4; ++s) {
+                float cmin = r[3], cmax = tcull;
+                for (int a = 0; a < 3; ++a) {
+                    const float t0 = std::fma(q[8 * a + s], idir[a], -ood[a]);
+                    const float t1 = std::fma(q[8 * a + 4 + s], idir[a], -ood[a]);
+                    cmin = std::fmax(cmin, std::fmin(t0, t1));
+                    cmax = std::fmin(cmax, std::fmax(t0, t1));
+                }
+                ref[s] = qref(node, s);
+                key[s] = (cmin <= cmax + tslack && ref[s] != PG_QNODE_EMPTY) ? cmin : INFINITY;
+            }
+            for (int a = 0; a < 4; ++a)  // far to near onto the stack
+                for (int b = a + 1; b < 4; ++b)
+                    if (key[b] > key[a]) {
+                        std::swap(key[a], key[b]);
+                        std::swap(ref[a], ref[b]);
+                    }
+            for (int s = 0; s < 4; ++s)
+                if (key[s] != INFINITY) st.push_back(ref[s]);
+        }
+        std::memcpy(&walk[2 * i], &tmax, 4);
+        walk[2 * i + 1] = best;
+    }
+}
+}
