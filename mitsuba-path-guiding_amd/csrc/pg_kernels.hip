@@ -229,15 +229,27 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
 // record, not to L, so it cannot race with the same path's NEE add).  Both parts are grid-stride loops over their shards; the
 // overflow ring holds two launches' worth of threads (2 x pg_stack_overflow_words(0)).
 static_assert(2 * WIDE_LDS_STACK >= LDS_STACK, "k_rays / k_trace_rays share one LDS stack array");
+#ifndef PG_RAYS_TRACE_FIRST
+#define PG_RAYS_TRACE_FIRST 0
+#endif
 template <bool ENV>
 __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                       Queue shq, uint32_t shadow_blocks) {
     __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
+#if PG_RAYS_TRACE_FIRST  // A/B: the costlier closest-hit blocks dispatched first
+    const uint32_t trace_blocks = gridDim.x - shadow_blocks;
+    if (blockIdx.x >= trace_blocks)
+        shadowRows(sc, p, shq, blockIdx.x - trace_blocks, shadow_blocks, threadWideStack(stack, p.stack_ovf));
+    else
+        traceRows<ENV, false>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks, threadStack(stack, p.stack_ovf),
+                              nullptr, 0);
+#else
     if (blockIdx.x < shadow_blocks)
         shadowRows(sc, p, shq, blockIdx.x, shadow_blocks, threadWideStack(stack, p.stack_ovf));
     else
         traceRows<ENV, false>(g, sc, p, q, cqs, nullptr, blockIdx.x - shadow_blocks, gridDim.x - shadow_blocks,
                                 threadStack(stack, p.stack_ovf), nullptr, 0);
+#endif
 }
 
 // ray order key of a new extension ray (PG_RAY_SORT): direction octant, then the Morton code of the
