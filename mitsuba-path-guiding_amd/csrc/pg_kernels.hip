@@ -47,9 +47,10 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     f3 wd = left * d.x + up * d.y + dir * d.z;
     stS(&p.ray_o[slot], make_float4(g.cam_o[0], g.cam_o[1], g.cam_o[2], g.near_clip * invZ));
     stS(&p.ray_d[slot], f4(wd, g.far_clip * invZ));
-    stS(&p.thr[slot], make_float4(1.f, 1.f, 1.f, 1.f));
+    // throughput (1, eta 1) and the previous vertex are implied by depth 1: the first bounce's readers
+    // (shadeOne, envEscapeRadiance) do not load them.  L = 0 is stored: a camera ray that escapes is
+    // never shaded and k_film reads its L.
     stS(&p.rad[slot], make_float4(0.f, 0.f, 0.f, 0.f));
-    stS(&p.prev[slot], make_float4(0.f, 0.f, 0.f, 0.f));
     stS(&p.pinfo[slot], make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u));
     q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
 }
@@ -82,12 +83,12 @@ __device__ __forceinline__ f3 envEscapeRadiance(const GParams &g, const SceneDev
                                                 f3 rd) {
     const uint4 pi = p.pinfo[slot];
     const uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16;
-    const float4 T4 = p.thr[slot];
     f3 add;
-    if (depth == 1) {  // camera ray: the loop-top miss with EEmittedRadiance
+    if (depth == 1) {  // camera ray (throughput 1): the loop-top miss with EEmittedRadiance
         if (!(flags & PF_EMITTED_QUERY) || (g.hide_emitters && !(flags & PF_SCATTERED))) return mk1(0.f);
-        add = xyz(T4) * envEval(*sc.env, rd);
+        add = envEval(*sc.env, rd);
     } else {
+        const float4 T4 = p.thr[slot];
         if (g.hide_emitters && !(flags & PF_SCATTERED)) return mk1(0.f);
         const float4 pv = p.prev[slot];
         float w = 1.0f;
@@ -230,13 +231,16 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_shadow(SceneDev sc, PathDev p, 
 // overflow ring holds two launches' worth of threads (2 x pg_stack_overflow_words(0)).
 static_assert(2 * WIDE_LDS_STACK >= LDS_STACK, "k_rays / k_trace_rays share one LDS stack array");
 #ifndef PG_RAYS_TRACE_FIRST
-#define PG_RAYS_TRACE_FIRST 0
+#define PG_RAYS_TRACE_FIRST 1
 #endif
 template <bool ENV>
-__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
+#ifndef PG_RAYS_WAVES
+#define PG_RAYS_WAVES 8
+#endif
+__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_RAYS_WAVES))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                       Queue shq, uint32_t shadow_blocks) {
     __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
-#if PG_RAYS_TRACE_FIRST  // A/B: the costlier closest-hit blocks dispatched first
+#if PG_RAYS_TRACE_FIRST  // the costlier closest-hit blocks dispatched first (profiles/r03zg_rays_order_ab)
     const uint32_t trace_blocks = gridDim.x - shadow_blocks;
     if (blockIdx.x >= trace_blocks)
         shadowRows(sc, p, shq, blockIdx.x - trace_blocks, shadow_blocks, threadWideStack(stack, p.stack_ovf));
@@ -290,6 +294,12 @@ __device__ __forceinline__ void waveAppendKey(bool pred, uint32_t value, uint16_
 // one bounce of Li for the path in `slot` (progressive_path.cpp:149-306 + guiding): reads its state,
 // writes the next one; alive = an extension ray was written, shadow = a shadow ray was written (sh_*)
 // mats: the material table (global memory, or a block's LDS copy); wantKey: compute rkey (PG_RAY_SORT)
+// the per-bounce half of a path's info record (depth | flags, vertex count): pixel and sample never
+// change after k_camera, so an 8-B store replaces the 16-B rewrite
+__device__ __forceinline__ void stPinfoZW(uint4 *p, uint32_t z, uint32_t w) {
+    reinterpret_cast<uint2 *>(p)[1] = make_uint2(z, w);
+}
+
 template <int MODEL, bool CAN_GUIDE, bool ENV>
 __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
                                          uint32_t slot, const GMat *mats, bool wantKey, bool &alive, bool &shadow,
@@ -301,8 +311,9 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         const uint32_t pix = pi.x, sample = pi.y;
         uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16, nv = pi.w;
         float4 hv = ldS(&p.hit[slot]);
-        float4 T4 = ldS(&p.thr[slot]);
-        float4 L4 = ldS(&p.rad[slot]);
+        // a camera ray's state is implied (k_camera stores neither throughput nor prev)
+        float4 T4 = depth == 1 ? make_float4(1.f, 1.f, 1.f, 1.f) : ldS(&p.thr[slot]);
+        float4 L4 = depth == 1 ? make_float4(0.f, 0.f, 0.f, 0.f) : ldS(&p.rad[slot]);
         f3 T = xyz(T4);
         L = xyz(L4);
         float eta = T4.w;
@@ -472,7 +483,7 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
                 stS(&p.thr[slot], f4(Tn, eta * bs.eta));
                 stS(&p.prev[slot], f4(refN, woPdf));
                 flags = (flags & ~(PF_EMITTED_QUERY | PF_PREV_DELTA)) | ((bs.type & EDelta) ? PF_PREV_DELTA : 0u);
-                stS(&p.pinfo[slot], make_uint4(pix, sample, (depth + 1) | (flags << 16), nv));
+                stPinfoZW(&p.pinfo[slot], (depth + 1) | (flags << 16), nv);
                 alive = true;
                 if (wantKey) rkey = rayOrderKey(sd, h.p, wo);
             }
@@ -482,7 +493,7 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
             stS(&p.sh_d[slot], f4(neeD, neeDist * (1 - kShadowEpsilon)));
             stS(&p.sh_c[slot], f4(neeC, __uint_as_float(vtxIndex)));
         }
-        if (!alive && nv != pi.w) stS(&p.pinfo[slot], make_uint4(pix, sample, pi.z, nv));
+        if (!alive && nv != pi.w) stPinfoZW(&p.pinfo[slot], pi.z, nv);
     } while (false);
     if (dirtyL) stS(&p.rad[slot], f4(L, 0.0f));
 }

@@ -250,6 +250,37 @@ __device__ __forceinline__ void cxch(float &ka, int &ra, float &kb, int &rb) {
     ra = r;
 }
 
+// Per-ray slab-test setup of the closest-hit walks.  t = fma(plane, idir, add) per axis; with
+// PG_ROBUST_BOX (default) the addends move each axis's near plane earlier and its far plane later by
+// 2^-21 |o_a idir_a| -- a spatial padding of 2^-21 |o_a| along that axis, which bounds the rounding of
+// o * idir and of the fma -- and box intervals are compared as cmin <= cmax (1 + 2^-21) for the
+// rounding relative to t.  Without it a ray clipping a box edge far from the origin could see its
+// rounded interval come out empty while it hits the triangle inside (tests/test_bvh4_build.py, a
+// strip of triangles spanning 1 to 1.6e5: 0.55 % of the rays).  It costs one multiply per box; a
+// global slack of 1e-6 max|o idir| instead made the kitchen's traversal 2.8x slower (near-axis rays).
+#ifndef PG_ROBUST_BOX
+#define PG_ROBUST_BOX 1
+#endif
+struct SlabRay {
+    f3 idir, addLo, addHi;
+    float tslack;  // culling-distance slack (tie rule): a few ulps of the largest |o_a idir_a|
+};
+constexpr float kBoxRel = PG_ROBUST_BOX ? 1.000000477f : 1.0f;  // 1 + 2^-21
+__device__ __forceinline__ SlabRay slabRay(f3 o, f3 d) {
+    const float eps = 1e-30f;
+    SlabRay r;
+    r.idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)), 1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
+                1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
+    const f3 ood = o * r.idir;
+    r.tslack = 1e-6f * fmaxf(fmaxf(fabsf(ood.x), fabsf(ood.y)), fabsf(ood.z));
+    const float k = PG_ROBUST_BOX ? 4.76837158e-7f : 0.0f;  // 2^-21
+    const f3 se = mk(copysignf(k * fabsf(ood.x), r.idir.x), copysignf(k * fabsf(ood.y), r.idir.y),
+                     copysignf(k * fabsf(ood.z), r.idir.z));
+    r.addLo = -ood - se;  // the lo plane is the near one for idir >= 0
+    r.addHi = -ood + se;
+    return r;
+}
+
 // Closest-hit walk of the 4-wide BVH (PG_BVH4): one 128-B node per visit instead of two 64-B binary
 // nodes, its hit children visited nearest first (a 5-exchange sorting network on the entry
 // distances; the others pushed far to near), with the binary walk's while-while loop, postponed
@@ -259,13 +290,10 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
                                           float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                           const TStack &stk) {
     const int DONE = 0x7fffffff;
-    const float eps = 1e-30f;
     const float INF = __builtin_huge_valf();
-    const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
-                       1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-                       1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
-    const f3 ood = o * idir;
-    const float tslack = 1e-6f * fmaxf(fmaxf(fabsf(ood.x), fabsf(ood.y)), fabsf(ood.z));
+    const SlabRay sr = slabRay(o, d);
+    const f3 idir = sr.idir, aLo = sr.addLo, aHi = sr.addHi;
+    const float tslack = sr.tslack;
     int sp = 0;
     int node = 0;
     int leaf = 0;
@@ -280,13 +308,13 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
             int r[4];
 #define PG_Q4_SLOT(i, c)                                                                              \
     {                                                                                                 \
-        const float x0 = fmaf(lx.c, idir.x, -ood.x), x1 = fmaf(hx.c, idir.x, -ood.x);                 \
-        const float y0 = fmaf(ly.c, idir.y, -ood.y), y1 = fmaf(hy.c, idir.y, -ood.y);                 \
-        const float z0 = fmaf(lz.c, idir.z, -ood.z), z1 = fmaf(hz.c, idir.z, -ood.z);                 \
+        const float x0 = fmaf(lx.c, idir.x, aLo.x), x1 = fmaf(hx.c, idir.x, aHi.x);                   \
+        const float y0 = fmaf(ly.c, idir.y, aLo.y), y1 = fmaf(hy.c, idir.y, aHi.y);                   \
+        const float z0 = fmaf(lz.c, idir.z, aLo.z), z1 = fmaf(hz.c, idir.z, aHi.z);                   \
         const float cmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));    \
         const float cmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcull));   \
         r[i] = __float_as_int(rf.c);                                                                  \
-        k[i] = (cmin <= cmax + tslack && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                                 \
+        k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
     }
             PG_Q4_SLOT(0, x) PG_Q4_SLOT(1, y) PG_Q4_SLOT(2, z) PG_Q4_SLOT(3, w)
 #undef PG_Q4_SLOT
@@ -328,13 +356,10 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
                                             float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                             const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
     const int DONE = 0x7fffffff;
-    const float eps = 1e-30f;
-    const f3 idir = mk(1.0f / (fabsf(d.x) > eps ? d.x : copysignf(eps, d.x)),
-                       1.0f / (fabsf(d.y) > eps ? d.y : copysignf(eps, d.y)),
-                       1.0f / (fabsf(d.z) > eps ? d.z : copysignf(eps, d.z)));
-    const f3 ood = o * idir;
+    const SlabRay sr = slabRay(o, d);
+    const f3 idir = sr.idir, aLo = sr.addLo, aHi = sr.addHi;
     // rounding of the slab distances fma(plane, idir, -o * idir) is bounded by a few ulps of |o * idir|
-    const float tslack = 1e-6f * fmaxf(fmaxf(fabsf(ood.x), fabsf(ood.y)), fabsf(ood.z));
+    const float tslack = sr.tslack;
     int sp = 0;
     int node = 0;   // >= 0 inner node, < 0 leaf ref, DONE
     int leaf = 0;   // postponed leaf ref (< 0) or none (>= 0)
@@ -343,9 +368,7 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
         // boxes are culled against tmax widened by the slab-distance rounding: a triangle that ties
         // with the current hit (shared edge, coplanar) can sit in a box whose rounded entry distance
         // lands just past tmax, and skipping it would make the tie-break (lower index) depend on
-        // traversal order, i.e. on which paths share the wave.  The same slack widens every box
-        // interval (cmin <= cmax + tslack): a ray that clips a box near an edge can see its rounded
-        // interval come out empty while it hits the triangle inside (tests/test_bvh4_build.py)
+        // traversal order, i.e. on which paths share the wave (box intervals: slabRay)
         const float tcull = tmax * 1.000001f + tslack;
         while (node >= 0 && node != DONE) {
             float4 n0, n1, n2, n3;
@@ -360,17 +383,17 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
                 n2 = nodes[4 * node + 2];
                 n3 = nodes[4 * node + 3];
             }
-            float a0 = fmaf(n0.x, idir.x, -ood.x), a1 = fmaf(n0.y, idir.x, -ood.x);
-            float a2 = fmaf(n0.z, idir.y, -ood.y), a3 = fmaf(n0.w, idir.y, -ood.y);
-            float a4 = fmaf(n2.x, idir.z, -ood.z), a5 = fmaf(n2.y, idir.z, -ood.z);
+            float a0 = fmaf(n0.x, idir.x, aLo.x), a1 = fmaf(n0.y, idir.x, aHi.x);
+            float a2 = fmaf(n0.z, idir.y, aLo.y), a3 = fmaf(n0.w, idir.y, aHi.y);
+            float a4 = fmaf(n2.x, idir.z, aLo.z), a5 = fmaf(n2.y, idir.z, aHi.z);
             float c0min = fmaxf(fmaxf(fminf(a0, a1), fminf(a2, a3)), fmaxf(fminf(a4, a5), tmin));
             float c0max = fminf(fminf(fmaxf(a0, a1), fmaxf(a2, a3)), fminf(fmaxf(a4, a5), tcull));
-            float b0 = fmaf(n1.x, idir.x, -ood.x), b1 = fmaf(n1.y, idir.x, -ood.x);
-            float b2 = fmaf(n1.z, idir.y, -ood.y), b3 = fmaf(n1.w, idir.y, -ood.y);
-            float b4 = fmaf(n2.z, idir.z, -ood.z), b5 = fmaf(n2.w, idir.z, -ood.z);
+            float b0 = fmaf(n1.x, idir.x, aLo.x), b1 = fmaf(n1.y, idir.x, aHi.x);
+            float b2 = fmaf(n1.z, idir.y, aLo.y), b3 = fmaf(n1.w, idir.y, aHi.y);
+            float b4 = fmaf(n2.z, idir.z, aLo.z), b5 = fmaf(n2.w, idir.z, aHi.z);
             float c1min = fmaxf(fmaxf(fminf(b0, b1), fminf(b2, b3)), fmaxf(fminf(b4, b5), tmin));
             float c1max = fminf(fminf(fmaxf(b0, b1), fmaxf(b2, b3)), fminf(fmaxf(b4, b5), tcull));
-            const bool h0 = c0min <= c0max + tslack, h1 = c1min <= c1max + tslack;
+            const bool h0 = c0min <= c0max * kBoxRel, h1 = c1min <= c1max * kBoxRel;
             const int ch0 = __float_as_int(n3.x), ch1 = __float_as_int(n3.y);
             if (!h0 && !h1) {
                 node = sp > 0 ? (int)stk.get(--sp) : DONE;

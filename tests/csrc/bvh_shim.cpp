@@ -1,7 +1,7 @@
 // Test-only shim (tests/test_bvh4_build.py): the library's BVH builder (pg_bvh.cpp) on the CPU.
 // Checks the 4-wide closest-hit layout (pg_layout.h PG_QNODE_*) for structure -- every triangle in
 // exactly one leaf, child boxes containing their subtrees, the stack bound -- and runs a scalar
-// restatement of the device walk (traverse4: slab test widened by the rounding slack, culling distance, nearest-first
+// restatement of the device walk (traverse4: slabRay's padded slab test, widened culling distance, nearest-first
 // order, lower-index tie rule) against a brute-force loop over the same Woop records.
 #include <cmath>
 #include <cstdint>
@@ -136,6 +136,12 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
             ood[a] = o[a] * idir[a];
         }
         const float tslack = 1e-6f * std::fmax(std::fmax(std::fabs(ood[0]), std::fabs(ood[1])), std::fabs(ood[2]));
+        float addLo[3], addHi[3];  // slabRay: near planes earlier, far planes later by 2^-21 |o_a idir_a|
+        for (int a = 0; a < 3; ++a) {
+            const float se = std::copysign(4.76837158e-7f * std::fabs(ood[a]), idir[a]);
+            addLo[a] = -ood[a] - se;
+            addHi[a] = -ood[a] + se;
+        }
         float tmax = r[7];
         uint32_t best = 0xFFFFFFFFu;
         std::vector<int32_t> st{0};
@@ -160,13 +166,13 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
             for (int s = 0; s < 4; ++s) {
                 float cmin = r[3], cmax = tcull;
                 for (int a = 0; a < 3; ++a) {
-                    const float t0 = std::fma(q[8 * a + s], idir[a], -ood[a]);
-                    const float t1 = std::fma(q[8 * a + 4 + s], idir[a], -ood[a]);
+                    const float t0 = std::fma(q[8 * a + s], idir[a], addLo[a]);
+                    const float t1 = std::fma(q[8 * a + 4 + s], idir[a], addHi[a]);
                     cmin = std::fmax(cmin, std::fmin(t0, t1));
                     cmax = std::fmin(cmax, std::fmax(t0, t1));
                 }
                 ref[s] = qref(node, s);
-                key[s] = (cmin <= cmax + tslack && ref[s] != PG_QNODE_EMPTY) ? cmin : INFINITY;
+                key[s] = (cmin <= cmax * 1.000000477f && ref[s] != PG_QNODE_EMPTY) ? cmin : INFINITY;
             }
             for (int a = 0; a < 4; ++a)  // far to near onto the stack
                 for (int b = a + 1; b < 4; ++b)
