@@ -262,7 +262,9 @@ def main():
                        "scene": a.scene, "triangles": scene.num_triangles, "width": a.width, "height": a.height,
                        "spp": a.spp, "training_iterations": a.train, "paths_per_step": paths_per_job,
                        "integrator_props": json.loads(a.props),
-                       "parallelism": f"tile-shard x{world}, RCCL {a.exchange} per training iteration"
+                       "parallelism": f"tile-shard x{world}, "
+                                      + (f"{'RCCL' if backend == 'nccl' else backend} {a.exchange} per training iteration"
+                                         if world > 1 else "no exchange (one rank)")
                                       + (", film reduce to rank 0" if world > 1 else "")},
             "roofline": roofline,
             "pipeline": pipeline,
