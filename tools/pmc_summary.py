@@ -47,7 +47,10 @@ def load_counter(path, name):
 
 
 def revision():
-    """git HEAD of the tree that was uploaded for the profile (run this right after the profile call)."""
+    """git HEAD of the tree that was uploaded for the profile (run this right after the profile call);
+    PG_REVISION names it when the summary runs on the GPU box (no .git there)."""
+    if os.environ.get("PG_REVISION"):
+        return os.environ["PG_REVISION"]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     try:
         head = subprocess.run(["git", "-C", root, "rev-parse", "--short=12", "HEAD"], capture_output=True,
