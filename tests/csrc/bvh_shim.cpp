@@ -46,6 +46,11 @@ int shim_build(const float *P, uint32_t nv, const uint32_t *I, uint32_t nt) {
     return pgh::buildBvh(g_P.data(), g_I.data(), nt, 48, g_bvh) ? 1 : 0;
 }
 
+// BVH-order triangle -> original triangle id
+void shim_order(uint32_t *out) {
+    for (size_t i = 0; i < g_bvh.order.size(); ++i) out[i] = g_bvh.order[i];
+}
+
 // structure of the 4-wide tree: out[0] nodes, out[1] max stack need, out[2] triangles reached
 // exactly once (all: == nt), out[3] child boxes not containing their subtree's triangles, out[4] depth
 void shim_check(uint32_t nt, uint32_t *out) {

@@ -16,22 +16,55 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 QSTACK_DEPTH = 96  # pg_layout.h PG_QSTACK_DEPTH
 
 
-@pytest.fixture(scope="module")
-def shim(tmp_path_factory):
-    out = str(tmp_path_factory.mktemp("bvhshim") / "libbvhshim.so")
+SHIM_SOURCES = [os.path.join(ROOT, "tests", "csrc", "bvh_shim.cpp"),
+                os.path.join(ROOT, "mitsuba-path-guiding_amd", "csrc", "pg_bvh.cpp"),
+                os.path.join(ROOT, "mitsuba-path-guiding_amd", "csrc", "pg_layout.h")]
+PREBUILT = os.path.join(ROOT, "tests", "csrc", "_build", "libbvhshim.so")  # __graft_entry__.build()
+
+
+def compile_shim(out):
     subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-o", out,
-                           os.path.join(ROOT, "tests", "csrc", "bvh_shim.cpp"),
-                           os.path.join(ROOT, "mitsuba-path-guiding_amd", "csrc", "pg_bvh.cpp")])
+                           *SHIM_SOURCES[:2]])
+
+
+def build_shim(tmp_path_factory):
+    out = PREBUILT
+    if not os.path.exists(out) or any(os.path.getmtime(f) > os.path.getmtime(out) for f in SHIM_SOURCES):
+        out = str(tmp_path_factory.mktemp("bvhshim") / "libbvhshim.so")
+        compile_shim(out)
     L = C.CDLL(out)
     L.shim_build.restype = C.c_int
     L.shim_build.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]
     L.shim_check.argtypes = [C.c_uint32, C.c_void_p]
     L.shim_trace.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint32]
+    L.shim_order.argtypes = [C.c_void_p]
     return L
 
 
+@pytest.fixture(scope="module")
+def shim(tmp_path_factory):
+    return build_shim(tmp_path_factory)
+
+
+def brute_force_hits(shim, V, F, rays):
+    """original triangle id (or ~0) of the closest hit of every ray, by brute force over the library's
+    Woop records (the shim's loop)"""
+    V, F = np.ascontiguousarray(V, np.float32), np.ascontiguousarray(F, np.uint32)
+    assert shim.shim_build(V.ctypes.data, len(V), F.ctypes.data, len(F)) == 1
+    n = len(rays)
+    walk = np.zeros((n, 2), np.uint32)
+    brute = np.zeros((n, 2), np.uint32)
+    shim.shim_trace(np.ascontiguousarray(rays).ctypes.data, n, walk.ctypes.data, brute.ctypes.data, len(F))
+    order = np.zeros(len(F), np.uint32)
+    shim.shim_order(order.ctypes.data)
+    hit = brute[:, 1] != 0xFFFFFFFF
+    out = np.full(n, 0xFFFFFFFF, np.uint32)
+    out[hit] = order[brute[hit, 1]]
+    return out
+
+
 def geometric_strip(n=3000):
-    """triangles at x = 1.02^k: centroid bins stay lopsided, so the SAH build peels a few triangles per
+    """triangles at x = 1.004^k: centroid bins stay lopsided, so the SAH build peels a few triangles per
     level down to its depth-32 median fallback"""
     x = 1.004 ** np.arange(n, dtype=np.float64)
     V = np.zeros((3 * n, 3), np.float32)

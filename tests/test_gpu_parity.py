@@ -92,6 +92,31 @@ def test_trace_rays_ragged_bunny(pg, O, n):
     assert (occ == (gp != 0xFFFFFFFF)).mean() >= (0.999 if n > 100 else 1.0)
 
 
+@pytest.mark.parametrize("name", ["strip", "bunny"])
+def test_trace_matches_bruteforce(pg, tmp_path_factory, name):
+    """GPU closest hits (pg_trace_rays, the 4-wide walk) against brute force over the library's own Woop
+    records on the CPU (tests/csrc/bvh_shim.cpp).  The strip of triangles spanning 1 to 1.6e5 is the
+    geometry on which the unpadded slab test let 0.55 % of the rays through a box edge past their
+    triangle (pg_trace.h slabRay); device FMA contraction may still flip a near-tie."""
+    import test_bvh4_build as T
+    shim = T.build_shim(tmp_path_factory)
+    V, F = T.geometry(pg, name)
+    rays = T.rays_through(V, F, 4000, 7)
+    s = pg.scenes.Scene()
+    s.add_mesh(V, F, material=s.add_material(pg.scenes.material("diffuse")))
+    c = V.mean(0)
+    s.set_camera(tuple(c + np.array([0, 0, 1.0])), tuple(c), (0, 1, 0), 40, 8, 8)
+    s.finalize()
+    dev = make_dev(pg, s)
+    g = dev.trace_rays(rays)
+    dev.close()
+    gp = g[:, 1].view(np.uint32)
+    bf = T.brute_force_hits(shim, V, F, rays)
+    assert (bf != 0xFFFFFFFF).mean() > 0.2
+    assert (gp == bf).mean() >= 0.999
+    assert ((gp == 0xFFFFFFFF) & (bf != 0xFFFFFFFF)).mean() <= 0.0005
+
+
 def test_dgeom_kat_gpu(pg, O):
     """src/tests/test_dgeom.cpp:36-121 through the GPU traversal (t, barycentrics)."""
     import json, os
