@@ -20,18 +20,20 @@ SHIM_SOURCES = [os.path.join(ROOT, "tests", "csrc", "bvh_shim.cpp"),
                 os.path.join(ROOT, "mitsuba-path-guiding_amd", "csrc", "pg_bvh.cpp"),
                 os.path.join(ROOT, "mitsuba-path-guiding_amd", "csrc", "pg_layout.h")]
 PREBUILT = os.path.join(ROOT, "tests", "csrc", "_build", "libbvhshim.so")  # __graft_entry__.build()
+# the same shim with FMA contraction (the device compiler contracts the Woop test's products)
+PREBUILT_FMA = os.path.join(ROOT, "tests", "csrc", "_build", "libbvhshim_fma.so")
 
 
-def compile_shim(out):
-    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-o", out,
-                           *SHIM_SOURCES[:2]])
+def compile_shim(out, fma=False):
+    contract = ["-ffp-contract=fast", "-mfma"] if fma else ["-ffp-contract=off"]
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", *contract, "-o", out, *SHIM_SOURCES[:2]])
 
 
-def build_shim(tmp_path_factory):
-    out = PREBUILT
+def build_shim(tmp_path_factory, fma=False):
+    out = PREBUILT_FMA if fma else PREBUILT
     if not os.path.exists(out) or any(os.path.getmtime(f) > os.path.getmtime(out) for f in SHIM_SOURCES):
-        out = str(tmp_path_factory.mktemp("bvhshim") / "libbvhshim.so")
-        compile_shim(out)
+        out = str(tmp_path_factory.mktemp("bvhshim") / ("libbvhshim_fma.so" if fma else "libbvhshim.so"))
+        compile_shim(out, fma)
     L = C.CDLL(out)
     L.shim_build.restype = C.c_int
     L.shim_build.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]

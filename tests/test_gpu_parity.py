@@ -97,9 +97,12 @@ def test_trace_matches_bruteforce(pg, tmp_path_factory, name):
     """GPU closest hits (pg_trace_rays, the 4-wide walk) against brute force over the library's own Woop
     records on the CPU (tests/csrc/bvh_shim.cpp).  The strip of triangles spanning 1 to 1.6e5 is the
     geometry on which the unpadded slab test let 0.55 % of the rays through a box edge past their
-    triangle (pg_trace.h slabRay); device FMA contraction may still flip a near-tie."""
+    triangle (pg_trace.h slabRay).  The strip's slivers at 1e5 make the Woop test itself sensitive to
+    FMA contraction (4.4 % of its rays change hit between a contracted and an uncontracted brute
+    force), so the walk is checked on the rays where both brute forces agree."""
     import test_bvh4_build as T
     shim = T.build_shim(tmp_path_factory)
+    shim_fma = T.build_shim(tmp_path_factory, fma=True)
     V, F = T.geometry(pg, name)
     rays = T.rays_through(V, F, 4000, 7)
     s = pg.scenes.Scene()
@@ -112,9 +115,10 @@ def test_trace_matches_bruteforce(pg, tmp_path_factory, name):
     dev.close()
     gp = g[:, 1].view(np.uint32)
     bf = T.brute_force_hits(shim, V, F, rays)
-    assert (bf != 0xFFFFFFFF).mean() > 0.2
-    assert (gp == bf).mean() >= 0.999
-    assert ((gp == 0xFFFFFFFF) & (bf != 0xFFFFFFFF)).mean() <= 0.0005
+    robust = bf == T.brute_force_hits(shim_fma, V, F, rays)
+    assert (bf != 0xFFFFFFFF).mean() > 0.2 and robust.mean() > 0.9
+    assert (gp[robust] == bf[robust]).mean() >= 0.999
+    assert ((gp == 0xFFFFFFFF) & (bf != 0xFFFFFFFF))[robust].mean() <= 0.0005
 
 
 def test_dgeom_kat_gpu(pg, O):
