@@ -531,6 +531,7 @@ def cpu_baseline(pg, scene, integ, final, a):
     g = image(final).reshape(-1, 3)[pix]
     c = image(c_rgbw).reshape(-1, 3)[pix]
     rmse = {"spp": a.spp, "pixels": int(len(pix)), "same_sdtree": same_tree}
+    gt, se_g = None, None
     if not vol and os.path.exists(GT_C3) and (a.width, a.height) == (1280, 720):
         # independent guided jobs (each trained its own tree; any differing record changes the trees, so
         # the final renders decorrelate): RMSE ratio against the ground truth, with a jackknife error
@@ -570,6 +571,14 @@ def cpu_baseline(pg, scene, integ, final, a):
                          "pixels_diverged_frac": round(float((rel > 1e-3).mean()), 6),
                          "note": "GPU and CPU final renders with one tree and the same RNG streams; a path whose "
                                  "fp32 libm/FMA rounding flips one branch diverges"}
+    if gt is not None:
+        # the paired form of the RMSE ratio: both renders draw the same paths, so only the diverged
+        # pixels separate them and the jackknife error over the tiles is small
+        se_s = ((s - gt) ** 2).reshape(ntiles, -1).sum(1)
+        jk3 = np.sqrt((se_g.sum() - se_g) / (se_s.sum() - se_s))
+        rmse["same_tree"].update({
+            "rmse_ratio_gpu_over_cpu": round(float(np.sqrt(se_g.sum() / se_s.sum())), 5),
+            "rmse_ratio_jackknife_se": round(float(np.sqrt((ntiles - 1) / ntiles * ((jk3 - jk3.mean()) ** 2).sum())), 5)})
     return cpu, rmse
 
 
