@@ -1000,7 +1000,7 @@ PGD float pgLog2(float x) {
     const uint32_t b = __float_as_uint(x);
     const float e = (float)((int)((b >> 23) & 0xFFu) - 127);
     const float m = __uint_as_float((b & 0x7FFFFFu) | 0x3F800000u);
-    const float t = __fdiv_rn(m - 1.0f, m + 1.0f), t2 = t * t;  // correctly rounded in any build (oracle)
+    const float t = (m - 1.0f) / (m + 1.0f), t2 = t * t;
     const float s = t * (1.0f + t2 * (0.333333343f + t2 * (0.2f + t2 * (0.142857149f + t2 * 0.111111112f))));
     return e + s * 2.88539004f;  // 2 / ln 2
 }
@@ -1008,7 +1008,7 @@ PGD float pgLog2(float x) {
 PGD unsigned long long fracStat(float w, float pb, float pg, float q0, int k) {
     const float a = fracCandidate(k);
     const float qk = a * pb + (1.0f - a) * pg;
-    float v = w * pgLog2(__fdiv_rn(qk, q0)) * kFracFixedScale;
+    float v = w * pgLog2(qk / q0) * kFracFixedScale;
     if (v > kFracCap) v = kFracCap;
     if (v < -kFracCap) v = -kFracCap;
     return (unsigned long long)(long long)v;

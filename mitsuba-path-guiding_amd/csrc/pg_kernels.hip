@@ -879,7 +879,7 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
         float val = 0.0f;
         {
 #pragma clang fp contract(off)
-            if (woPdf > 0) val = __fdiv_rn(b.x, woPdf);  // the oracle's IEEE quotient in any build
+            if (woPdf > 0) val = b.x / woPdf;
         }
         valid = woPdf > 0 && val >= 0 && val < 1e30f;
         if (valid) {
@@ -924,7 +924,7 @@ __global__ __launch_bounds__(256) void k_splat(SDDev sd, const pg_record *__rest
 #pragma clang fp contract(off)
             const float la = __uint_as_float(sd.meta[dt].z);
             const float a0 = la > 0 ? la : sd.alpha0;
-            pb = fmaxf(__fdiv_rn(q0 - (1.0f - a0) * pg, a0), 0.0f);
+            pb = fmaxf((q0 - (1.0f - a0) * pg) / a0, 0.0f);
             stat = true;
         }
     }
@@ -990,7 +990,7 @@ __global__ __launch_bounds__(256) void k_splat_lds(SDDev sd, const pg_record *__
             float val = 0.0f;
             {
 #pragma clang fp contract(off)
-                if (woPdf > 0) val = __fdiv_rn(b.x, woPdf);  // the oracle's IEEE quotient in any build
+                if (woPdf > 0) val = b.x / woPdf;
             }
             valid = woPdf > 0 && val >= 0 && val < 1e30f;
             if (valid) {
@@ -1027,7 +1027,7 @@ __global__ __launch_bounds__(256) void k_splat_lds(SDDev sd, const pg_record *__
 #pragma clang fp contract(off)
                     const float la = __uint_as_float(sd.meta[dt].z);
                     const float a0 = la > 0 ? la : sd.alpha0;
-                    pb = fmaxf(__fdiv_rn(q0 - (1.0f - a0) * pg, a0), 0.0f);
+                    pb = fmaxf((q0 - (1.0f - a0) * pg) / a0, 0.0f);
                     stat = true;
                 }
             }

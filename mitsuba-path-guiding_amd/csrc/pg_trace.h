@@ -81,7 +81,7 @@ __device__ __forceinline__ bool woopHit(const float4 *__restrict__ woop, uint32_
     const float4 w0 = woop[3 * tr + 0];
     float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
     float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-    tt = __fdiv_rn(oz, dz);  // correctly rounded in any build: hits as the brute-force tests compute them
+    tt = oz / dz;
     if (!(tt >= tmin && tt <= tmax)) return false;
     const float4 w1 = woop[3 * tr + 1];
     float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
@@ -217,7 +217,7 @@ __device__ __forceinline__ bool leafTest(const float4 *__restrict__ woop, int le
         const float4 w0 = woop[3 * tr + 0];
         float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
         float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-        float tt = __fdiv_rn(oz, dz);
+        float tt = oz / dz;
         if (tt >= tmin && tt <= tmax) {
             const float4 w1 = woop[3 * tr + 1];
             float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
@@ -423,7 +423,7 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
                 const float4 w0 = woop[3 * tr + 0];
                 float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
                 float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-                float tt = __fdiv_rn(oz, dz);
+                float tt = oz / dz;
                 if (tt >= tmin && tt <= tmax) {
                     const float4 w1 = woop[3 * tr + 1];
                     float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
