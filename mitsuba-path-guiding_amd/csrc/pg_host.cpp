@@ -35,6 +35,13 @@ constexpr uint32_t kBounceWords = 640;
 constexpr uint32_t kShadowCounts = PG_QSHARDS, kClassCounts = 2 * PG_QSHARDS;
 static_assert(kClassCounts + (PG_NUM_CLASSES + 1) * PG_QSHARDS <= kBounceWords, "counter layout");
 constexpr uint32_t kCounterWords = kBounceWords * (kMaxBounces + 1);
+// the device's bounce cap (GParams::depth_cap): max_depth + 1 or gpu_depth_cap, at most kMaxBounces - 2,
+// so the bounce-by-bounce loop (maxBounces = depth_cap + 2 <= kMaxBounces) and k_tail, which loops until
+// shadeOne's depth_cap test ends the path, stop at the same bounce
+static uint32_t deviceDepthCap(const pg_config &cfg) {
+    const int64_t cap = cfg.max_depth > 0 ? (int64_t)cfg.max_depth + 1 : (int64_t)cfg.gpu_depth_cap;
+    return (uint32_t)std::min<int64_t>(cap, (int64_t)kMaxBounces - 2);
+}
 
 // shading-queue class of a BSDF model (one specialised k_shade per class)
 int materialClass(uint32_t model) {
@@ -687,6 +694,7 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     c->cfg = *cfg;
     if (c->cfg.tile_size == 0) c->cfg.tile_size = 32;
     if (c->cfg.gpu_depth_cap <= 0) c->cfg.gpu_depth_cap = 1024;
+    if (c->cfg.gpu_depth_cap > (int32_t)kMaxBounces - 2) c->cfg.gpu_depth_cap = (int32_t)kMaxBounces - 2;
     if (c->cfg.path_lanes < 0 || c->cfg.path_lanes > PG_MAX_LANES) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: path_lanes must be 0..4");
@@ -919,13 +927,20 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
             gmed[m].by = (pm.res[1] + 3) / 4;
             const size_t lin = (size_t)pm.res[0] * pm.res[1] * pm.res[2];
             const size_t cells = (size_t)(pm.res[0] - 1) * (pm.res[1] - 1) * (pm.res[2] - 1);
-            gmed[m].corners = PG_DENSITY_CORNERS ? 1u : 0u;
             const size_t n = PG_DENSITY_BRICKS ? (size_t)gmed[m].bx * gmed[m].by * ((pm.res[2] + 3) / 4) * 64
                              : PG_DENSITY_CORNERS ? cells * 8 : lin;
             if (PG_DENSITY_CORNERS && cells) linMax = std::max(linMax, lin);
             words += (n + 63) & ~(size_t)63;
         }
-        HIPC(c, c->density.grow(std::max<size_t>(words * 4, 256)));
+        {
+            // corner packing takes 8x the grid's memory plus a linear staging copy (pg_layout.h)
+            const hipError_t e = c->density.grow(std::max<size_t>(words * 4, 256));
+            if (e != hipSuccess)
+                return fail(c, e == hipErrorOutOfMemory ? PG_ERR_OOM : PG_ERR_HIP,
+                            "pg_upload_scene: cannot allocate " + std::to_string(words * 4) + " B of density" +
+                                (PG_DENSITY_CORNERS ? " (corner-packed: 8 floats per cell)" : "") + ": " +
+                                hipGetErrorString(e));
+        }
         DevBuf linTmp;  // the linear grid of a corner-packed medium, expanded on the device
         if (linMax) HIPC(c, linTmp.alloc(linMax * 4));
         for (uint32_t m = 0; m < d->num_media; ++m) {
@@ -1106,7 +1121,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     g.strict_normals = c->cfg.strict_normals;
     g.max_component_value = c->cfg.max_component_value;
     g.seed = c->cfg.seed;
-    g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
+    g.depth_cap = deviceDepthCap(c->cfg);
     g.guiding = c->cfg.guiding;
     g.bsdf_fraction = c->cfg.bsdf_sampling_fraction;
     g.fraction_bound = c->cfg.bsdf_fraction_bound;
@@ -1275,7 +1290,7 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     g.fraction_bound = c->cfg.bsdf_fraction_bound;
     g.glossy_prior = c->cfg.glossy_prior;
     g.seed = c->cfg.seed;
-    g.depth_cap = (uint32_t)(c->cfg.max_depth > 0 ? c->cfg.max_depth + 1 : c->cfg.gpu_depth_cap);
+    g.depth_cap = deviceDepthCap(c->cfg);
     const SceneDev sc = sceneView(c);
     const SDDev sd = sdView(c);
     const uint32_t maxBounces = std::min<uint32_t>(g.depth_cap + 2, kMaxBounces);

@@ -140,7 +140,7 @@ void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, cons
                        uint32_t sample_base);
 void pg_launch_phase_query(hipStream_t s, const GMedium *medium, const float *in, const float *wog, uint32_t n,
                            float *out);
-// corner-packed density of a linear grid (pg_layout.h GMedium.corners); out: 8 floats per cell
+// corner-packed density of a linear grid (pg_layout.h PG_DENSITY_CORNERS); out: 8 floats per cell
 void pg_launch_density_corners(hipStream_t s, const float *lin, uint32_t rx, uint32_t ry, uint32_t rz, float *out);
 void pg_launch_medium_query(hipStream_t s, const GMedium *medium, int op, const float *in, const uint32_t *keys,
                             uint32_t n, float *out);

@@ -665,9 +665,10 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_tail(GParams g, SceneDev sc, SD
     const TStack stk = threadStack(stack, p.stack_ovf);
     const WStack wstk = threadWideStack(stack, p.stack_ovf);
     const uint32_t s = blockIdx.x & (PG_QSHARDS - 1);
-    const uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x;
+    const uint32_t rows = gridDim.x / PG_QSHARDS;  // grid capped at TRACE_MAX_BLOCKS: the overflow ring's size
+    const uint32_t n = q.counts[s];
     uint32_t segs = 0, esc = 0, shadows = 0;
-    if (i < q.counts[s]) {
+    for (uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += rows * TRACE_BLOCK) {
         const uint32_t slot = q.items[(size_t)s * q.stride + i];
         uint32_t tri = __float_as_uint(ldS(&p.hit[slot]).y);
         while (tri != 0xFFFFFFFFu) {
@@ -1223,7 +1224,9 @@ void pg_launch_shadow(hipStream_t s, const SceneDev &sc, const PathDev &p, Queue
 void pg_launch_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p, Queue q,
                     uint32_t max_shard, unsigned long long *stats) {
     if (!max_shard) return;
-    const dim3 grid(PG_QSHARDS * blocks(max_shard, TRACE_BLOCK));
+    // at most TRACE_MAX_BLOCKS blocks (a grid-stride loop over each shard): the traversal stacks' overflow
+    // ring (threadStack / threadWideStack, stride gridDim.x * TRACE_BLOCK) holds that many threads
+    const dim3 grid = shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS);
     if (sc.env) hipLaunchKernelGGL(k_tail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, sd, p, q, stats);
     else hipLaunchKernelGGL(k_tail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, sd, p, q, stats);
 }

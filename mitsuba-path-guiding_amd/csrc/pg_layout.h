@@ -94,11 +94,11 @@ struct GMedium {
     float albedo[3];
     uint32_t by;  // bricks along y
     const float *maj;
-    uint32_t corners;  // 1: density holds the 8 trilinear corners of every cell (below), 0: linear voxels
-    uint32_t pad5;
+    uint32_t pad4, pad5;
 };
 static_assert(sizeof(GMedium) == 128, "GMedium layout");
-// Corner-packed density (default when it fits, see pg_host.cpp kCornerBudget): cell (x, y, z) of the
+// Corner-packed density (PG_DENSITY_CORNERS, the default build; the layout is a compile-time choice of
+// lookupDensity, there is no runtime fallback, and an upload that cannot hold it fails with PG_ERR_OOM): cell (x, y, z) of the
 // (rx-1)(ry-1)(rz-1) cells between voxel centres stores its 8 corner voxels, 32 B in lookup order
 // (z, y, x bits: d000 d001 d010 d011 | d100 d101 d110 d111), so a trilinear lookup is two aligned
 // 16-B loads instead of eight scattered 4-B loads over four cache lines.  8x the memory of the grid

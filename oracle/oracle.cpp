@@ -434,6 +434,66 @@ void oracle_trace_rays(void *sp, const float *rays, uint64_t n, int32_t any, flo
     }
 }
 
+// The same queries by brute force over every TriAccel (Scene::bruteForce: traverse()'s contract)
+void oracle_trace_rays_brute(void *sp, const float *rays, uint64_t n, float *hits) {
+    const Scene &S = *(const Scene *)sp;
+    for (uint64_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * i;
+        Ray ray{V3(r[0], r[1], r[2]), V3(r[4], r[5], r[6]), r[3], r[7]};
+        float *h = hits + 4 * i;
+        float mint, maxt, t = 0, u = 0, v = 0;
+        uint32_t prim = 0xFFFFFFFFu;
+        bool hit = false;
+        if (S.bounds.rayIntersect(ray, mint, maxt)) {
+            float rayMinT = ray.mint;
+            if (rayMinT == kEpsilon)
+                rayMinT *= std::max(std::max(std::max(std::fabs(ray.o.x), std::fabs(ray.o.y)), std::fabs(ray.o.z)), kEpsilon);
+            if (rayMinT > mint) mint = rayMinT;
+            if (ray.maxt < maxt) maxt = ray.maxt;
+            if (maxt > mint) hit = S.bruteForce(ray, mint, maxt, t, u, v, prim);
+        }
+        if (!hit) prim = 0xFFFFFFFFu;
+        h[0] = hit ? t : 0.0f;
+        std::memcpy(&h[1], &prim, 4);
+        h[2] = u;
+        h[3] = v;
+    }
+}
+
+// One path (pixel, sample) of oracle_render's loop with every ray it casts logged (Scene::logRay,
+// 11 floats each: kind 0 closest hit / 1 shadow, o.xyz, mint, d.xyz, maxt, t or occluded, prim bits).
+// Returns the number of rays (the log is truncated at `max`); L = the path's clamped radiance.
+// Debug aid for GPU/oracle divergence (tools/diverge_c3.py): re-trace the rays on both sides.
+uint64_t oracle_path_rays(void *sp, const pg_config *cfg, void *tp, uint32_t pixel, uint32_t sample, float *out,
+                          uint64_t max, float *Lout) {
+    const Scene &S = *(const Scene *)sp;
+    const SDTree *tree = (const SDTree *)tp;
+    std::vector<float> log;
+    g_rayLog = &log;
+    Rng rng{rngKey(pixel, cfg->seed), sample};
+    float jx, jy;
+    rng.next2(0, jx, jy);
+    Ray ray = S.cameraRay((float)(pixel % S.cam.W) + jx, (float)(pixel / S.cam.W) + jy);
+    Counters cnt;
+    V3 L;
+    if (cfg->integrator == PG_INTEGRATOR_VOLPATH) {
+        SeqRng srng{rng};
+        VolCounters vc;
+        L = VolLi(S, *cfg, srng, ray, vc, !g_volpathEager, tree, nullptr);
+    } else {
+        L = Li(S, *cfg, tree, rng, ray, nullptr, cnt);
+    }
+    g_rayLog = nullptr;
+    float m = maxc(L);
+    if (m > cfg->max_component_value) L = L * (cfg->max_component_value / m);
+    Lout[0] = L.x;
+    Lout[1] = L.y;
+    Lout[2] = L.z;
+    const uint64_t nr = log.size() / 11;
+    std::memcpy(out, log.data(), sizeof(float) * 11 * std::min(nr, max));
+    return nr;
+}
+
 // Full hit record (fillIntersectionRecord): out[16] = p.xyz, t, geoN.xyz, shN.xyz, dpdu.xyz, u, v, prim
 void oracle_intersect(void *sp, const float *rays, uint64_t n, float *out) {
     const Scene &S = *(const Scene *)sp;

@@ -46,6 +46,9 @@ def lib(capi):
             "oracle_sdtree_pdf": (None, [VP, VP, VP, C.c_uint64, VP]),
             "oracle_sdtree_sample": (None, [VP, VP, VP, C.c_uint64, VP, VP]),
             "oracle_trace_rays": (None, [VP, VP, C.c_uint64, C.c_int32, VP]),
+            "oracle_trace_rays_brute": (None, [VP, VP, C.c_uint64, VP]),
+            "oracle_path_rays": (C.c_uint64, [VP, C.POINTER(capi.pg_config), VP, C.c_uint32, C.c_uint32, VP,
+                                              C.c_uint64, VP]),
             "oracle_bsdf_query": (None, [C.POINTER(capi.pg_material), VP, VP, VP, C.c_uint64, VP]),
             "oracle_material_type": (C.c_uint32, [C.POINTER(capi.pg_material)]),
             "oracle_rough_transmittance": (None, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
@@ -130,6 +133,23 @@ class OracleScene:
         hits = np.zeros((len(rays), 4), np.float32)
         self.L.oracle_trace_rays(self.h, _p(rays), len(rays), int(any_hit), _p(hits))
         return hits
+
+    def trace_brute(self, rays):
+        """trace() by brute force over every triangle (the walk's contract: smallest t, ties to the lower
+        triangle index)"""
+        rays = np.ascontiguousarray(rays, np.float32)
+        hits = np.zeros((len(rays), 4), np.float32)
+        self.L.oracle_trace_rays_brute(self.h, _p(rays), len(rays), _p(hits))
+        return hits
+
+    def path_rays(self, cfg, sdtree, pixel, sample, max_rays=4096):
+        """The rays one path casts: (n x 11: kind 0 closest / 1 shadow, o, mint, d, maxt, t or occluded,
+        prim bits), and its clamped radiance"""
+        out = np.zeros((max_rays, 11), np.float32)
+        L = np.zeros(3, np.float32)
+        n = self.L.oracle_path_rays(self.h, C.byref(cfg), sdtree.h if sdtree else None, pixel, sample, _p(out),
+                                    max_rays, _p(L))
+        return out[:min(n, max_rays)], L
 
 
 class OracleSDTree:

@@ -303,6 +303,10 @@ struct Env {
     }
 };
 
+// Debug log of the rays one path casts (oracle_path_rays, tools/diverge_c3.py): when set, every
+// closest-hit and shadow query appends (kind 0 / 1, o.xyz, mint, d.xyz, maxt, t or occluded, prim).
+inline thread_local std::vector<float> *g_rayLog = nullptr;
+
 struct Scene {
     std::vector<V3> pos, nrm;
     std::vector<uint32_t> idx;
@@ -322,10 +326,27 @@ struct Scene {
     int camMedium = -1;
 
     void build(const pg_scene_desc &d);
-    bool intersect(const Ray &ray, Its &its) const;
-    bool occluded(const Ray &ray) const;
+    bool intersect(const Ray &ray, Its &its) const {
+        const bool h = intersectImpl(ray, its);
+        logRay(0, ray, h ? its.t : 0.0f, h ? its.prim : 0xFFFFFFFFu);
+        return h;
+    }
+    bool occluded(const Ray &ray) const {
+        const bool o = occludedImpl(ray);
+        logRay(1, ray, o ? 1.0f : 0.0f, 0u);
+        return o;
+    }
+    bool intersectImpl(const Ray &ray, Its &its) const;
+    bool occludedImpl(const Ray &ray) const;
     bool intersectRaw(const Ray &ray, float &t, uint32_t &prim) const;
     bool traverse(const Ray &r, float mint, float maxt, bool any, float &t, float &u, float &v, uint32_t &prim) const;
+    bool bruteForce(const Ray &r, float mint, float maxt, float &t, float &u, float &v, uint32_t &prim) const;
+    static void logRay(int kind, const Ray &r, float res, uint32_t prim) {
+        if (!g_rayLog) return;
+        float pb;
+        std::memcpy(&pb, &prim, 4);
+        g_rayLog->insert(g_rayLog->end(), {(float)kind, r.o.x, r.o.y, r.o.z, r.mint, r.d.x, r.d.y, r.d.z, r.maxt, res, pb});
+    }
     void fill(const Ray &r, float t, float u, float v, uint32_t prim, Its &its) const;
     Ray cameraRay(float sx, float sy) const;
 };
@@ -507,38 +528,59 @@ inline void Scene::build(const pg_scene_desc &d) {
     }
 }
 
+// Closest hit over the BVH with the same contract as a brute-force loop over every TriAccel: the
+// smallest t in [mint, maxt], equal distances (shared edges, coplanar triangles) to the lower
+// original triangle index, so the hit depends on neither the tree nor the visiting order (the
+// kd-tree of skdtree.cpp:112-142 finds every triangle its TriAccel test accepts).  Box tests are made
+// robust to rounding as the kernels' walk is (pg_trace.h slabRay): each axis's slab is padded by
+// 2^-21 |o_a / d_a| (the rounding of (plane - o) / d far from the origin), intervals are compared as
+// t0 <= t1 (1 + 2^-21), and boxes are culled against the current hit distance widened by its own
+// rounding, so a box holding a tie is still visited.  Without this a ray grazing a box edge far from
+// the origin could miss a hit inside it (tests/test_oracle_kat.py: strip geometry).
 inline bool Scene::traverse(const Ray &r, float mint, float maxt, bool any, float &tBest, float &uBest, float &vBest,
                             uint32_t &prim) const {
     if (nodes.empty()) return false;
-    V3 inv(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    const float eps = 1e-30f;  // as the kernels: no infinite reciprocals, so no inf - inf below
+    const V3 inv(1.0f / (std::fabs(r.d.x) > eps ? r.d.x : std::copysign(eps, r.d.x)),
+                 1.0f / (std::fabs(r.d.y) > eps ? r.d.y : std::copysign(eps, r.d.y)),
+                 1.0f / (std::fabs(r.d.z) > eps ? r.d.z : std::copysign(eps, r.d.z)));
+    const float kPad = 4.76837158e-7f, kRel = 1.000000477f;  // 2^-21, 1 + 2^-21
+    V3 pad;
+    float oidMax = 0.0f;
+    for (int a = 0; a < 3; ++a) {
+        const float oid = std::fabs(r.o[a] * inv[a]);
+        pad[a] = kPad * oid;
+        oidMax = std::max(oidMax, oid);
+    }
+    const float tslack = 1e-6f * oidMax;
     bool hit = false;
     float far = maxt;
-    // slab test of node n against [mint, far]; returns the entry distance or +inf on a miss
+    auto cull = [&]() { return hit ? far * 1.000001f + tslack : far; };
+    // slab test of node n against [mint, cull()]; returns the entry distance or +inf on a miss
     auto enter = [&](const BvhNode &n) {
-        float t0 = mint, t1 = far;
+        float t0 = mint, t1 = cull();
         for (int a = 0; a < 3; ++a) {
             float ta = (n.box.lo[a] - r.o[a]) * inv[a], tb = (n.box.hi[a] - r.o[a]) * inv[a];
             if (ta > tb) std::swap(ta, tb);
-            if (std::isnan(ta) || std::isnan(tb)) continue;  // degenerate slab with d == 0 and o on the plane
-            t0 = std::max(t0, ta);
-            t1 = std::min(t1, tb);
-            if (t0 > t1) return kInf;
+            if (std::isnan(ta) || std::isnan(tb)) continue;  // degenerate slab with o on the plane
+            t0 = std::max(t0, ta - pad[a]);
+            t1 = std::min(t1, tb + pad[a]);
         }
-        return t0;
+        return t0 <= t1 * kRel ? t0 : kInf;
     };
-    // near-first traversal: stack entries carry their entry distance, culled against `far`
+    // near-first traversal: stack entries carry their entry distance, culled against the widened far
     std::vector<std::pair<uint32_t, float>> stack;
     stack.reserve(64);
     if (enter(nodes[0]) < kInf) stack.push_back({0u, 0.0f});
     while (!stack.empty()) {
         auto [ni, tin] = stack.back();
         stack.pop_back();
-        if (tin > far) continue;
+        if (tin > cull()) continue;
         const BvhNode &n = nodes[ni];
         if (n.count > 0) {
             for (uint32_t i = n.left_or_first; i < n.left_or_first + n.count; ++i) {
                 float u, v, t;
-                if (accel[i].intersect(r, mint, far, u, v, t)) {
+                if (accel[i].intersect(r, mint, far, u, v, t) && (!hit || t < far || accel[i].prim < prim)) {
                     if (any) return true;
                     far = t;
                     tBest = t;
@@ -558,6 +600,25 @@ inline bool Scene::traverse(const Ray &r, float mint, float maxt, bool any, floa
                 if (t0 < kInf) stack.push_back({c0, t0});
                 if (t1 < kInf) stack.push_back({c1, t1});
             }
+        }
+    }
+    return hit;
+}
+
+// every TriAccel with traverse()'s accept rule (smallest t, ties to the lower original index): the
+// walk's contract, checked in tests/test_oracle_kat.py
+inline bool Scene::bruteForce(const Ray &r, float mint, float maxt, float &tBest, float &uBest, float &vBest,
+                              uint32_t &prim) const {
+    bool hit = false;
+    float far = maxt;
+    for (const TriAccel &a : accel) {
+        float u, v, t;
+        if (a.intersect(r, mint, far, u, v, t) && (!hit || t < far || a.prim < prim)) {
+            far = tBest = t;
+            uBest = u;
+            vBest = v;
+            prim = a.prim;
+            hit = true;
         }
     }
     return hit;
@@ -589,7 +650,7 @@ inline void Scene::fill(const Ray &r, float t, float u, float v, uint32_t prim, 
 }
 
 // ShapeKDTree::rayIntersect(ray, its): AABB clip + adaptive epsilon (skdtree.cpp:112-142)
-inline bool Scene::intersect(const Ray &ray, Its &its) const {
+inline bool Scene::intersectImpl(const Ray &ray, Its &its) const {
     its.valid = false;
     float mint, maxt;
     if (!bounds.rayIntersect(ray, mint, maxt)) return false;
@@ -607,7 +668,7 @@ inline bool Scene::intersect(const Ray &ray, Its &its) const {
 }
 
 // ShapeKDTree::rayIntersect(ray) shadow variant (skdtree.cpp:207-227)
-inline bool Scene::occluded(const Ray &ray) const {
+inline bool Scene::occludedImpl(const Ray &ray) const {
     float mint, maxt;
     if (!bounds.rayIntersect(ray, mint, maxt)) return false;
     float rayMinT = ray.mint;
