@@ -300,15 +300,54 @@ __device__ __forceinline__ void stPinfoZW(uint4 *p, uint32_t z, uint32_t w) {
     reinterpret_cast<uint2 *>(p)[1] = make_uint2(z, w);
 }
 
+// Debug build only (PG_WATCH=1, make watch -> build/libpgamd_watch.so; tools/diverge_c3.py): shadeOne
+// logs every vertex of one (pixel, sample) path, the same record the oracle's Li writes (oracle.cpp
+// g_vtxLog): depth, original triangle, p, T, alpha, guided, mode, woPdf, weight, wo, L, NEE
+// contribution and pdfs, RR q / outcome, alive, shadow, b0, b1.  The product build has none of it.
+#ifndef PG_WATCH
+#define PG_WATCH 0
+#endif
+#if PG_WATCH
+#define PG_WATCH_F 32
+#define PG_WATCH_MAX 256
+__device__ uint32_t pgWatch[3];  // pixel, sample, records written
+__device__ float pgWatchLog[PG_WATCH_MAX * PG_WATCH_F];
+extern "C" int pg_debug_watch(uint32_t pixel, uint32_t sample) {
+    const uint32_t w[3] = {pixel, sample, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(pgWatch), w, sizeof(w)) == hipSuccess ? 0 : -1;
+}
+extern "C" int pg_debug_watch_read(float *out, uint32_t max, uint32_t *n) {
+    uint32_t w[3];
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(w, HIP_SYMBOL(pgWatch), sizeof(w)) != hipSuccess) return -1;
+    *n = w[2] < PG_WATCH_MAX ? w[2] : PG_WATCH_MAX;
+    const uint32_t k = *n < max ? *n : max;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pgWatchLog), (size_t)k * PG_WATCH_F * 4) == hipSuccess ? 0 : -1;
+}
+#define WSET(i, v) (wr[i] = (float)(v))
+#define WSET3(i, v) (wr[i] = (v).x, wr[(i) + 1] = (v).y, wr[(i) + 2] = (v).z)
+#else
+#define WSET(i, v) ((void)0)
+#define WSET3(i, v) ((void)0)
+#endif
+
 template <int MODEL, bool CAN_GUIDE, bool ENV>
 __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, const SDDev &sd, const PathDev &p,
                                          uint32_t slot, const GMat *mats, bool wantKey, bool &alive, bool &shadow,
                                          uint32_t &rkey) {
     bool dirtyL = false;
     f3 L = mk1(0.f);
+#if PG_WATCH
+    float wr[PG_WATCH_F];
+    for (int i = 0; i < PG_WATCH_F; ++i) wr[i] = -1.0f;
+    bool watched = false;
+#endif
     do {
         uint4 pi = ldS(&p.pinfo[slot]);
         const uint32_t pix = pi.x, sample = pi.y;
+#if PG_WATCH
+        watched = pix == pgWatch[0] && sample == pgWatch[1];
+#endif
         uint32_t depth = pi.z & 0xFFFFu, flags = pi.z >> 16, nv = pi.w;
         float4 hv = ldS(&p.hit[slot]);
         // a camera ray's state is implied (k_camera stores neither throughput nor prev)
@@ -323,6 +362,9 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         f3 rd = xyz(ldS(&p.ray_d[slot]));
         Hit h;
         fetchHit(sc, tri, hv.z, hv.w, rd, h);
+        WSET(0, depth);
+        WSET(1, __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w));
+        WSET3(2, h.p);
         f3 Le = mk1(0.f);
         if (h.emitter >= 0 && dot(h.shN, -rd) > 0) {  // AreaLight::eval (area.cpp)
             const GEmitter &em = sc.ems[h.emitter];
@@ -346,10 +388,16 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
             }
             if (depth - 1 >= (uint32_t)g.rr_depth) {
                 float q = fminf(maxc(T) * eta * eta, 0.95f);
+                WSET(26, q);
+                WSET3(18, L);
+                WSET3(5, T);
+                WSET(27, 0);
                 if (rng1(key, sample, dimOf(depth - 1, SLOT_RR)) >= q) break;
+                WSET(27, 1);
                 T = T / q;
             }
         }
+        WSET3(5, T);
         if (depth > g.depth_cap) break;
         const GMat M = mats[h.mat];
         if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
@@ -359,6 +407,7 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         if ((g.max_depth > 0 && (int)depth >= g.max_depth) ||
             (g.strict_normals && dot(rd, h.geoN) * h.wi.z >= 0))
             break;
+        WSET3(18, L);
         const f3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? h.shN : mk1(0.f);
         // glossy prior (pg_config.glossy_prior): r = BSDF::getGlossySamplingRate; r = 1 is not guided
         const float gRate = (CAN_GUIDE && g.glossy_prior) ? glossyRate<MODEL>(M, h.wi.z) : 0.0f;
@@ -412,6 +461,8 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
             float b0, b1;
             rng2(key, sample, dimOf(depth, SLOT_BSDF), b0, b1);
             float b2 = rng1(key, sample, dimOf(depth, SLOT_COMP));
+            WSET(30, b0);
+            WSET(31, b1);
             int mode = 0;  // D-tree walk of the sampled direction: 0 none, 1 pdf (BSDF sample), 2 sample
             float bu = 0, bw = 0;
             if (!guide) {
@@ -457,8 +508,17 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
                     }
                 }
             }
+            WSET(10, mode + (ok ? 0 : 10));
         }
         uint32_t vtxIndex = 0xFFFFFFFFu;
+        WSET(8, alpha);
+        WSET(9, guide ? 1 : 0);
+        WSET(11, woPdf);
+        WSET3(12, weight);
+        WSET3(15, h.sh.toWorld(bs.wo));
+        WSET3(21, neeC);
+        WSET(24, neeEmPdf);
+        WSET(25, neeBp);
         if (ok && !isZero(weight)) {
             if (bs.type != ENull) flags |= PF_SCATTERED;
             f3 wo = h.sh.toWorld(bs.wo);
@@ -496,6 +556,15 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         if (!alive && nv != pi.w) stPinfoZW(&p.pinfo[slot], pi.z, nv);
     } while (false);
     if (dirtyL) stS(&p.rad[slot], f4(L, 0.0f));
+#if PG_WATCH
+    if (watched) {
+        wr[28] = alive ? 1.0f : 0.0f;
+        wr[29] = shadow ? 1.0f : 0.0f;
+        const uint32_t k = atomicAdd(&pgWatch[2], 1u);
+        if (k < PG_WATCH_MAX)
+            for (int i = 0; i < PG_WATCH_F; ++i) pgWatchLog[k * PG_WATCH_F + i] = wr[i];
+    }
+#endif
 }
 
 template <int MODEL, bool CAN_GUIDE, bool ENV>

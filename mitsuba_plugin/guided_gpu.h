@@ -26,6 +26,7 @@
 #include <mitsuba/core/fresolver.h>
 #include <mitsuba/core/fstream.h>
 #include <mitsuba/core/timer.h>
+#include <mitsuba/render/denoiser.h>
 #include <boost/algorithm/string.hpp>
 #include <map>
 #include <thread>
@@ -49,7 +50,20 @@ public:
         m_cfg.s_tree_threshold = props.getFloat("sTreeThreshold", 12000.f);
         m_cfg.d_tree_threshold = props.getFloat("dTreeThreshold", 0.01f);
         m_cfg.distance_guiding = props.getFloat("distanceGuiding", m_cfg.distance_guiding);  // volpath only
+        // denoiser feature buffers (the fork's OIDN wrapper, denoiser.h): the first hit's BSDF::getAlbedo
+        // and shading normal per camera sample, averaged per pixel on the device; after the render the
+        // adapter feeds the means to Denoiser and stores its buffers ("denoiserFile"); with
+        // denoise = true the film receives the denoised image
         m_cfg.aovs = props.getBoolean("aovs", false);
+        m_denoise = props.getBoolean("denoise", false);
+        if (m_denoise) m_cfg.aovs = 1;
+        m_denoiserFile = props.getString("denoiserFile", "");
+        // combination of the training iterations' images with the final render: "discard" (Mueller et al.
+        // 2017's default: the final render only) or "inversevar" (each image weighted by the inverse of
+        // its mean per-pixel variance; integrator.py combine_inverse_variance is the same arithmetic)
+        m_sampleCombination = boost::to_lower_copy(props.getString("sampleCombination", "discard"));
+        if (m_sampleCombination != "discard" && m_sampleCombination != "inversevar")
+            Log(EError, "guided_gpu: sampleCombination must be \"discard\" or \"inversevar\"");
         // volpath: MIS of emitters behind index-matched surfaces with the whole ray length (unbiased)
         // instead of the reference's last segment
         m_cfg.volpath_exact_mis = props.getBoolean("exactMis", false);
@@ -82,6 +96,9 @@ public:
         m_commIdFile = s->readString();
         m_exchange = s->readString();
         m_mediumResolution = s->readInt();
+        m_sampleCombination = s->readString();
+        m_denoiserFile = s->readString();
+        m_denoise = s->readBool();
     }
     void serialize(Stream *s, InstanceManager *m) const {
         ProgressiveMonteCarloIntegrator::serialize(s, m);
@@ -91,6 +108,9 @@ public:
         s->writeString(m_commIdFile);
         s->writeString(m_exchange);
         s->writeInt(m_mediumResolution);
+        s->writeString(m_sampleCombination);
+        s->writeString(m_denoiserFile);
+        s->writeBool(m_denoise);
     }
 
     bool preprocess(const Scene *scene, RenderQueue *queue, const RenderJob *job,
@@ -117,10 +137,20 @@ public:
                 int sceneResID, int sensorResID, int samplerResID) {
         ref<Timer> timer = new Timer();
         uint32_t offset = 0;
+        const size_t npix = (size_t) m_flat.desc.camera.width * m_flat.desc.camera.height;
+        m_iterationFilms.clear();
         for (int it = 0; it < m_trainingIterations && m_cfg.guiding; ++it) {   // training progressions
             preprogression(queue, job, sceneResID, sensorResID, samplerResID);
             if (!pass(1u << it, offset, 1)) return false;
             offset += 1u << it;
+            if (m_sampleCombination == "inversevar") {           // keep this iteration's image (this rank's tiles)
+                FilmSums f;
+                f.rgbw.resize(4 * npix);
+                f.sumsq.resize(4 * npix);
+                check(pg_read_film(m_ctx, f.rgbw.data(), f.sumsq.data()));
+                check(pg_reset_film(m_ctx));
+                m_iterationFilms.push_back(std::move(f));
+            }
             if (m_cfg.world_size > 1 && m_exchange == "allgather") {
                 check(pg_comm_allgather_records(m_ctx, NULL));  // RCCL: every rank splats every rank's records
             } else {
@@ -172,21 +202,62 @@ public:
                 postprogression(queue, job, sceneResID, sensorResID, samplerResID);
             }
         }
+        // the image: per pixel (sum rgb, count); the film sums of this rank's tiles
+        std::vector<float> rgbw(4 * npix);
+        if (m_sampleCombination == "inversevar" && !m_iterationFilms.empty()) {
+            FilmSums last;
+            last.rgbw.resize(4 * npix);
+            last.sumsq.resize(4 * npix);
+            check(pg_read_film(m_ctx, last.rgbw.data(), last.sumsq.data()));
+            m_iterationFilms.push_back(std::move(last));
+            combineInverseVariance(rgbw);                        // weights agree over ranks (all-reduced)
+            if (m_cfg.world_size > 1) {                          // disjoint tiles: the sum over ranks is the image
+                std::vector<double> img(rgbw.begin(), rgbw.end());
+                check(pg_comm_allreduce_f64(m_ctx, img.data(), img.size()));
+                for (size_t i = 0; i < img.size(); ++i) rgbw[i] = (float) img[i];
+            }
+        }
         if (m_cfg.world_size > 1) {
-            check(pg_comm_reduce_film(m_ctx, 0));                // RCCL: disjoint tiles summed on rank 0
+            check(pg_comm_reduce_film(m_ctx, 0));                // RCCL: disjoint tiles (and features) on rank 0
             if (m_cfg.rank != 0) return true;                    // only rank 0 develops the film
         }
+        if (m_sampleCombination != "inversevar" || m_iterationFilms.empty())
+            check(pg_read_film(m_ctx, rgbw.data(), NULL));
         Film *film = scene->getSensor()->getFilm();
         Vector2i size = film->getSize();
-        std::vector<float> rgbw(size.x * size.y * 4);
-        check(pg_read_film(m_ctx, rgbw.data(), NULL));
+        // the film read-out index of output pixel (x, y): a mirrored toWorld flips x
+        auto src = [&](int x, int y) { return (size_t) y * size.x + (m_flat.mirrorX ? size.x - 1 - x : x); };
+        std::unique_ptr<Denoiser> denoiser;
+        if (m_cfg.aovs) {                                         // Denoiser::add's inputs (denoiser.cpp:138-144)
+            std::vector<float> alb(4 * npix), nrm(4 * npix);
+            check(pg_read_aovs(m_ctx, alb.data(), nrm.data()));
+            denoiser.reset(new Denoiser());
+            denoiser->init(size, true);
+            for (int y = 0; y < size.y; ++y)
+                for (int x = 0; x < size.x; ++x) {
+                    const size_t i = src(x, y);
+                    const float w = std::max(rgbw[4 * i + 3], 1.0f), n = std::max(alb[4 * i + 3], 1.0f);
+                    Denoiser::Sample smp;                         // one add of the pixel means = their average
+                    smp.color.fromLinearRGB(rgbw[4 * i] / w, rgbw[4 * i + 1] / w, rgbw[4 * i + 2] / w);
+                    smp.albedo.fromLinearRGB(alb[4 * i] / n, alb[4 * i + 1] / n, alb[4 * i + 2] / n);
+                    smp.normal = Vector3(nrm[4 * i] / n, nrm[4 * i + 1] / n, nrm[4 * i + 2] / n);
+                    if (m_flat.mirrorX) smp.normal.x = -smp.normal.x;  // the image's x axis is flipped
+                    denoiser->add(y * size.x + x, smp);
+                }
+            denoiser->denoise();
+            if (!m_denoiserFile.empty()) denoiser->storeBuffers(m_denoiserFile);
+        }
         ref<ImageBlock> block = new ImageBlock(Bitmap::ESpectrumAlphaWeight, size, NULL);
         for (int y = 0; y < size.y; ++y)
             for (int x = 0; x < size.x; ++x) {
-                const float *p = &rgbw[4 * (y * size.x + (m_flat.mirrorX ? size.x - 1 - x : x))];
-                Float w = std::max(p[3], 1.0f);
                 Spectrum s;
-                s.fromLinearRGB(p[0] / w, p[1] / w, p[2] / w);
+                if (m_denoise) {
+                    s = denoiser->get(y * size.x + x);
+                } else {
+                    const float *p = &rgbw[4 * src(x, y)];
+                    Float w = std::max(p[3], 1.0f);
+                    s.fromLinearRGB(p[0] / w, p[1] / w, p[2] / w);
+                }
                 block->getBitmap()->setPixel(Point2i(x, y), s);  // box filter: one value per pixel
             }
         film->setBitmap(block->getBitmap());
@@ -216,6 +287,51 @@ protected:
         check(st);
         return true;
     }
+    // Inverse-variance combination of m_iterationFilms (training iterations + the final render): image
+    // i has per-pixel means m_i and the variance estimate v_i = the mean over rendered pixels and
+    // channels of (E[x^2] - m_i^2) / n; weights 1 / v_i (normalised; the sums are all-reduced over
+    // ranks so every tile shard uses the same weights).  out: per pixel (combined mean x total count,
+    // total count), i.e. film sums.  integrator.py combine_inverse_variance is the same arithmetic.
+    void combineInverseVariance(std::vector<float> &out) const {
+        const size_t K = m_iterationFilms.size(), npix = out.size() / 4;
+        std::vector<double> st(2 * K, 0.0);
+        for (size_t k = 0; k < K; ++k) {
+            const FilmSums &f = m_iterationFilms[k];
+            for (size_t i = 0; i < npix; ++i) {
+                const float cnt = f.rgbw[4 * i + 3];
+                if (!(cnt > 0)) continue;
+                for (int c = 0; c < 3; ++c) {
+                    const float m = f.rgbw[4 * i + c] / cnt, m2 = f.sumsq[4 * i + c] / cnt;
+                    st[2 * k] += (double) (std::max(m2 - m * m, 0.0f) / cnt);
+                    st[2 * k + 1] += 1.0;
+                }
+            }
+        }
+        if (m_cfg.world_size > 1) check(pg_comm_allreduce_f64(m_ctx, st.data(), st.size()));
+        std::vector<double> w(K, 0.0);
+        double wsum = 0;
+        for (size_t k = 0; k < K; ++k) {
+            const double v = st[2 * k + 1] > 0 ? st[2 * k] / st[2 * k + 1] : 0.0;
+            w[k] = v > 0 && std::isfinite(v) ? 1.0 / v : 0.0;
+            wsum += w[k];
+        }
+        if (!(wsum > 0)) {                                       // no variance estimate: the final render
+            std::fill(w.begin(), w.end(), 0.0);
+            w[K - 1] = wsum = 1.0;
+        }
+        for (size_t i = 0; i < npix; ++i) {
+            double total = 0, mean[3] = {0, 0, 0};
+            for (size_t k = 0; k < K; ++k) {
+                const FilmSums &f = m_iterationFilms[k];
+                const float cnt = f.rgbw[4 * i + 3], n = std::max(cnt, 1.0f);
+                total += cnt;
+                for (int c = 0; c < 3; ++c) mean[c] += w[k] / wsum * (f.rgbw[4 * i + c] / n);
+            }
+            for (int c = 0; c < 3; ++c) out[4 * i + c] = (float) (mean[c] * total);
+            out[4 * i + 3] = (float) total;
+        }
+    }
+
     // the communicator's id travels through a file next to the scene (any out-of-band channel works:
     // MPI_Bcast, a socket); rank 0 writes it, the other ranks wait for it
     void initComm() {
@@ -280,6 +396,10 @@ protected:
     Float m_maxRenderTime;
     std::string m_commIdFile, m_exchange;
     int m_mediumResolution;
+    std::string m_sampleCombination, m_denoiserFile;
+    bool m_denoise = false;
+    struct FilmSums { std::vector<float> rgbw, sumsq; };
+    std::vector<FilmSums> m_iterationFilms;                     // sampleCombination = "inversevar"
 };
 
 static inline void pgRGB(const Spectrum &s, float *out) {

@@ -25,6 +25,16 @@ using namespace orc;
 namespace {
 
 bool g_volpathEager = false;  // oracle_set_volpath_eager: the reference's eager transmittance walk
+// oracle_path_rays: Li's per-vertex log, the record of the kernels' PG_WATCH build (pg_kernels.hip)
+thread_local std::vector<float> *g_vtxLog = nullptr;
+struct VtxRec {
+    float f[32];
+    VtxRec() { std::fill(f, f + 32, -1.0f); }
+    void set3(int i, V3 v) { f[i] = v.x, f[i + 1] = v.y, f[i + 2] = v.z; }
+    void flush() {
+        if (g_vtxLog) g_vtxLog->insert(g_vtxLog->end(), f, f + 32);
+    }
+};
 
 inline float miWeight(float a, float b) {
     a *= a;
@@ -69,6 +79,7 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
     bool emittedQuery = true;  // RadianceQueryRecord::ERadiance, then ERadianceNoEmission
     int depth = 1;
 
+    VtxRec wr;  // g_vtxLog: this vertex's record (RR fields filled by the previous iteration)
     while (depth <= maxDepth || maxDepth < 0) {
         if (!its.valid) {  // only the camera ray gets here (EEmittedRadiance, progressive_path.cpp:150-158)
             if (S.env.valid && emittedQuery && (!cfg.hide_emitters || scattered)) L += T * S.env.eval(ray.d);
@@ -77,9 +88,16 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
         const pg_shape &shp = S.shapes[its.shape];
         const Material &M = S.mats[shp.material];
         if (shp.emitter >= 0 && emittedQuery && (!cfg.hide_emitters || scattered)) L += T * emitterLe(S, its, -ray.d);
+        wr.f[0] = (float)depth;
+        wr.f[1] = (float)its.prim;
+        wr.set3(2, its.p);
+        wr.set3(5, T);
+        wr.set3(18, L);
         if ((depth >= maxDepth && maxDepth > 0) ||
-            (cfg.strict_normals && dot(ray.d, its.geoN) * its.wi.z >= 0))
+            (cfg.strict_normals && dot(ray.d, its.geoN) * its.wi.z >= 0)) {
+            wr.flush();
             break;
+        }
 
         V3 refN = (M.type & (ETransmission | EBackSide)) == 0 ? its.sh.n : V3(0.f);
         // glossy prior (pg_config.glossy_prior): vertices with glossy rate r = 1 are not guided, the rest
@@ -107,8 +125,12 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                 V3 bsdfVal = bsdfEval(M, its.wi, woL);
                 if (!isZero(bsdfVal) && (!cfg.strict_normals || dot(its.geoN, dr.d) * woL.z > 0)) {
                     float bsdfPdfV = bsdfPdf(M, its.wi, woL);
+                    wr.f[25] = bsdfPdfV;
+                    wr.f[24] = dr.pdf;
                     if (dt) bsdfPdfV = alpha * bsdfPdfV + (1 - alpha) * SDTree::pdfDir(*dt, dr.d);
                     float w = miWeight(dr.pdf, bsdfPdfV);
+                    if (g_vtxLog) wr.set3(21, T * value * bsdfVal * w);
+                    wr.f[29] = 1.0f;  // visible light sample (the kernels log 1 for any queued shadow ray)
                     L += T * value * bsdfVal * w;
                 }
             }
@@ -122,6 +144,11 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
             float b0, b1;
             rng.next2(dimOf(depth, SLOT_BSDF), b0, b1);
             float b2 = rng.next1(dimOf(depth, SLOT_COMP));
+            wr.f[30] = b0;
+            wr.f[31] = b1;
+            wr.f[8] = alpha;
+            wr.f[9] = dt ? 1.0f : 0.0f;
+            wr.f[10] = !dt ? 0.0f : rng.next1(dimOf(depth, SLOT_GUIDE_CHOICE)) < alpha ? 1.0f : 2.0f;
             if (!dt) {
                 weight = bsdfSample(M, its.wi, b0, b1, b2, bs);
                 woPdf = bs.pdf;
@@ -129,7 +156,12 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                 float choice = rng.next1(dimOf(depth, SLOT_GUIDE_CHOICE));
                 if (choice < alpha) {
                     weight = bsdfSample(M, its.wi, b0, b1, b2, bs);
-                    if (isZero(weight)) break;
+                    if (isZero(weight)) {
+                        wr.f[10] = 11;
+                        wr.f[28] = 0;
+                        wr.flush();
+                        break;
+                    }
                     float dPdf = SDTree::pdfDir(*dt, its.toWorld(bs.wo));
                     woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
                     weight = weight * (bs.pdf / woPdf);
@@ -142,7 +174,12 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                     V3 f = bsdfEval(M, its.wi, woL);
                     float bp = bsdfPdf(M, its.wi, woL);
                     woPdf = alpha * bp + (1 - alpha) * dPdf;
-                    if (!(woPdf > 0) || isZero(f)) break;
+                    if (!(woPdf > 0) || isZero(f)) {
+                        wr.f[10] = 12;
+                        wr.f[28] = 0;
+                        wr.flush();
+                        break;
+                    }
                     weight = f / woPdf;
                     pgWo = dPdf;
                     bs.wo = woL;
@@ -154,11 +191,24 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
                 }
             }
         }
-        if (isZero(weight)) break;
+        wr.f[11] = woPdf;
+        wr.set3(12, weight);
+        wr.set3(15, its.toWorld(bs.wo));
+        wr.f[28] = 0;
+        if (isZero(weight)) {
+            wr.flush();
+            break;
+        }
         scattered |= bs.sampledType != ENull;
         V3 wo = its.toWorld(bs.wo);
         float woDotGeoN = dot(its.geoN, wo);
-        if (cfg.strict_normals && woDotGeoN * bs.wo.z <= 0) break;
+        if (cfg.strict_normals && woDotGeoN * bs.wo.z <= 0) {
+            wr.flush();
+            break;
+        }
+        wr.f[28] = 1;
+        wr.flush();
+        wr = VtxRec();
 
         // ---- training-record vertex (before tracing: escaped directions record zero radiance)
         if (recs && !(bs.sampledType & EDelta) && nv < maxV) {
@@ -205,7 +255,18 @@ V3 Li(const Scene &S, const pg_config &cfg, const SDTree *tree, const Rng &rng, 
         if (!hit) break;
         if (depth++ >= cfg.rr_depth) {
             float q = std::min(maxc(T) * eta * eta, 0.95f);
-            if (rng.next1(dimOf(depth - 1, SLOT_RR)) >= q) break;
+            wr.f[26] = q;
+            wr.f[27] = 0;
+            if (rng.next1(dimOf(depth - 1, SLOT_RR)) >= q) {
+                wr.f[0] = (float)depth;
+                wr.f[1] = (float)its.prim;
+                wr.set3(2, its.p);
+                wr.set3(5, T);
+                wr.set3(18, L);
+                wr.flush();
+                break;
+            }
+            wr.f[27] = 1;
             T /= q;
         }
     }
@@ -462,14 +523,16 @@ void oracle_trace_rays_brute(void *sp, const float *rays, uint64_t n, float *hit
 
 // One path (pixel, sample) of oracle_render's loop with every ray it casts logged (Scene::logRay,
 // 11 floats each: kind 0 closest hit / 1 shadow, o.xyz, mint, d.xyz, maxt, t or occluded, prim bits).
-// Returns the number of rays (the log is truncated at `max`); L = the path's clamped radiance.
+// Returns the number of rays (the log is truncated at `max`); L = the path's clamped radiance; vtx:
+// the per-vertex records of the surface path (32 floats, the kernels' PG_WATCH record; n_vtx of them).
 // Debug aid for GPU/oracle divergence (tools/diverge_c3.py): re-trace the rays on both sides.
 uint64_t oracle_path_rays(void *sp, const pg_config *cfg, void *tp, uint32_t pixel, uint32_t sample, float *out,
-                          uint64_t max, float *Lout) {
+                          uint64_t max, float *Lout, float *vtx, uint64_t max_vtx, uint64_t *n_vtx) {
     const Scene &S = *(const Scene *)sp;
     const SDTree *tree = (const SDTree *)tp;
-    std::vector<float> log;
+    std::vector<float> log, vlog;
     g_rayLog = &log;
+    g_vtxLog = &vlog;
     Rng rng{rngKey(pixel, cfg->seed), sample};
     float jx, jy;
     rng.next2(0, jx, jy);
@@ -484,6 +547,9 @@ uint64_t oracle_path_rays(void *sp, const pg_config *cfg, void *tp, uint32_t pix
         L = Li(S, *cfg, tree, rng, ray, nullptr, cnt);
     }
     g_rayLog = nullptr;
+    g_vtxLog = nullptr;
+    *n_vtx = vlog.size() / 32;
+    std::memcpy(vtx, vlog.data(), sizeof(float) * 32 * std::min<uint64_t>(*n_vtx, max_vtx));
     float m = maxc(L);
     if (m > cfg->max_component_value) L = L * (cfg->max_component_value / m);
     Lout[0] = L.x;

@@ -48,7 +48,7 @@ def lib(capi):
             "oracle_trace_rays": (None, [VP, VP, C.c_uint64, C.c_int32, VP]),
             "oracle_trace_rays_brute": (None, [VP, VP, C.c_uint64, VP]),
             "oracle_path_rays": (C.c_uint64, [VP, C.POINTER(capi.pg_config), VP, C.c_uint32, C.c_uint32, VP,
-                                              C.c_uint64, VP]),
+                                              C.c_uint64, VP, VP, C.c_uint64, VP]),
             "oracle_bsdf_query": (None, [C.POINTER(capi.pg_material), VP, VP, VP, C.c_uint64, VP]),
             "oracle_material_type": (C.c_uint32, [C.POINTER(capi.pg_material)]),
             "oracle_rough_transmittance": (None, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
@@ -144,12 +144,16 @@ class OracleScene:
 
     def path_rays(self, cfg, sdtree, pixel, sample, max_rays=4096):
         """The rays one path casts: (n x 11: kind 0 closest / 1 shadow, o, mint, d, maxt, t or occluded,
-        prim bits), and its clamped radiance"""
+        prim bits), its clamped radiance, and its per-vertex records (n x 32, the kernels' PG_WATCH
+        record: depth, triangle, p, T, alpha, guided, mode, woPdf, weight, wo, L, NEE contribution, NEE
+        pdfs, RR q / survived, alive, shadow, b0, b1)"""
         out = np.zeros((max_rays, 11), np.float32)
         L = np.zeros(3, np.float32)
+        vtx = np.zeros((256, 32), np.float32)
+        nv = C.c_uint64()
         n = self.L.oracle_path_rays(self.h, C.byref(cfg), sdtree.h if sdtree else None, pixel, sample, _p(out),
-                                    max_rays, _p(L))
-        return out[:min(n, max_rays)], L
+                                    max_rays, _p(L), _p(vtx), 256, C.byref(nv))
+        return out[:min(n, max_rays)], L, vtx[:min(nv.value, 256)]
 
 
 class OracleSDTree:

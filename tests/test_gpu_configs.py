@@ -218,7 +218,7 @@ def test_max_render_time(pg):
     g.postprocess()
 
 
-def test_training_independent_of_lanes_and_runs(pg):
+def test_training_independent_of_lanes_and_runs(pg, monkeypatch):
     """Paths are pure functions of (pixel, sample): guided kitchen training gives the same sorted
     records, films and trees for 1 and 3 lanes in flight, again on a fresh context (closest-hit
     ties resolved independently of traversal order; DESIGN.md §4 Determinism), and with the fused
@@ -242,6 +242,11 @@ def test_training_independent_of_lanes_and_runs(pg):
     a = train(3)
     assert train(1) == a
     assert train(3) == a
-    # per-launch timing runs every class, shadow and trace kernel as its own launch; without it a
-    # bounce runs k_shade_all + k_rays: same paths either way
+    # per-launch timing times the fused launches a render runs (k_shade_all + k_rays)
     assert train(3, timing=1) == a
+    # the unfused per-class k_shade launches and separate k_shadow / k_trace launches (the path an
+    # environment-lit scene takes for shading): same paths
+    monkeypatch.setenv("PG_NO_SHADE_FUSION", "1")
+    monkeypatch.setenv("PG_NO_RAYS_FUSION", "1")
+    assert train(3) == a
+    assert train(1, timing=1) == a

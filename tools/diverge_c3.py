@@ -7,6 +7,10 @@ the GPU's traversal (pg_trace_rays) and the oracle's (Scene::traverse) disagree,
 verdict over every triangle (OracleScene.trace_brute).  GPU box only; writes JSON to argv[1].
 
   python tools/diverge_c3.py gpurun_out/r04b/diverge.json [--top 12]
+
+With the debug build (make -C mitsuba-path-guiding_amd watch: PG_WATCH, loaded through PG_LIB) each
+diverged path is also replayed with its vertex log on the GPU and compared with the oracle's Li log
+field by field (FIELDS below): the first vertex and quantity where the two part ways.
 """
 import argparse
 import json
@@ -21,6 +25,31 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 
+FIELDS = ["depth", "tri", "px", "py", "pz", "Tr", "Tg", "Tb", "alpha", "guided", "mode", "woPdf", "wr", "wg", "wb",
+          "wox", "woy", "woz", "Lr", "Lg", "Lb", "neeR", "neeG", "neeB", "neeEmPdf", "neeBsdfPdf", "rrQ", "rrSurvived",
+          "alive", "shadow", "b0", "b1"]
+WATCH_LIB = os.path.join(ROOT, "mitsuba-path-guiding_amd", "build", "libpgamd_watch.so")
+
+
+def first_difference(gv, cv):
+    """first (vertex, field) where the GPU and oracle vertex logs differ beyond fp32 noise"""
+    for i in range(max(len(gv), len(cv))):
+        if i >= len(gv) or i >= len(cv):
+            return {"vertex": i, "field": "count", "gpu_vertices": len(gv), "cpu_vertices": len(cv)}
+        for k, name in enumerate(FIELDS):
+            if name in ("shadow", "neeR", "neeG", "neeB"):
+                continue  # the kernels log every queued shadow ray, the oracle visible ones only
+            a, b = float(gv[i][k]), float(cv[i][k])
+            if name == "tri":
+                if int(a) != int(b):
+                    return {"vertex": i, "field": name, "gpu": a, "cpu": b}
+                continue
+            if not (abs(a - b) <= 2e-4 * max(1.0, abs(a), abs(b))):
+                return {"vertex": i, "field": name, "gpu": a, "cpu": b,
+                        "gpu_vertex": [float(x) for x in gv[i]], "cpu_vertex": [float(x) for x in cv[i]]}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
@@ -29,6 +58,10 @@ def main():
     ap.add_argument("--tiles", type=int, default=32)
     ap.add_argument("--threads", type=int, default=16)
     a = ap.parse_args()
+    watch = os.path.exists(WATCH_LIB)
+    if watch:
+        os.environ["PG_LIB"] = WATCH_LIB
+    import ctypes as C
     import pgload
     pg = pgload.load()
     import bench
@@ -41,6 +74,11 @@ def main():
     integ.reset()
     final, _ = integ.render(a.spp)
     dev = integ.dev
+    if watch:
+        from mitsuba_path_guiding_amd import integrator as I
+        wl = I.library()
+        wl.pg_debug_watch.argtypes = [C.c_uint32, C.c_uint32]
+        wl.pg_debug_watch_read.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
     off = 2 ** 5 - 1
     W, T = scene.width, 32
     tiles = [[y * W + x for y in range(ty, min(ty + T, scene.height)) for x in range(tx, min(tx + T, W))]
@@ -82,11 +120,23 @@ def main():
         ent = {"pixel": int(p), "xy": [int(p % W), int(p // W)], "gpu": g[top[j]].tolist(), "cpu": s[top[j]].tolist(),
                "share": float(se[top[j]] / se.sum()), "samples": []}
         for k in range(a.spp):
-            rays, L = osc.path_rays(cfg, tree, int(p), off + k)
+            rays, L, cv = osc.path_rays(cfg, tree, int(p), off + k)
             d = np.abs(gs[j, k] - L).max()
             if d <= 1e-3 * max(float(np.abs(L).max()), float(np.abs(gs[j, k]).max()), 1e-6):
                 continue
             smp = {"sample": off + k, "gpu_L": gs[j, k].tolist(), "cpu_L": L.tolist(), "rays": int(len(rays))}
+            if watch:  # replay the path with the kernels' vertex log
+                assert wl.pg_debug_watch(int(p), off + k) == 0
+                dev.reset_film()
+                dev.render_pass(1, off + k)
+                gv = np.zeros((256, 32), np.float32)
+                nv = C.c_uint32()
+                assert wl.pg_debug_watch_read(gv.ctypes.data, 256, C.byref(nv)) == 0
+                gv = gv[: nv.value]
+                gv = gv[np.argsort(gv[:, 0], kind="stable")]
+                smp["first_vertex_difference"] = first_difference(gv, cv)
+                smp["gpu_vertices"] = gv.tolist()
+                smp["cpu_vertices"] = cv.tolist()
             # re-trace the oracle path's rays on the GPU: first disagreement
             for i, r in enumerate(rays):
                 kind = int(r[0])
@@ -113,7 +163,7 @@ def main():
         print(json.dumps({k: v for k, v in ent.items() if k != "samples"}), len(ent["samples"]), "diverged samples",
               flush=True)
         for smp in ent["samples"][:4]:
-            print("   ", json.dumps(smp), flush=True)
+            print("   ", json.dumps({k: v for k, v in smp.items() if not k.endswith("_vertices")}), flush=True)
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(out, f, indent=1)
