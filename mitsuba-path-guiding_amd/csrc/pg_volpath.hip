@@ -12,6 +12,34 @@
 // stream the CPU oracle (oracle/orc_volpath.h) draws from.
 #include "pg_trace.h"
 
+// Index checks of the megakernel (debug build PG_VOL_CHECK=1, make volcheck): VCHK(cond, code, value)
+// is `cond` in the product build (a guard the code keeps) and, in the check build, also counts
+// violations and keeps the first one's code and value (pg_debug_volcheck_read).  Codes: 1 the emitter
+// walk's transmittance re-walk missed a surface the first walk hit, 2 a shadow walk's medium
+// transition on an invalid triangle, 3 rad[item] out of range, 4 a training vertex out of range,
+// 5 a majorant cell out of range, 6 a density cell out of range.
+#ifndef PG_VOL_CHECK
+#define PG_VOL_CHECK 0
+#endif
+#if PG_VOL_CHECK
+__device__ uint32_t pgVolCheck[12];  // count, first code, first value, per-code counts [3 + code - 1]
+__device__ __forceinline__ bool volCheck(bool ok, uint32_t code, uint32_t value) {
+    if (!ok && atomicAdd(&pgVolCheck[0], 1u) == 0) {
+        pgVolCheck[1] = code;
+        pgVolCheck[2] = value;
+    }
+    if (!ok) atomicAdd(&pgVolCheck[2 + code], 1u);  // per-code counts in [3, 8] (codes 1..6)
+    return ok;
+}
+extern "C" int pg_debug_volcheck_read(uint32_t *out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(pgVolCheck), 12 * 4) == hipSuccess ? 0 : -1;
+}
+#define VCHK(cond, code, value) volCheck((cond), (code), (uint32_t)(value))
+#else
+#define VCHK(cond, code, value) (cond)
+#endif
+
 namespace {
 
 #define VOL_BLOCK TRACE_BLOCK  // the traversal stack columns assume TRACE_BLOCK threads per block
@@ -96,6 +124,10 @@ __device__ __forceinline__ float lookupDensity(const MedView &M, f3 p) {
     const float px = p.x * M.gs.x + M.go.x, py = p.y * M.gs.y + M.go.y, pz = p.z * M.gs.z + M.go.z;
     const int x1 = (int)floorf(px), y1 = (int)floorf(py), z1 = (int)floorf(pz);
     if (x1 < 0 || y1 < 0 || z1 < 0 || x1 + 1 >= M.rx || y1 + 1 >= M.ry || z1 + 1 >= M.rz) return 0.0f;
+#if PG_VOL_CHECK
+    if (!VCHK((size_t)x1 + 1 < (size_t)M.rx && (size_t)y1 + 1 < (size_t)M.ry && (size_t)z1 + 1 < (size_t)M.rz, 6, x1))
+        return 0.0f;
+#endif
     const float fx = px - x1, fy = py - y1, fz = pz - z1, _fx = 1.0f - fx, _fy = 1.0f - fy, _fz = 1.0f - fz;
 #if PG_DENSITY_BRICKS
     // per-axis (brick, in-brick) offsets of the two corner coordinates
@@ -209,6 +241,9 @@ __device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0
     float t = t0;
     for (;;) {
         const float tExit = fminf(fminf(tNext[0], tNext[1]), fminf(tNext[2], t1));
+#if PG_VOL_CHECK
+        if (!VCHK(c[0] >= 0 && c[1] >= 0 && c[2] >= 0 && c[0] < n[0] && c[1] < n[1] && c[2] < n[2], 5, c[0])) return false;
+#endif
         const float mu = M.maj[((size_t)c[2] * M.my + c[1]) * M.mx + c[0]];
         if (mu > 0) {
             for (;;) {
@@ -343,6 +378,11 @@ __device__ __forceinline__ float mediumTransmittance(const VolDev &v, int m, f3 
 }
 
 // ---- scene queries ----------------------------------------------------------------------------
+// o + d t with explicit FMAs: the emitter walk's second pass must reproduce its first pass's origins
+// bit for bit (with `o + d * t` the compiler may contract one site and not the other)
+__device__ __forceinline__ f3 advance(f3 o, f3 d, float t) {
+    return mk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z));
+}
 __device__ __forceinline__ float max3abs(f3 o) { return fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)); }
 // ShapeKDTree::rayIntersect(ray, its) epsilon rule for mint == Epsilon (skdtree.cpp:125-128)
 __device__ __forceinline__ float itsMinT(f3 o) { return kEpsilon * fmaxf(max3abs(o), kEpsilon); }
@@ -392,6 +432,7 @@ __device__ __forceinline__ float sceneTransmittance(const SceneDev &sc, const Vo
         if (surface && (interactions == maxInteractions || !isNullMat(sc, triBits(sc, tri)))) return 0.0f;
         if (medium >= 0) T *= mediumTransmittance(v, medium, o, d, fminf(t, remaining), rng);
         if (!surface || T == 0) break;
+        if (!VCHK(tri != 0xFFFFFFFFu, 2, interactions)) break;
         const uint32_t tm = v.tmed[tri];
         if (tm) {
             const f3 n = rawFaceNormal(sc, tri);
@@ -444,7 +485,7 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
             fetchHit(sc, tri, u, w, d, h);
             m = targetMedium(tm, d, h.geoN);
         }
-        o = o + d * t;
+        o = advance(o, d, t);
         walked += t;
         mint = itsMinT(o);
         if (++interactions > 100) return;
@@ -463,8 +504,15 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
         for (int k = 0; k <= interactions; ++k) {
             float tt, uu, ww;
             uint32_t tr;
-            closestHit(sc, oo, d, mt, __int_as_float(0x7f800000), tt, tr, uu, ww, stk);
+            const bool hitR = closestHit(sc, oo, d, mt, __int_as_float(0x7f800000), tt, tr, uu, ww, stk);
             segs++;
+            // the re-walk repeats the first walk's rays, so it hits the same surfaces; were a rounding
+            // difference to make it miss, tr would be ~0 and v.tmed[tr] / fetchHit would read 16 GB
+            // past their arrays (the round-3 C5 faults): end the estimate instead
+            if (!VCHK(hitR, 1, k)) {
+                T = 0.0f;
+                break;
+            }
             if (mm >= 0) {
                 T *= mediumTransmittance(v, mm, oo, d, tt, rng);
                 if (T == 0) break;
@@ -475,7 +523,7 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
                 fetchHit(sc, tr, uu, ww, d, hh);
                 mm = targetMedium(tm, d, hh.geoN);
             }
-            oo = oo + d * tt;
+            oo = advance(oo, d, tt);
             mt = itsMinT(oo);
         }
     }
@@ -508,6 +556,9 @@ __device__ __forceinline__ void writeVertex(const VolDev &v, uint32_t item, uint
                                             f3 L) {
     float cu, cv;
     dirToCanonical(wo, cu, cv);
+#if PG_VOL_CHECK
+    if (!VCHK(item < v.vtx_P, 4, item)) return;
+#endif
     float4 *vb = v.vtx + ((size_t)k * v.vtx_P + item) * PG_VTX_F4;
     vb[0] = f4(x, woPdf);
     vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
@@ -820,6 +871,9 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
         }
         if (!__any(alive)) break;
         if (alive && !volStep<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows)) {
+#if PG_VOL_CHECK
+            if (VCHK(item < nitems, 3, item))
+#endif
             v.rad[item] = f4(P.L, __uint_as_float(P.nv));  // .w: training vertices (k_commit)
             lookups += rng.lookups;
             alive = false;

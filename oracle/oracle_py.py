@@ -11,7 +11,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(_HERE, "_build", "liboracle.so")
+LIB = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "_build", "liboracle.so")  # ORACLE_LIB: sanitizer builds
 _lib = None
 
 
