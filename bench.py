@@ -349,10 +349,18 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
         if t and v[2]:
             e["traffic_bytes_per_launch"] = t
             e["traffic_over_algorithmic"] = round(t / (v[1] / v[2]), 3)
+        cal = measured.get(k, {}).get("calibration_avg_ns")
+        if cal and v[2]:  # the same launches' duration in the committed rocprofv3 summary
+            e["avg_launch_ms_rocprof"] = round(cal / 1e6, 4)
+            e["frac_rocprof"] = round(v[1] / v[2] / (cal / 1e9) / 1e9 / HBM_PEAK_GBS, 5)
         out[k] = e
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
             "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
+            # the fraction with the kernel's duration from the committed rocprofv3 summary of the same
+            # launches (profiles/pmc_latest.json "calibration", revision in traffic_source) in place of
+            # this run's HIP events: the two agree when the profiled revision is this one
+            "frac_rocprof": out[dom].get("frac_rocprof"), "avg_launch_ms_rocprof": out[dom].get("avg_launch_ms_rocprof"),
             "kernel": dom, "dominant_by": "algorithmic bytes per pass (time shares under kernels)",
             "algorithmic_bytes_per_launch": int(per_launch),
             "avg_launch_ms": round(ms / max(launches, 1), 4),
@@ -374,18 +382,21 @@ def volume_roofline(d):
     ms, launches = d["volume_ms"], max(d["volume_launches"], 1)
     nbytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    traffic, source = None, None
+    traffic, source, cal = None, None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_volpath_latest.json")
     if os.path.exists(pmc):
         try:
             pj = json.load(open(pmc))
             traffic = pj.get("kernels", {}).get("k_volpath", {}).get("hbm_bytes_per_launch")
+            cal = pj.get("kernels", {}).get("k_volpath", {}).get("avg_ns")
             source = {"file": "profiles/pmc_volpath_latest.json", "profiled": pj.get("source"),
                       "revision": pj.get("revision")}
         except (OSError, ValueError):
             traffic = None
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
+            "frac_rocprof": round(nbytes / launches / (cal / 1e9) / 1e9 / HBM_PEAK_GBS, 5) if cal else None,
+            "avg_launch_ms_rocprof": round(cal / 1e6, 4) if cal else None,
             "kernel": "k_volpath", "algorithmic_bytes_per_launch": int(nbytes / launches),
             "avg_launch_ms": round(ms / launches, 4),
             "density_lookups_per_launch": int(d["density_lookups"] / launches),

@@ -176,6 +176,11 @@ struct Ctx {
     DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
     DevBuf vol_vtx;                     // guided volpath training vertices (48 B each)
     uint64_t vol_vtx_cap = 0;
+    // volumetric wavefront (PG_VOL_WAVEFRONT): SoA path state (VolWave, 7 x 16 B per slot) and five
+    // sharded queues (flight / surface for two iterations, medium vertices) + their counters
+    DevBuf vw_state, vw_items, vw_counts;
+    PinnedBuf vw_host;                  // counter readback
+    uint32_t vw_cap = 0;
     uint32_t vol_cap = 0;
     uint32_t num_tris = 0, num_mats = 0;
     uint32_t bvh_top_nodes = 0;  // breadth-first top levels of the binary BVH (staged in LDS by k_trace)
@@ -1094,7 +1099,83 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     return PG_OK;
 }
 
-// progressive_volpath: chunks of (pixel, sample) items through k_volpath, films in chunk order
+// The volumetric path as a wavefront (pg_volpath.hip k_vcam / k_vflight / k_vvertex / k_vtail) or as the
+// persistent megakernel k_volpath (PG_VOL_WAVEFRONT=0): the same per-path arithmetic and random
+// streams, so the same films and trees
+// (read per chunk, so tests can compare both in one process)
+bool volWavefront() {
+    const char *e = std::getenv("PG_VOL_WAVEFRONT");
+    return e ? std::atoi(e) != 0 : true;
+}
+// below this many live paths a chunk's remaining paths finish in one k_vtail launch (PG_VOL_TAIL_PATHS)
+uint32_t volTailPaths() {
+    const char *e = std::getenv("PG_VOL_TAIL_PATHS");
+    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 16;
+}
+
+// One chunk (np pixels from pb, nl layers) through the wavefront: camera rays, then per iteration the
+// free flights and the interactions, until at most volTailPaths() paths live; the tail finishes them.
+// The host reads the queue counters once per iteration (grid sizes; the kernels read the counts).
+pg_status volWavefrontChunk(Ctx *c, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                            uint32_t pb, uint32_t np, uint32_t nl, uint32_t sample_base) {
+    const uint32_t n = np * nl;
+    const uint32_t stride = pg_queue_stride(n);
+    if (c->vw_cap < n) {
+        HIPC(c, c->vw_state.alloc((size_t)n * 16 * 7));
+        HIPC(c, c->vw_items.alloc((size_t)stride * PG_QSHARDS * 4 * 5));
+        c->vw_cap = n;
+    }
+    HIPC(c, c->vw_counts.alloc((size_t)PG_QSHARDS * 4 * 5));
+    HIPC(c, c->vw_host.reserve((size_t)PG_QSHARDS * 4 * 5));
+    float4 *st = c->vw_state.as<float4>();
+    const size_t cap = c->vw_cap;
+    VolWave w{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
+              reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap};
+    // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices
+    const size_t qstride = (size_t)pg_queue_stride(c->vw_cap) * PG_QSHARDS;
+    Queue q[5];
+    for (int k = 0; k < 5; ++k)
+        q[k] = Queue{c->vw_items.as<uint32_t>() + k * qstride, c->vw_counts.as<uint32_t>() + k * PG_QSHARDS, stride};
+    uint32_t *hc = reinterpret_cast<uint32_t *>(c->vw_host.p);
+    auto maxShard = [&](int k) {
+        uint32_t m = 0, t = 0;
+        for (int i = 0; i < PG_QSHARDS; ++i) {
+            m = std::max(m, hc[k * PG_QSHARDS + i]);
+            t += hc[k * PG_QSHARDS + i];
+        }
+        return std::make_pair(m, t);
+    };
+    HIPC(c, hipMemsetAsync(c->vw_counts.p, 0, (size_t)PG_QSHARDS * 4 * 5, c->stream));
+    pg_launch_vol_camera(c->stream, g, sc, v, w, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_base, q[0], q[2]);
+    HIPC(c, hipGetLastError());
+    const uint32_t tail = volTailPaths();
+    for (int it = 0;; ++it) {
+        const int cur = it & 1, nxt = cur ^ 1;
+        HIPC(c, hipMemcpyAsync(hc, c->vw_counts.p, (size_t)PG_QSHARDS * 4 * 5, hipMemcpyDeviceToHost, c->stream));
+        HIPC(c, hipStreamSynchronize(c->stream));
+        if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+        const auto f = maxShard(cur), su = maxShard(2 + cur);
+        if (f.second + su.second == 0) break;
+        if (f.second + su.second <= tail) {
+            pg_launch_vol_tail(c->stream, g, sc, v, sd, w, q[cur], f.first, q[2 + cur], su.first);
+            HIPC(c, hipGetLastError());
+            break;
+        }
+        // the next iteration's output queues and the medium queue start empty
+        HIPC(c, hipMemsetAsync(q[nxt].counts, 0, PG_QSHARDS * 4, c->stream));
+        HIPC(c, hipMemsetAsync(q[2 + nxt].counts, 0, PG_QSHARDS * 4, c->stream));
+        HIPC(c, hipMemsetAsync(q[4].counts, 0, PG_QSHARDS * 4, c->stream));
+        pg_launch_vol_flight(c->stream, g, v, sd, w, q[cur], f.first, q[4], q[2 + cur]);
+        // shard bounds without a readback: a medium vertex came from a flight; a surface vertex from a
+        // flight or from the previous iteration's interactions; no shard exceeds the queue stride
+        const uint32_t mm = f.first, ms = std::min(stride, f.first + su.first);
+        pg_launch_vol_vertex(c->stream, g, sc, v, sd, w, q[4], mm, q[2 + cur], ms, q[nxt], q[2 + nxt]);
+        HIPC(c, hipGetLastError());
+    }
+    return PG_OK;
+}
+
+// progressive_volpath: chunks of (pixel, sample) items through the wavefront or k_volpath, films in chunk order
 pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) {
     const uint32_t npix = (uint32_t)c->local_pixels.size();
     // 2^25 items per launch: fewer persistent-kernel tails (C5 guided: 177.8 -> 189.8 Mpaths/s
@@ -1167,8 +1248,13 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
             HIPC(c, hipEventCreate(&e.b));
             evs.push_back(e);
             HIPC(c, hipEventRecord(e.a, c->stream));
-            pg_launch_volpath(c->stream, g, sc, v, sd, c->d_local_pixels.as<uint32_t>(), pb, np, nl,
-                              sample_offset + layer);
+            if (volWavefront()) {
+                pg_status ws = volWavefrontChunk(c, g, sc, v, sd, pb, np, nl, sample_offset + layer);
+                if (ws) return ws;
+            } else {
+                pg_launch_volpath(c->stream, g, sc, v, sd, c->d_local_pixels.as<uint32_t>(), pb, np, nl,
+                                  sample_offset + layer);
+            }
             HIPC(c, hipEventRecord(e.b, c->stream));
             if (g.record) {
                 const uint64_t items = (uint64_t)np * nl, add = items * (uint64_t)maxV;

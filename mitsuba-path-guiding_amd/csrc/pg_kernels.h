@@ -71,6 +71,18 @@ struct VolDev {
     uint32_t refill_min;       // k_volpath refills a wave's finished lanes once at least this many are idle
 };
 
+// Volumetric wavefront (pg_volpath.hip k_vcam, k_vflight, k_vvertex, k_vtail): the megakernel's per-lane
+// VPath + VRng as SoA per slot (slot = the chunk's work item), read and written by each stage
+struct VolWave {
+    float4 *o;   // (ray origin, its.t)
+    float4 *d;   // (ray direction, its.u)
+    uint4 *s;    // (bits(its.v), its.tri, (medium + 1) | valid << 16 | scattered << 17 | emission << 18, depth)
+    float4 *T;   // (throughput, eta)
+    float4 *L;   // (radiance, bits(training vertices written))
+    uint4 *r;    // random stream (key, sample, next dimension, density lookups so far)
+    float4 *mp;  // the medium interaction point of the current iteration's free flight
+};
+
 // Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).
 // Appends are wave-aggregated atomics on the shard's own counter: one counter per queue serialized
 // every append of the chip (58k returning atomics on one address: 658 us; on 64 addresses: 18 us,
@@ -138,6 +150,21 @@ void pg_launch_splat(hipStream_t s, const SDDev &sd, const pg_record *recs, unsi
 void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                        const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
                        uint32_t sample_base);
+// Volumetric wavefront, one chunk of npix * nlayers items (slot = item): the camera rays and first hits
+// (paths in a medium -> flight, others -> surface queue); per iteration the free flights of `flight`
+// (medium interactions -> med, flights reaching their surface -> surf) and the vertices of `med` and
+// `surf` (surviving paths -> next_flight / next_surf by their medium); the tail finishes the paths
+// of `flight` and `surf` one thread each.  max_*: upper bounds of the largest shard counts.
+void pg_launch_vol_camera(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w,
+                          const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
+                          uint32_t sample_base, Queue flight, Queue surf);
+void pg_launch_vol_flight(hipStream_t s, const GParams &g, const VolDev &v, const SDDev &sd, const VolWave &w,
+                          Queue flight, uint32_t max_flight, Queue med, Queue surf);
+void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf,
+                          Queue next_flight, Queue next_surf);
+void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                        const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf);
 void pg_launch_phase_query(hipStream_t s, const GMedium *medium, const float *in, const float *wog, uint32_t n,
                            float *out);
 // corner-packed density of a linear grid (pg_layout.h PG_DENSITY_CORNERS); out: 8 floats per cell

@@ -566,32 +566,51 @@ __device__ __forceinline__ void writeVertex(const VolDev &v, uint32_t item, uint
     vb[3] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
 }
 
-// one iteration of the Li loop; false when the path ends.  GUIDED: SD-tree guiding at medium and
-// smooth surface vertices (one-sample MIS with the phase function / BSDF, oracle/orc_volpath.h),
-// guided free flight and training vertices; with an unbuilt tree it only writes the vertices.
+// One iteration of the Li loop, in three parts that the megakernel (volStep) and the wavefront
+// kernels (k_vflight, k_vvertex) share, so both run the same arithmetic on the same random streams:
+//   volDepthOk   the loop condition (progressive_volpath.cpp:107) and the device bounce cap;
+//   volFlight    the free flight of a path in a medium (Medium::sampleDistance, :109-115): true with
+//                the medium interaction point mp, false when the flight reaches the surface its.t;
+//   volMedium /  the medium (:117-196) and surface (:197-352) interactions including Russian roulette
+//   volSurface   (:354-370); false when the path ends.
+// GUIDED: SD-tree guiding at medium and smooth surface vertices (one-sample MIS with the phase function
+// / BSDF, oracle/orc_volpath.h), guided free flight and training vertices; with an unbuilt tree it
+// only writes the vertices.
+__device__ __forceinline__ bool volDepthOk(const GParams &g, const VPath &P) {
+    return (P.depth <= g.max_depth || g.max_depth < 0) && P.depth <= g.depth_cap;
+}
 template <bool GUIDED>
-__device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                                        VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
-                                        uint32_t &shadows) {
+__device__ __forceinline__ bool volFlight(const VolDev &v, const SDDev &sd, VPath &P, VRng &rng, f3 &mp) {
+    const bool guiding = GUIDED && sd.built;
+    const float maxt = P.its.valid ? P.its.t : __int_as_float(0x7f800000);
+    if (guiding && v.dist_beta > 0) {
+        float w;
+        const bool inMedium = mediumSampleGuided(v, sd, P.medium, P.o, P.d, maxt, rng, mp, w);
+        P.T = P.T * w;
+        return inMedium;
+    }
+    return mediumSample(v, P.medium, P.o, P.d, maxt, rng, mp);
+}
+// Russian roulette at the end of an interaction (progressive_volpath.cpp:354-370)
+__device__ __forceinline__ bool volRoulette(const GParams &g, VPath &P, VRng &rng) {
+    if (P.depth++ >= g.rr_depth) {
+        const float q = fminf(maxc(P.T) * P.eta * P.eta, 0.95f);
+        if (rng.next1() >= q) return false;
+        P.T = P.T / q;
+    }
+    P.scattered = true;
+    return true;
+}
+template <bool GUIDED>
+__device__ __forceinline__ bool volMedium(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                                          VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
+                                          uint32_t &shadows, f3 mp) {
     const int maxDepth = g.max_depth;
-    if (!(P.depth <= maxDepth || maxDepth < 0) || P.depth > g.depth_cap) return false;
     const int maxInter = maxDepth - P.depth - 1;
     const bool guiding = GUIDED && sd.built;
     const bool record = GUIDED && g.record;
     const float alpha = g.bsdf_fraction;
-    bool inMedium = false;
-    f3 mp = mk1(0.f);
-    if (P.medium >= 0) {
-        const float maxt = P.its.valid ? P.its.t : __int_as_float(0x7f800000);
-        if (guiding && v.dist_beta > 0) {
-            float w;
-            inMedium = mediumSampleGuided(v, sd, P.medium, P.o, P.d, maxt, rng, mp, w);
-            P.T = P.T * w;
-        } else {
-            inMedium = mediumSample(v, P.medium, P.o, P.d, maxt, rng, mp);
-        }
-    }
-    if (inMedium) {
+    {
         // ---- medium interaction (progressive_volpath.cpp:117-196)
         if (P.depth >= maxDepth && maxDepth != -1) return false;
         const GMedium &GM = v.media[P.medium];
@@ -674,7 +693,19 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
             P.L = P.L + P.T * value * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
         }
         P.emission = false;
-    } else {
+    }
+    return volRoulette(g, P, rng);
+}
+template <bool GUIDED>
+__device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                                           VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
+                                           uint32_t &shadows) {
+    const int maxDepth = g.max_depth;
+    const int maxInter = maxDepth - P.depth - 1;
+    const bool guiding = GUIDED && sd.built;
+    const bool record = GUIDED && g.record;
+    const float alpha = g.bsdf_fraction;
+    {
         // ---- surface interaction (progressive_volpath.cpp:197-352)
         if (!P.its.valid) return false;  // no environment emitter
         Hit h;
@@ -799,15 +830,298 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
         }
         P.emission = false;
     }
-    if (P.depth++ >= g.rr_depth) {
-        const float q = fminf(maxc(P.T) * P.eta * P.eta, 0.95f);
-        if (rng.next1() >= q) return false;
-        P.T = P.T / q;
-    }
-    P.scattered = true;
-    return true;
+    return volRoulette(g, P, rng);
+}
+template <bool GUIDED>
+__device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                                        VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
+                                        uint32_t &shadows) {
+    if (!volDepthOk(g, P)) return false;
+    f3 mp = mk1(0.f);
+    if (P.medium >= 0 && volFlight<GUIDED>(v, sd, P, rng, mp))
+        return volMedium<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows, mp);
+    return volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows);
 }
 
+// the camera ray of work item `item` (PerspectiveCamera::sampleRay, perspective.cpp:271-298) and its
+// first hit: a new path state
+__device__ __forceinline__ void volCamera(const GParams &g, const SceneDev &sc, const VolDev &v,
+                                          const uint32_t *__restrict__ local_pixels, uint32_t pix_begin, uint32_t npix,
+                                          uint32_t sample_base, uint32_t item, VPath &P, VRng &rng, const TStack &stk,
+                                          uint32_t &segs) {
+    const uint32_t layer = item / npix, lp = item - layer * npix;
+    const uint32_t pix = local_pixels[pix_begin + lp];
+    rng = VRng{rngKey(pix, g.seed), sample_base + layer, 1, 0};
+    float jx, jy;
+    rng2(rng.key, rng.sample, 0, jx, jy);
+    const float px = (float)(pix % g.width) + jx, py = (float)(pix / g.width) + jy;
+    const float sx = px / (float)g.width, sy = py / (float)g.height;
+    const f3 nearP = mk((1.0f - 2.0f * sx) * g.tan_half, (1.0f - 2.0f * sy) / g.aspect * g.tan_half, 1.0f);
+    const f3 dl = normalize(nearP);
+    const float invZ = 1.0f / dl.z;
+    P.o = mk(g.cam_o[0], g.cam_o[1], g.cam_o[2]);
+    P.d = mk(g.cam_left[0], g.cam_left[1], g.cam_left[2]) * dl.x +
+          mk(g.cam_up[0], g.cam_up[1], g.cam_up[2]) * dl.y + mk(g.cam_dir[0], g.cam_dir[1], g.cam_dir[2]) * dl.z;
+    float t, u, w;
+    uint32_t tri;
+    const bool hit = closestHit(sc, P.o, P.d, g.near_clip * invZ, g.far_clip * invZ, t, tri, u, w, stk);
+    segs++;
+    P.its = ItsRef{hit, hit ? t : __int_as_float(0x7f800000), u, w, tri};
+    P.T = mk1(1.f);
+    P.L = mk1(0.f);
+    P.eta = 1.0f;
+    P.medium = v.cam_medium;
+    P.depth = 1;
+    P.scattered = false;
+    P.emission = true;
+    P.nv = 0;
+}
+
+// ---- wavefront state (VolWave, pg_kernels.h) ---------------------------------------------------
+__device__ __forceinline__ void loadPath(const VolWave &w, uint32_t slot, VPath &P, VRng &rng) {
+    const float4 o = w.o[slot], d = w.d[slot], T = w.T[slot], L = w.L[slot];
+    const uint4 s = w.s[slot], r = w.r[slot];
+    P.o = xyz(o);
+    P.d = xyz(d);
+    P.its = ItsRef{((s.z >> 16) & 1u) != 0, o.w, d.w, __uint_as_float(s.x), s.y};
+    P.medium = (int)(s.z & 0xFFFFu) - 1;
+    P.scattered = ((s.z >> 17) & 1u) != 0;
+    P.emission = ((s.z >> 18) & 1u) != 0;
+    P.depth = (int)s.w;
+    P.T = xyz(T);
+    P.eta = T.w;
+    P.L = xyz(L);
+    P.nv = __float_as_uint(L.w);
+    rng = VRng{r.x, r.y, r.z, r.w};
+}
+__device__ __forceinline__ void storePath(const VolWave &w, uint32_t slot, const VPath &P, const VRng &rng) {
+    w.o[slot] = f4(P.o, P.its.t);
+    w.d[slot] = f4(P.d, P.its.u);
+    w.s[slot] = make_uint4(__float_as_uint(P.its.v), P.its.tri,
+                           (uint32_t)(P.medium + 1) | (P.its.valid ? 1u << 16 : 0u) | (P.scattered ? 1u << 17 : 0u) |
+                               (P.emission ? 1u << 18 : 0u),
+                           (uint32_t)P.depth);
+    w.T[slot] = f4(P.T, P.eta);
+    w.L[slot] = f4(P.L, __uint_as_float(P.nv));
+    w.r[slot] = make_uint4(rng.key, rng.sample, rng.dim, rng.lookups);
+}
+// wave sums of the per-thread counters, one atomic each per wave
+__device__ __forceinline__ void volStats(const VolDev &v, uint32_t segs, uint32_t shadows, uint32_t lookups) {
+    unsigned long long s0 = segs, s1 = shadows, s2 = lookups;
+    for (int off = 32; off > 0; off >>= 1) {
+        s0 += __shfl_xor(s0, off);
+        s1 += __shfl_xor(s1, off);
+        s2 += __shfl_xor(s2, off);
+    }
+    if ((threadIdx.x & 63) == 0 && (s0 | s1 | s2)) {
+        atomicAdd(v.stats, s0);
+        atomicAdd(v.stats + 1, s1);
+        atomicAdd(v.stats + 2, s2);
+    }
+}
+// a path that ended: its radiance and training-vertex count (k_film / k_commit), its lookups counted
+__device__ __forceinline__ void volEnd(const VolDev &v, uint32_t slot, const VPath &P, const VRng &rng,
+                                       uint32_t &lookups) {
+    v.rad[slot] = f4(P.L, __uint_as_float(P.nv));
+    lookups += rng.lookups;
+}
+__device__ __forceinline__ uint32_t slotShard(uint32_t slot) { return (slot >> 6) & (PG_QSHARDS - 1); }
+
+}  // namespace
+
+// ---- volumetric wavefront (the volpath loop as a wavefront of path states) -----
+// Stages per iteration of progressive_volpath.cpp:98-374: the free flight of every path in a medium
+// (k_vflight), then the medium and surface interactions in one launch whose blocks take one kind each
+// (k_vvertex: no wave runs both branches), each path in its slot with its random stream carried in
+// VolWave, so films and trees are bit-identical to k_volpath's (which runs the same volFlight /
+// volMedium / volSurface per lane).  The last few paths finish one thread each (k_vtail).
+template <bool GUIDED>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, VolDev v, VolWave w,
+                                                      const uint32_t *__restrict__ local_pixels, uint32_t pix_begin,
+                                                      uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue qf,
+                                                      Queue qs) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, v.stack_ovf);
+    const uint32_t n = npix * nlayers;
+    uint32_t segs = 0, lookups = 0;
+    for (uint32_t base = blockIdx.x * TRACE_BLOCK; base < n; base += gridDim.x * TRACE_BLOCK) {
+        const uint32_t slot = base + threadIdx.x;
+        bool toF = false, toS = false;
+        if (slot < n) {
+            VPath P;
+            VRng rng;
+            volCamera(g, sc, v, local_pixels, pix_begin, npix, sample_base, slot, P, rng, stk, segs);
+            if (!volDepthOk(g, P)) {
+                volEnd(v, slot, P, rng, lookups);
+            } else {
+                storePath(w, slot, P, rng);
+                toF = P.medium >= 0;
+                toS = !toF;
+            }
+        }
+        const uint32_t sh = slotShard(base + (threadIdx.x & ~63u));
+        waveAppend(toF, slot, qf.items + (size_t)sh * qf.stride, qf.counts + sh);
+        waveAppend(toS, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
+    }
+    volStats(v, segs, 0, lookups);
+}
+
+// free flights: medium interaction -> med, the flight reached its surface (or left the medium) -> surf
+template <bool GUIDED>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm,
+                                                         Queue qs) {
+    const uint32_t sh = blockIdx.x & (PG_QSHARDS - 1), rows = gridDim.x / PG_QSHARDS;
+    const uint32_t n = qf.counts[sh];
+    for (uint32_t base = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        bool toM = false, toS = false;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = qf.items[(size_t)sh * qf.stride + i];
+            const float4 o = w.o[slot], d = w.d[slot];
+            const uint4 s = w.s[slot], r = w.r[slot];
+            VPath P;
+            P.o = xyz(o);
+            P.d = xyz(d);
+            P.its.valid = ((s.z >> 16) & 1u) != 0;
+            P.its.t = o.w;
+            P.medium = (int)(s.z & 0xFFFFu) - 1;
+            const bool wT = GUIDED && sd.built && v.dist_beta > 0;  // guided free flight reweights T
+            if (wT) P.T = xyz(w.T[slot]);
+            VRng rng{r.x, r.y, r.z, r.w};
+            f3 mp = mk1(0.f);
+            toM = volFlight<GUIDED>(v, sd, P, rng, mp);
+            toS = !toM;
+            w.r[slot] = make_uint4(rng.key, rng.sample, rng.dim, rng.lookups);
+            if (wT) w.T[slot] = f4(P.T, w.T[slot].w);
+            if (toM) w.mp[slot] = f4(mp, 0.0f);
+        }
+        waveAppend(toM, slot, qm.items + (size_t)sh * qm.stride, qm.counts + sh);
+        waveAppend(toS, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
+    }
+}
+
+// interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices
+template <bool GUIDED>
+__global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
+                                                                       VolWave w, Queue qm, Queue qs, uint32_t mblocks,
+                                                                       Queue nf, Queue ns) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, v.stack_ovf);
+    const bool medium = blockIdx.x < mblocks;
+    const uint32_t b = medium ? blockIdx.x : blockIdx.x - mblocks;
+    const uint32_t nb = medium ? mblocks : gridDim.x - mblocks;
+    const Queue &q = medium ? qm : qs;
+    const uint32_t sh = b & (PG_QSHARDS - 1), rows = nb / PG_QSHARDS;
+    const uint32_t n = q.counts[sh];
+    uint32_t segs = 0, shadows = 0, lookups = 0;
+    for (uint32_t base = (b / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
+        const uint32_t i = base + threadIdx.x;
+        bool toF = false, toS = false;
+        uint32_t slot = 0;
+        if (i < n) {
+            slot = q.items[(size_t)sh * q.stride + i];
+            VPath P;
+            VRng rng;
+            loadPath(w, slot, P, rng);
+            const bool alive = medium ? volMedium<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, xyz(w.mp[slot]))
+                                      : volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+            if (alive && volDepthOk(g, P)) {
+                storePath(w, slot, P, rng);
+                toF = P.medium >= 0;
+                toS = !toF;
+            } else {
+                volEnd(v, slot, P, rng, lookups);
+            }
+        }
+        waveAppend(toF, slot, nf.items + (size_t)sh * nf.stride, nf.counts + sh);
+        waveAppend(toS, slot, ns.items + (size_t)sh * ns.stride, ns.counts + sh);
+    }
+    volStats(v, segs, shadows, lookups);
+}
+
+// the chunk's last paths: each thread runs one to its end (paths of `qf` start with their flight, those
+// of `qs` with their surface interaction)
+template <bool GUIDED>
+__global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vtail(GParams g, SceneDev sc, VolDev v, SDDev sd,
+                                                                     VolWave w, Queue qf, Queue qs, uint32_t fblocks) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, v.stack_ovf);
+    const bool flight = blockIdx.x < fblocks;
+    const uint32_t b = flight ? blockIdx.x : blockIdx.x - fblocks;
+    const uint32_t nb = flight ? fblocks : gridDim.x - fblocks;
+    const Queue &q = flight ? qf : qs;
+    const uint32_t sh = b & (PG_QSHARDS - 1), rows = nb / PG_QSHARDS;
+    const uint32_t n = q.counts[sh];
+    uint32_t segs = 0, shadows = 0, lookups = 0;
+    for (uint32_t i = (b / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += rows * TRACE_BLOCK) {
+        const uint32_t slot = q.items[(size_t)sh * q.stride + i];
+        VPath P;
+        VRng rng;
+        loadPath(w, slot, P, rng);
+        bool alive = flight || volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+        while (alive) alive = volStep<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+        volEnd(v, slot, P, rng, lookups);
+    }
+    volStats(v, segs, shadows, lookups);
+}
+
+namespace {
+static inline uint32_t vrows(uint32_t max_shard, uint32_t cap) {
+    const uint32_t r = (max_shard + TRACE_BLOCK - 1) / TRACE_BLOCK;
+    return r < cap ? r : cap;
+}
+}  // namespace
+
+void pg_launch_vol_camera(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w,
+                          const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
+                          uint32_t sample_base, Queue flight, Queue surf) {
+    const uint64_t n = (uint64_t)npix * nlayers;
+    if (!n) return;
+    const uint64_t want = (n + TRACE_BLOCK - 1) / TRACE_BLOCK;
+    const dim3 grid((uint32_t)(want < TRACE_MAX_BLOCKS ? want : TRACE_MAX_BLOCKS));  // the overflow ring's size
+    if (g.guiding)
+        hipLaunchKernelGGL(k_vcam<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, w, local_pixels, pix_begin, npix,
+                           nlayers, sample_base, flight, surf);
+    else
+        hipLaunchKernelGGL(k_vcam<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, w, local_pixels, pix_begin, npix,
+                           nlayers, sample_base, flight, surf);
+}
+void pg_launch_vol_flight(hipStream_t s, const GParams &g, const VolDev &v, const SDDev &sd, const VolWave &w,
+                          Queue flight, uint32_t max_flight, Queue med, Queue surf) {
+    if (!max_flight) return;
+    const dim3 grid(PG_QSHARDS * vrows(max_flight, TRACE_MAX_BLOCKS / PG_QSHARDS));
+    if (g.guiding) hipLaunchKernelGGL(k_vflight<true>, grid, dim3(TRACE_BLOCK), 0, s, g, v, sd, w, flight, med, surf);
+    else hipLaunchKernelGGL(k_vflight<false>, grid, dim3(TRACE_BLOCK), 0, s, g, v, sd, w, flight, med, surf);
+}
+void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf,
+                          Queue next_flight, Queue next_surf) {
+    // both block ranges within TRACE_MAX_BLOCKS (the traversal stacks' overflow ring)
+    const uint32_t mr = max_med ? vrows(max_med, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
+    const uint32_t sr = max_surf ? vrows(max_surf, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
+    if (mr + sr == 0) return;
+    const dim3 grid(PG_QSHARDS * (mr + sr));
+    if (g.guiding)
+        hipLaunchKernelGGL(k_vvertex<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, PG_QSHARDS * mr,
+                           next_flight, next_surf);
+    else
+        hipLaunchKernelGGL(k_vvertex<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, PG_QSHARDS * mr,
+                           next_flight, next_surf);
+}
+void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                        const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf) {
+    const uint32_t fr = max_flight ? vrows(max_flight, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
+    const uint32_t sr = max_surf ? vrows(max_surf, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
+    if (fr + sr == 0) return;
+    const dim3 grid(PG_QSHARDS * (fr + sr));
+    if (g.guiding)
+        hipLaunchKernelGGL(k_vtail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, PG_QSHARDS * fr);
+    else
+        hipLaunchKernelGGL(k_vtail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, PG_QSHARDS * fr);
+}
+
+namespace {
 }  // namespace
 
 template <bool GUIDED>
@@ -838,33 +1152,7 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
                 if (item >= nitems) {
                     done = true;
                 } else {
-                    // camera ray (PerspectiveCamera::sampleRay, perspective.cpp:271-298) + first hit
-                    const uint32_t layer = item / npix, lp = item - layer * npix;
-                    const uint32_t pix = local_pixels[pix_begin + lp];
-                    rng = VRng{rngKey(pix, g.seed), sample_base + layer, 1, 0};
-                    float jx, jy;
-                    rng2(rng.key, rng.sample, 0, jx, jy);
-                    const float px = (float)(pix % g.width) + jx, py = (float)(pix / g.width) + jy;
-                    const float sx = px / (float)g.width, sy = py / (float)g.height;
-                    const f3 nearP = mk((1.0f - 2.0f * sx) * g.tan_half, (1.0f - 2.0f * sy) / g.aspect * g.tan_half, 1.0f);
-                    const f3 dl = normalize(nearP);
-                    const float invZ = 1.0f / dl.z;
-                    P.o = mk(g.cam_o[0], g.cam_o[1], g.cam_o[2]);
-                    P.d = mk(g.cam_left[0], g.cam_left[1], g.cam_left[2]) * dl.x +
-                          mk(g.cam_up[0], g.cam_up[1], g.cam_up[2]) * dl.y + mk(g.cam_dir[0], g.cam_dir[1], g.cam_dir[2]) * dl.z;
-                    float t, u, w;
-                    uint32_t tri;
-                    const bool hit = closestHit(sc, P.o, P.d, g.near_clip * invZ, g.far_clip * invZ, t, tri, u, w, stk);
-                    segs++;
-                    P.its = ItsRef{hit, hit ? t : __int_as_float(0x7f800000), u, w, tri};
-                    P.T = mk1(1.f);
-                    P.L = mk1(0.f);
-                    P.eta = 1.0f;
-                    P.medium = v.cam_medium;
-                    P.depth = 1;
-                    P.scattered = false;
-                    P.emission = true;
-                    P.nv = 0;
+                    volCamera(g, sc, v, local_pixels, pix_begin, npix, sample_base, item, P, rng, stk, segs);
                     alive = true;
                 }
             }

@@ -223,6 +223,7 @@ def test_volpath_refill_threshold_bit_identical(pg, monkeypatch):
     from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer
     sc = pg.scenes.smoke(96, 96, res=48)
     out = []
+    monkeypatch.setenv("PG_VOL_WAVEFRONT", "0")  # the megakernel (the wavefront has no lane refill)
     for r in ("1", "24", "64"):
         monkeypatch.setenv("PG_VOL_REFILL", r)
         t = GuidedVolumetricPathTracer({"trainingIterations": 3, "samplesPerProgression": 8})
@@ -233,3 +234,44 @@ def test_volpath_refill_threshold_bit_identical(pg, monkeypatch):
     for o in out[1:]:
         assert np.array_equal(o[0], out[0][0]) and np.array_equal(o[1], out[0][1])
         assert np.array_equal(o[2], out[0][2])
+
+
+@pytest.mark.parametrize("case", ["guided", "plain_global", "guided_exact_chunked"])
+def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
+    """The volumetric wavefront (k_vcam / k_vflight / k_vvertex / k_vtail, PG_VOL_WAVEFRONT) runs the
+    megakernel's volFlight / volMedium / volSurface on the same random streams, each path in its own
+    slot: films, sums of squares, training records (through the trees) and path counters must be the
+    megakernel's bit for bit -- whether every iteration runs as launches (tail threshold 0), the
+    default tail threshold, or the tail kernel takes the whole chunk after the camera rays."""
+    from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer, ProgressiveVolumetricPathTracer
+    sc = pg.scenes.smoke(96, 96, res=48)
+    props = {"trainingIterations": 3, "samplesPerProgression": 8}
+    if case == "plain_global":
+        Tracer, props = ProgressiveVolumetricPathTracer, {"samplesPerProgression": 8}
+    else:
+        Tracer = GuidedVolumetricPathTracer
+    if case == "guided_exact_chunked":
+        props.update({"exactMis": True, "maxPathsInFlight": 4096 + 512})
+    out = []
+    for wf, tail in (("0", None), ("1", "0"), ("1", None), ("1", str(1 << 30))):
+        monkeypatch.setenv("PG_VOL_WAVEFRONT", wf)
+        if tail is None:
+            monkeypatch.delenv("PG_VOL_TAIL_PATHS", raising=False)
+        else:
+            monkeypatch.setenv("PG_VOL_TAIL_PATHS", tail)
+        t = Tracer(dict(props))
+        if case == "plain_global":  # the reference's single majorant (heterogeneous.cpp:589-660)
+            t.cfg.volume_majorant = pg.capi.PG_MAJORANT_GLOBAL
+        t.preprocess(sc)
+        rgbw, sq = t.render(8)
+        st = t.dev.stats()
+        out.append((rgbw, sq, t.dev.get_sdtree() if t.guided else None,
+                    (st["paths"], st["segments"], st["shadow_rays"], st["density_lookups"], st["records"])))
+        t.postprocess()
+    base = out[0]
+    assert base[3][0] > 0 and base[3][3] > 0
+    for o in out[1:]:
+        assert np.array_equal(o[0], base[0]) and np.array_equal(o[1], base[1])
+        if base[2] is not None:
+            assert np.array_equal(o[2], base[2])
+        assert o[3] == base[3], (o[3], base[3])
