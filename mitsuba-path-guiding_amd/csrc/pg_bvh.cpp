@@ -227,6 +227,39 @@ static void woopRecord(const float *P, const uint32_t *I, uint32_t t, float *w) 
     w[11] = (float)(-rowdot(1));
 }
 
+// TriAccel record of triangle t (TriAccel::load, triaccel.h:37-94, in fp32 as the reference computes
+// it; this file builds with -ffp-contract=off): 12 floats, pg_layout.h PG_TRIACCEL
+static void triAccelRecord(const float *P, const uint32_t *I, uint32_t t, float *w) {
+    static const int waldModulo[4] = {1, 2, 0, 1};
+    const float *A = P + 3 * (size_t)I[3 * (size_t)t], *B = P + 3 * (size_t)I[3 * (size_t)t + 1],
+                *C = P + 3 * (size_t)I[3 * (size_t)t + 2];
+    const float b[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]}, c[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]};
+    const float N[3] = {c[1] * b[2] - c[2] * b[1], c[2] * b[0] - c[0] * b[2], c[0] * b[1] - c[1] * b[0]};  // cross(c, b)
+    int k = 0;
+    for (int j = 0; j < 3; ++j)
+        if (std::fabs(N[j]) > std::fabs(N[k])) k = j;
+    const int u = waldModulo[k], v = waldModulo[k + 1];
+    const float n_k = N[k], denom = b[u] * c[v] - b[v] * c[u];
+    for (int i = 0; i < 12; ++i) w[i] = 0.0f;
+    uint32_t kk = (uint32_t)k;
+    if (denom == 0) {  // degenerate: k = 3, a NaN plane that no t passes
+        w[0] = w[1] = w[2] = std::numeric_limits<float>::quiet_NaN();
+        kk = 3;
+    } else {
+        w[0] = N[u] / n_k;                                          // n_u
+        w[1] = N[v] / n_k;                                          // n_v
+        w[2] = (A[0] * N[0] + A[1] * N[1] + A[2] * N[2]) / n_k;    // n_d = dot(A, N) / n_k
+        w[4] = A[u];                                                // a_u
+        w[5] = A[v];                                                // a_v
+        w[6] = b[u] / denom;                                        // b_nu
+        w[7] = -b[v] / denom;                                       // b_nv
+        w[8] = c[v] / denom;                                        // c_nu
+        w[9] = -c[u] / denom;                                       // c_nv
+    }
+    std::memcpy(&w[3], &kk, 4);
+    std::memcpy(&w[10], &t, 4);  // the original triangle id
+}
+
 namespace {
 
 // Child-slot assignment by ray octant: slot s holds the child a ray of octant s (bit a set =
@@ -444,8 +477,9 @@ static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t s
     out.wide_depth = wideDepth;
     if (wideDepth + 1 > stack_limit || order.size() != nt) return false;
     out.order.swap(order);
-    out.woop.assign(12 * (size_t)nt, 0.0f);
-    for (uint32_t k = 0; k < nt; ++k) woopRecord(P, I, out.order[k], &out.woop[12 * (size_t)k]);
+    out.tris.assign(12 * (size_t)nt, 0.0f);
+    for (uint32_t k = 0; k < nt; ++k)
+        (PG_TRIACCEL ? triAccelRecord : woopRecord)(P, I, out.order[k], &out.tris[12 * (size_t)k]);
     return true;
 }
 
@@ -679,14 +713,14 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         }
         out.wnodes.assign(PG_WIDE_NODE_F4 * 4, 0.0f);
         out.order.clear();
-        out.woop.clear();
+        out.tris.clear();
         out.max_depth = out.wide_depth = 1;
         out.top_nodes = 1;
         for (int a = 0; a < 3; ++a) out.lo[a] = out.hi[a] = 0.0f;
         return true;
     }
     // one binary build (leaves <= PG_WIDE_LEAF_MAX triangles) serves both BVHs, and both walk one
-    // Woop triangle array in one order (the L2 of an XCD then holds one copy of the triangles)
+    // triangle array in one order (the L2 of an XCD then holds one copy of the triangles)
     std::vector<BNode> bn;
     std::vector<uint32_t> ord, posOf;
     uint32_t maxDepth = 0;

@@ -166,7 +166,7 @@ struct Ctx {
     // scene
     bool has_scene = false;
     GParams g{};
-    DevBuf nodes, woop, wnodes, tshade, tclass, mats, rtab, ems, emtri, emcdf;  // woop: both BVHs' triangles
+    DevBuf nodes, tris, wnodes, tshade, tclass, mats, rtab, ems, emtri, emcdf;  // tris: both BVHs' triangles
     DevBuf env, envtex, envtab;  // environment emitter: GEnv record, texels, CDFs + row weights
     bool has_env = false;
     // media (volpath)
@@ -364,7 +364,7 @@ pg_status upload(Ctx *c, DevBuf &b, const std::vector<T> &v) {
 }
 
 SceneDev sceneView(const Ctx *c) {
-    return SceneDev{c->nodes.as<float4>(), c->woop.as<float4>(), c->wnodes.as<float4>(), c->woop.as<float4>(),
+    return SceneDev{c->nodes.as<float4>(), c->tris.as<float4>(), c->wnodes.as<float4>(), c->tris.as<float4>(),
                     c->tshade.as<float4>(), c->tclass.as<uint8_t>(),
                     c->mats.as<GMat>(),
                     c->ems.as<GEmitter>(), c->emtri.as<float4>(), c->emcdf.as<float>(),
@@ -912,7 +912,7 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     if ((s = upload(c, c->rtab, rtab))) return s;
     for (auto &mo : rtabOf) c->host_mats[mo.first].rtrans = c->rtab.as<float>() + mo.second;
     c->bvh_top_nodes = std::min<uint32_t>(bvh.top_nodes, PG_BVH_TOP_NODES);
-    if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->woop, bvh.woop)) ||
+    if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->tris, bvh.tris)) ||
         (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||
         (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||

@@ -7,9 +7,9 @@
 
 struct SceneDev {
     const float4 *nodes;    // binary BVH (closest hit), PG_BVH_NODE_F4 float4 per node
-    const float4 *woop;     // 3 float4 per BVH-order triangle
+    const float4 *tris;     // 3 float4 per BVH-order triangle
     const float4 *wnodes;   // 8-wide BVH (shadow rays), PG_WIDE_NODE_F4 float4 per node
-    const float4 *wwoop;    // the same triangle records as woop (both BVHs share one triangle order)
+    const float4 *wtris;    // the same triangle records as tris (both BVHs share one triangle order)
     const float4 *tshade;   // PG_TRI_SHADE_F4 float4 per BVH-order triangle
     const uint8_t *tclass;  // PG_CLASS_* of the triangle's material, per BVH-order triangle
     const GMat *mats;

@@ -160,7 +160,7 @@ __device__ __forceinline__ void traceRows(const GParams &g, const SceneDev &sc, 
             float tmax = d.w;
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
-            bool h = traverse<false, LTOP>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk, top, ntop);
+            bool h = traverse<false, LTOP>(sc.nodes, sc.tris, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk, top, ntop);
             float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
             if (first) first[slot] = hr;
             if (ENV && !h) {
@@ -763,7 +763,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_tail(GParams g, SceneDev sc, SD
             const float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.ray_d[slot]);
             float tmax = d.w, u = 0, v = 0;
             tri = 0xFFFFFFFFu;
-            const bool h = traverse<false>(sc.nodes, sc.woop, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
+            const bool h = traverse<false>(sc.nodes, sc.tris, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk);
             float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
             if (ENV && !h) {
                 const f3 e = envEscapeRadiance(g, sc, p, slot, xyz(d));
@@ -1131,7 +1131,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const f
         h[1] = h[2] = h[3] = 0.0f;
         return;
     }
-    bool hit = traverse<false>(sc.nodes, sc.woop, o, d, r[3], tmax, tri, u, v, stk);
+    bool hit = traverse<false>(sc.nodes, sc.tris, o, d, r[3], tmax, tri, u, v, stk);
     uint32_t orig = hit ? __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w) : 0xFFFFFFFFu;
     h[0] = hit ? tmax : 0.0f;
     h[1] = __uint_as_float(orig);

@@ -104,6 +104,16 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 // 16-B loads instead of eight scattered 4-B loads over four cache lines.  8x the memory of the grid
 // (530 MB for 256^3): a trade the 288 GB of HBM3E affords.
 
+// Triangle records of both BVHs (48 B = 3 x float4 per BVH-order triangle).  PG_TRIACCEL (default): the
+// reference's own triangle test, TriAccel (include/mitsuba/render/triaccel.h:37-157; the oracle's
+// orc_scene.h TriAccel): (n_u, n_v, n_d, bits(k)), (a_u, a_v, b_nu, b_nv), (c_nu, c_nv, bits(original
+// triangle id), 0), built in fp32 as TriAccel::load builds it and tested with contraction off, so a hit's
+// t and barycentrics are the oracle's bit for bit; k = 3 marks a degenerate triangle (NaN plane: never
+// hit).  PG_TRIACCEL = 0: Woop unit-triangle rows (rows of [e0 e1 n]^-1 in double; A/B).
+#ifndef PG_TRIACCEL
+#define PG_TRIACCEL 1
+#endif
+
 // Per-triangle shading record (5 x float4 = 80 B), indexed by BVH-order triangle id:
 //   [0] p0.xyz, bits(material | (emitter + 1) << 16)
 //   [1] p1.xyz, n2.z

@@ -39,7 +39,8 @@ __device__ __forceinline__ void stS(uint4 *p, uint4 a) { *p = a; }
 // BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,
 // sahkdtree3.h:178-308) with the same contract: closest t in [tmin, tmax] (any hit for shadow
 // rays).  Closest-hit rays walk the 4-wide BVH (128-B nodes; the binary BVH's 64-B nodes in PG_BVH4 = 0
-// builds), shadow rays the 8-wide BVH with quantised boxes (80-B nodes); all test 48-B Woop unit triangles.
+// builds), shadow rays the 8-wide BVH with quantised boxes (80-B nodes); all test the 48-B triangle records
+// of pg_layout.h PG_TRIACCEL (the reference's TriAccel).
 // Stacks: entries [0, LDS) in LDS (columns per thread, stride TRACE_BLOCK: conflict-free), deeper
 // entries in a per-thread column of a global overflow ring (stride = launched threads).
 struct TStack {
@@ -75,23 +76,47 @@ struct WStack {
     }
 };
 
-// Woop unit-triangle test (closest hit: a hit at t <= tmax replaces the current one)
-__device__ __forceinline__ bool woopHit(const float4 *__restrict__ woop, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
-                                        float &tt, float &bu, float &bv) {
-    const float4 w0 = woop[3 * tr + 0];
+// Triangle test of every walk (pg_layout.h PG_TRIACCEL): a hit at t in [tmin, tmax] with (bu, bv) the
+// barycentric weights of p1 and p2.  TriAccel::rayIntersect (triaccel.h:96-157) with the reference's
+// expression order and no contraction: the oracle's t, u, v bit for bit.
+__device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
+                                       float &tt, float &bu, float &bv) {
+#if PG_TRIACCEL
+#pragma clang fp contract(off)
+    const float4 r0 = tris[3 * tr + 0];
+    const uint32_t k = __float_as_uint(r0.w);  // projection axis; (u, v) = the next two axes cyclically
+    const float ou = k == 0 ? o.y : (k == 1 ? o.z : o.x), ov = k == 0 ? o.z : (k == 1 ? o.x : o.y);
+    const float ok = k == 0 ? o.x : (k == 1 ? o.y : o.z);
+    const float du = k == 0 ? d.y : (k == 1 ? d.z : d.x), dv = k == 0 ? d.z : (k == 1 ? d.x : d.y);
+    const float dk = k == 0 ? d.x : (k == 1 ? d.y : d.z);
+    tt = (r0.z - ou * r0.x - ov * r0.y - ok) / (du * r0.x + dv * r0.y + dk);
+    if (!(tt >= tmin && tt <= tmax)) return false;
+    const float4 r1 = tris[3 * tr + 1];
+    const float hu = ou + tt * du - r1.x, hv = ov + tt * dv - r1.y;
+    const float u = hv * r1.z + hu * r1.w;
+    if (!(u >= 0.0f)) return false;
+    const float2 r2 = *reinterpret_cast<const float2 *>(tris + 3 * tr + 2);
+    const float v = hu * r2.x + hv * r2.y;
+    if (!(v >= 0.0f && u + v <= 1.0f)) return false;
+    bu = u;
+    bv = v;
+    return true;
+#else
+    const float4 w0 = tris[3 * tr + 0];
     float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
     float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
     tt = oz / dz;
     if (!(tt >= tmin && tt <= tmax)) return false;
-    const float4 w1 = woop[3 * tr + 1];
+    const float4 w1 = tris[3 * tr + 1];
     float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
     if (!(a >= 0.0f && a <= 1.0f)) return false;
-    const float4 w2 = woop[3 * tr + 2];
+    const float4 w2 = tris[3 * tr + 2];
     float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
     if (!(b >= 0.0f && a + b <= 1.0f)) return false;
     bu = b;             // weight of p1
     bv = 1.0f - a - b;  // weight of p2
     return true;
+#endif
 }
 
 __device__ __forceinline__ float qbyte(uint32_t lo, uint32_t hi, int s) {
@@ -121,7 +146,7 @@ __device__ __forceinline__ uint32_t permuteXor8(uint32_t m, uint32_t x) {
 // stack as one group entry.  (Postponing triangle groups while few lanes have triangle work, as
 // in the paper, measured slower here: 20.0 vs 17.4 ms per pass.)
 template <bool ANY>
-__device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o,
+__device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, const float4 *__restrict__ tris, f3 o,
                                              f3 d, float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                              const WStack &stk) {
     const float eps = 1e-30f;
@@ -188,7 +213,7 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
             const uint32_t tr = T.x + (uint32_t)(__ffs(T.y) - 1);
             T.y &= T.y - 1u;
             float tt, bu, bv;
-            if (woopHit(woop, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {  // ties: lower index
+            if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {  // ties: lower index
                 found = true;
                 if (ANY) return true;
                 tmax = tt;
@@ -208,32 +233,21 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
 // Postponed-leaf triangle tests shared by the binary and the 4-wide closest-hit walks: every
 // triangle of leaf ref `leaf` (< 0: ~leaf = first << 4 | count) against the ray.
 template <bool ANY>
-__device__ __forceinline__ bool leafTest(const float4 *__restrict__ woop, int leaf, f3 o, f3 d, float tmin,
+__device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int leaf, f3 o, f3 d, float tmin,
                                          float &tmax, uint32_t &hitTri, float &hu, float &hv, bool &found) {
     const uint32_t lr = ~(uint32_t)leaf;
     const uint32_t first = lr >> 4, cnt = lr & 15u;
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t tr = first + k;
-        const float4 w0 = woop[3 * tr + 0];
-        float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
-        float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-        float tt = oz / dz;
-        if (tt >= tmin && tt <= tmax) {
-            const float4 w1 = woop[3 * tr + 1];
-            float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
-            if (a >= 0.0f && a <= 1.0f) {
-                const float4 w2 = woop[3 * tr + 2];
-                float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
-                // equal distances: the lower triangle index (see traverseBin)
-                if (b >= 0.0f && a + b <= 1.0f && (tt < tmax || tr < hitTri)) {
-                    found = true;
-                    if (ANY) return true;
-                    tmax = tt;
-                    hitTri = tr;
-                    hu = b;
-                    hv = 1.0f - a - b;
-                }
-            }
+        float tt, bu, bv;
+        // equal distances: the lower triangle index (see traverseBin)
+        if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {
+            found = true;
+            if (ANY) return true;
+            tmax = tt;
+            hitTri = tr;
+            hu = bu;
+            hv = bv;
         }
     }
     return false;
@@ -286,7 +300,7 @@ __device__ __forceinline__ SlabRay slabRay(f3 o, f3 d) {
 // distances; the others pushed far to near), with the binary walk's while-while loop, postponed
 // leaves, tie rule and widened culling distance, so it returns the same hit.
 template <bool ANY>
-__device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+__device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, const float4 *__restrict__ tris, f3 o, f3 d,
                                           float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                           const TStack &stk) {
     const int DONE = 0x7fffffff;
@@ -338,7 +352,7 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
             if (!__any(leaf >= 0)) break;
         }
         while (leaf < 0) {
-            if (leafTest<ANY>(woop, leaf, o, d, tmin, tmax, hitTri, hu, hv, found)) return true;
+            if (leafTest<ANY>(tris, leaf, o, d, tmin, tmax, hitTri, hu, hv, found)) return true;
             leaf = node;
             if (node < 0) node = sp > 0 ? (int)stk.get(--sp) : DONE;
         }
@@ -352,7 +366,7 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
 // utilisation on gfx950).
 // LTOP: nodes [0, ntop) are read from `lnodes` (the top levels, staged in LDS by the caller).
 template <bool ANY, bool LTOP = false>
-__device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+__device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, const float4 *__restrict__ tris, f3 o, f3 d,
                                             float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                             const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
     const int DONE = 0x7fffffff;
@@ -420,28 +434,17 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
             const uint32_t first = lr >> 4, cnt = lr & 15u;
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t tr = first + k;
-                const float4 w0 = woop[3 * tr + 0];
-                float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
-                float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
-                float tt = oz / dz;
-                if (tt >= tmin && tt <= tmax) {
-                    const float4 w1 = woop[3 * tr + 1];
-                    float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
-                    if (a >= 0.0f && a <= 1.0f) {
-                        const float4 w2 = woop[3 * tr + 2];
-                        float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
-                        // equal distances (shared edges, coplanar triangles) go to the lower triangle
-                        // index, so the closest hit does not depend on the order in which the wave's
-                        // postponed leaves are visited (and thus on which paths share the wave)
-                        if (b >= 0.0f && a + b <= 1.0f && (tt < tmax || tr < hitTri)) {
-                            found = true;
-                            if (ANY) return true;
-                            tmax = tt;
-                            hitTri = tr;
-                            hu = b;             // weight of p1
-                            hv = 1.0f - a - b;  // weight of p2
-                        }
-                    }
+                float tt, bu, bv;
+                // equal distances (shared edges, coplanar triangles) go to the lower triangle index, so
+                // the closest hit does not depend on the order in which the wave's postponed leaves are
+                // visited (and thus on which paths share the wave)
+                if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {
+                    found = true;
+                    if (ANY) return true;
+                    tmax = tt;
+                    hitTri = tr;
+                    hu = bu;  // weight of p1
+                    hv = bv;  // weight of p2
                 }
             }
             // another postponed leaf (in node)?  process it too
@@ -454,14 +457,14 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
 
 // the closest-hit walk of this build's closest-hit BVH (SceneDev::nodes)
 template <bool ANY, bool LTOP = false>
-__device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ woop, f3 o, f3 d,
+__device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const float4 *__restrict__ tris, f3 o, f3 d,
                                          float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                          const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
 #if PG_BVH4
     static_assert(!LTOP, "LDS-staged top levels are a binary-BVH option");
-    return traverse4<ANY>(nodes, woop, o, d, tmin, tmax, hitTri, hu, hv, stk);
+    return traverse4<ANY>(nodes, tris, o, d, tmin, tmax, hitTri, hu, hv, stk);
 #else
-    return traverseBin<ANY, LTOP>(nodes, woop, o, d, tmin, tmax, hitTri, hu, hv, stk, lnodes, ntop);
+    return traverseBin<ANY, LTOP>(nodes, tris, o, d, tmin, tmax, hitTri, hu, hv, stk, lnodes, ntop);
 #endif
 }
 
@@ -474,9 +477,9 @@ __device__ __forceinline__ bool occluded(const SceneDev &sc, f3 o, f3 d, float t
     uint32_t tri = 0xFFFFFFFFu;
     float u, v;
 #if PG_BVH4 && PG_SHADOW4
-    return traverse4<true>(sc.nodes, sc.woop, o, d, tmin, tmax, tri, u, v, TStack{w.lds, w.ovf, w.ostride});
+    return traverse4<true>(sc.nodes, sc.tris, o, d, tmin, tmax, tri, u, v, TStack{w.lds, w.ovf, w.ostride});
 #else
-    return traverseWide<true>(sc.wnodes, sc.wwoop, o, d, tmin, tmax, tri, u, v, w);
+    return traverseWide<true>(sc.wnodes, sc.wtris, o, d, tmin, tmax, tri, u, v, w);
 #endif
 }
 
@@ -533,8 +536,12 @@ __device__ __forceinline__ void fetchHit(const SceneDev &sc, uint32_t tri, float
     float b0 = 1 - u - v;
     f3 p0 = xyz(s0), p1 = xyz(s1), p2 = xyz(s2);
     f3 n0 = xyz(s3), n1 = mk(s3.w, s4.x, s4.y), n2 = mk(s4.z, s4.w, s1.w);
-    // fillIntersectionRecord<true> (skdtree.h:343-430)
-    h.p = p0 * b0 + p1 * u + p2 * v;
+    // fillIntersectionRecord<true> (skdtree.h:343-430); the position without contraction, as the
+    // oracle's Scene::fill computes it (with the TriAccel barycentrics, the same point bit for bit)
+    {  // scalar expressions: the f3 operators' bodies lie outside this pragma's scope
+#pragma clang fp contract(off)
+        h.p = mk(p0.x * b0 + p1.x * u + p2.x * v, p0.y * b0 + p1.y * u + p2.y * v, p0.z * b0 + p1.z * u + p2.z * v);
+    }
     f3 side1 = p1 - p0, side2 = p2 - p0;
     f3 fn = cross(side1, side2);
     float l = len(fn);

@@ -393,7 +393,7 @@ __device__ __forceinline__ bool closestHit(const SceneDev &sc, f3 o, f3 d, float
     tri = 0xFFFFFFFFu;
     u = v = 0;
     if (!(tmax > tmin)) return false;
-    return traverse<false>(sc.nodes, sc.woop, o, d, tmin, t, tri, u, v, stk);
+    return traverse<false>(sc.nodes, sc.tris, o, d, tmin, t, tri, u, v, stk);
 }
 __device__ __forceinline__ uint32_t triBits(const SceneDev &sc, uint32_t tri) {
     return __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri].w);

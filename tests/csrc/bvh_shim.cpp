@@ -2,7 +2,7 @@
 // Checks the 4-wide closest-hit layout (pg_layout.h PG_QNODE_*) for structure -- every triangle in
 // exactly one leaf, child boxes containing their subtrees, the stack bound -- and runs a scalar
 // restatement of the device walk (traverse4: slabRay's padded slab test, widened culling distance, nearest-first
-// order, lower-index tie rule) against a brute-force loop over the same Woop records.
+// order, lower-index tie rule) against a brute-force loop over the same triangle records (TriAccel).
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -16,8 +16,21 @@ pgh::BvhOut g_bvh;
 std::vector<float> g_P;
 std::vector<uint32_t> g_I;
 
-bool woopHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax, float &tt) {
-    const float *w = &g_bvh.woop[12 * (size_t)tr];
+bool triHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax, float &tt) {
+    const float *w = &g_bvh.tris[12 * (size_t)tr];
+#if PG_TRIACCEL
+    // TriAccel::rayIntersect (triaccel.h:96-157), the device triHit's arithmetic (no contraction)
+    uint32_t k;
+    std::memcpy(&k, &w[3], 4);
+    const int iu = k == 0 ? 1 : (k == 1 ? 2 : 0), iv = k == 0 ? 2 : (k == 1 ? 0 : 1), ik = k == 0 ? 0 : (k == 1 ? 1 : 2);
+    tt = (w[2] - o[iu] * w[0] - o[iv] * w[1] - o[ik]) / (d[iu] * w[0] + d[iv] * w[1] + d[ik]);
+    if (!(tt >= tmin && tt <= tmax)) return false;
+    const float hu = o[iu] + tt * d[iu] - w[4], hv = o[iv] + tt * d[iv] - w[5];
+    const float u = hv * w[6] + hu * w[7];
+    if (!(u >= 0.0f)) return false;
+    const float v = hu * w[8] + hv * w[9];
+    return v >= 0.0f && u + v <= 1.0f;
+#else
     const float dz = d[0] * w[0] + d[1] * w[1] + d[2] * w[2];
     const float oz = w[3] - (o[0] * w[0] + o[1] * w[1] + o[2] * w[2]);
     tt = oz / dz;
@@ -26,6 +39,7 @@ bool woopHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax
     if (!(a >= 0.0f && a <= 1.0f)) return false;
     const float b = (w[11] + o[0] * w[8] + o[1] * w[9] + o[2] * w[10]) + tt * (d[0] * w[8] + d[1] * w[9] + d[2] * w[10]);
     return b >= 0.0f && a + b <= 1.0f;
+#endif
 }
 
 const float *qnode(int32_t n) { return &g_bvh.nodes[(size_t)n * 4 * PG_QNODE_F4]; }
@@ -125,7 +139,7 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
             uint32_t best = 0xFFFFFFFFu;
             for (uint32_t tr = 0; tr < nt; ++tr) {
                 float tt;
-                if (woopHit(tr, o, d, r[3], tmax, tt) && (tt < tmax || tr < best)) {
+                if (triHit(tr, o, d, r[3], tmax, tt) && (tt < tmax || tr < best)) {
                     tmax = tt;
                     best = tr;
                 }
@@ -157,7 +171,7 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
                 const uint32_t lr = ~(uint32_t)node, first = lr >> 4, cnt = lr & 15u;
                 for (uint32_t k = 0; k < cnt; ++k) {
                     float tt;
-                    if (woopHit(first + k, o, d, r[3], tmax, tt) && (tt < tmax || first + k < best)) {
+                    if (triHit(first + k, o, d, r[3], tmax, tt) && (tt < tmax || first + k < best)) {
                         tmax = tt;
                         best = first + k;
                     }
