@@ -552,6 +552,51 @@ static bool buildBinaryBvh(const std::vector<BNode> &bn, uint32_t maxDepth, cons
     return true;
 }
 
+// one 4-wide node (pg_layout.h PG_QNODE_*): child boxes box[2a][s] / box[2a+1][s] (lo / hi along axis
+// a) of the first `used` slots, refs r[4]; full-precision planes, or (PG_QNODE_QUANT) bytes in the
+// node's frame rounded outward as the 8-wide nodes' are
+static void putQuadNode(float *o, const float box[6][4], const int32_t r[4], int used) {
+#if PG_QNODE_QUANT
+    Box parent;
+    if (used == 0)
+        for (int a = 0; a < 3; ++a) parent.lo[a] = parent.hi[a] = 0.0f;
+    for (int s = 0; s < used; ++s)
+        for (int a = 0; a < 3; ++a) {
+            parent.lo[a] = std::min(parent.lo[a], box[2 * a][s]);
+            parent.hi[a] = std::max(parent.hi[a], box[2 * a + 1][s]);
+        }
+    uint32_t e = 0, w[6] = {0, 0, 0, 0, 0, 0};
+    for (int a = 0; a < 3; ++a) {
+        const int ex = quantExponent(parent.hi[a] - parent.lo[a]);
+        const float scale = std::ldexp(1.0f, ex);
+        e |= (uint32_t)(ex + 127) << (8 * a);
+        o[a] = parent.lo[a];
+        for (int s = 0; s < 4; ++s) {
+            double lo = 255, hi = 0;  // empty slot: an inverted box
+            if (s < used) {
+                lo = std::floor(((double)box[2 * a][s] - parent.lo[a]) / scale);
+                hi = std::ceil(((double)box[2 * a + 1][s] - parent.lo[a]) / scale);
+                lo = std::max(0.0, std::min(255.0, lo));
+                hi = std::max(0.0, std::min(255.0, hi));
+                while (lo > 0 && parent.lo[a] + (float)lo * scale > box[2 * a][s]) lo -= 1;
+                while (hi < 255 && parent.lo[a] + (float)hi * scale < box[2 * a + 1][s]) hi += 1;
+            }
+            w[2 * a] |= (uint32_t)lo << (8 * s);
+            w[2 * a + 1] |= (uint32_t)hi << (8 * s);
+        }
+    }
+    std::memcpy(&o[3], &e, 4);
+    std::memcpy(&o[4], r, 16);
+    std::memcpy(&o[8], w, 24);
+    o[14] = o[15] = 0.0f;
+#else
+    (void)used;
+    for (int a = 0; a < 6; ++a)
+        for (int s = 0; s < 4; ++s) o[4 * a + s] = box[a][s];
+    std::memcpy(&o[24], r, 16);
+#endif
+}
+
 // 4-wide BVH (PG_BVH4, closest hit) over the same tree; its leaves are the binary leaves (same refs).
 // Which binary nodes a 4-wide node absorbs is the SAH-optimal choice (the 8-wide collapse's dynamic
 // programme with 4 slots and the leaves fixed: it minimises the summed surface area of the opened
@@ -640,11 +685,12 @@ static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_
         const uint32_t q = alloc();
         float *o = &nodes[(size_t)q * 4 * PG_QNODE_F4];
         int32_t r[4] = {ref(0, 0), PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY};
+        float box[6][4] = {};
         for (int a = 0; a < 3; ++a) {
-            o[8 * a + 0] = bn[0].box.lo[a];
-            o[8 * a + 4] = bn[0].box.hi[a];
+            box[2 * a][0] = bn[0].box.lo[a];
+            box[2 * a + 1][0] = bn[0].box.hi[a];
         }
-        std::memcpy(&o[24], r, 16);
+        putQuadNode(o, box, r, 1);
         out.nodes.swap(nodes);
         return true;
     }
@@ -689,9 +735,7 @@ static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_
             }
         }
         float *o = &nodes[(size_t)t.qnode * 4 * PG_QNODE_F4];
-        for (int a = 0; a < 6; ++a)
-            for (int s = 0; s < 4; ++s) o[4 * a + s] = box[a][s];
-        std::memcpy(&o[24], r, 16);
+        putQuadNode(o, box, r, (int)ch.size());
     }
     out.nodes.swap(nodes);
     out.top_nodes = 0;
@@ -709,7 +753,8 @@ bool buildBvh(const float *P, const uint32_t *I, uint32_t nt, uint32_t stack_lim
         if (PG_BVH4) {  // one node without children
             out.nodes.assign(4 * PG_QNODE_F4, 0.0f);
             const int32_t r[4] = {PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY};
-            std::memcpy(&out.nodes[24], r, 16);
+            const float box[6][4] = {};
+            putQuadNode(out.nodes.data(), box, r, 0);
         }
         out.wnodes.assign(PG_WIDE_NODE_F4 * 4, 0.0f);
         out.order.clear();

@@ -143,11 +143,50 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 #ifndef PG_BVH4
 #define PG_BVH4 1
 #endif
+// PG_QNODE_QUANT = 1: the same tree in 64-B nodes (4 x float4) with child boxes quantised to bytes in the
+// node's frame (as the 8-wide shadow nodes):
+//   [0] origin.xyz (the node box's lo corner), bits((e_x + 127) | (e_y + 127) << 8 | (e_z + 127) << 16)
+//   [1] bits(child[4])
+//   [2] u32 lo.x, hi.x, lo.y, hi.y  [3] u32 lo.z, hi.z, 0, 0   -- byte s of each word: slot s's plane
+// plane = origin + q * 2^e, rounded outward (floor / ceil, checked against the fp32 reconstruction);
+// an empty slot has lo = 255, hi = 0 (an inverted box) and the PG_QNODE_EMPTY ref
+#ifndef PG_QNODE_QUANT
+#define PG_QNODE_QUANT 0
+#endif
+#if PG_QNODE_QUANT
+#define PG_QNODE_F4 4
+#else
 #define PG_QNODE_F4 8
+#endif
 #define PG_QNODE_EMPTY 0x7ffffffe
 // closest-hit stack entries a 4-wide traversal may need (the builder checks its trees against it;
 // the global overflow ring already holds PG_QSTACK_DEPTH - LDS_STACK words per thread)
 #define PG_QSTACK_DEPTH 96
+// host-side accessors of a 4-wide node (either layout; tests/csrc/bvh_shim.cpp): slot s's ref and box
+inline int32_t pg_qnode_ref(const float *node, int s) {
+    int32_t r;
+    __builtin_memcpy(&r, node + (PG_QNODE_QUANT ? 4 : 24) + s, 4);
+    return r;
+}
+inline void pg_qnode_box(const float *node, int s, float lo[3], float hi[3]) {
+#if PG_QNODE_QUANT
+    uint32_t e, w[6];
+    __builtin_memcpy(&e, node + 3, 4);
+    __builtin_memcpy(w, node + 8, 24);
+    for (int a = 0; a < 3; ++a) {
+        uint32_t eb = ((e >> (8 * a)) & 0xFFu) << 23;
+        float scale;
+        __builtin_memcpy(&scale, &eb, 4);
+        lo[a] = node[a] + (float)((w[2 * a] >> (8 * s)) & 0xFFu) * scale;
+        hi[a] = node[a] + (float)((w[2 * a + 1] >> (8 * s)) & 0xFFu) * scale;
+    }
+#else
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = node[8 * a + s];
+        hi[a] = node[8 * a + 4 + s];
+    }
+#endif
+}
 
 // 8-wide BVH node for shadow rays, with quantised child boxes (5 x float4 = 80 B; after Ylitie et al. 2017):
 //   [0] p.xyz (quantisation origin = node box min), bits(ex | ey << 8 | ez << 16 | imask << 24)

@@ -316,10 +316,38 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
         const float tcull = tmax * 1.000001f + tslack;
         while (node >= 0 && node != DONE) {
             const float4 *np = nodes + (size_t)PG_QNODE_F4 * node;
-            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
-            const float4 rf = np[6];
             float k[4];
             int r[4];
+#if PG_QNODE_QUANT
+            // planes origin + q 2^e: t = q (2^e idir) + (origin - o) idir, the latter padded outward by
+            // slabRay's addends and by 2^-22 |origin idir| (its own rounding)
+            const float4 n0 = np[0], rf = np[1], q0 = np[2], q1 = np[3];
+            const uint32_t e = __float_as_uint(n0.w);
+            const float sx = __uint_as_float((e & 0xFFu) << 23) * idir.x;
+            const float sy = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y;
+            const float sz = __uint_as_float(((e >> 16) & 0xFFu) << 23) * idir.z;
+            const float px = copysignf(2.38418579e-7f * fabsf(n0.x * idir.x), idir.x);
+            const float py = copysignf(2.38418579e-7f * fabsf(n0.y * idir.y), idir.y);
+            const float pz = copysignf(2.38418579e-7f * fabsf(n0.z * idir.z), idir.z);
+            const float bxl = fmaf(n0.x, idir.x, aLo.x) - px, bxh = fmaf(n0.x, idir.x, aHi.x) + px;
+            const float byl = fmaf(n0.y, idir.y, aLo.y) - py, byh = fmaf(n0.y, idir.y, aHi.y) + py;
+            const float bzl = fmaf(n0.z, idir.z, aLo.z) - pz, bzh = fmaf(n0.z, idir.z, aHi.z) + pz;
+            const uint32_t wlx = __float_as_uint(q0.x), whx = __float_as_uint(q0.y), wly = __float_as_uint(q0.z),
+                           why = __float_as_uint(q0.w), wlz = __float_as_uint(q1.x), whz = __float_as_uint(q1.y);
+#define PG_QB(w, i) ((float)(((w) >> (8 * (i))) & 0xFFu))
+#define PG_Q4_SLOT(i, c)                                                                              \
+    {                                                                                                 \
+        const float x0 = fmaf(PG_QB(wlx, i), sx, bxl), x1 = fmaf(PG_QB(whx, i), sx, bxh);              \
+        const float y0 = fmaf(PG_QB(wly, i), sy, byl), y1 = fmaf(PG_QB(why, i), sy, byh);              \
+        const float z0 = fmaf(PG_QB(wlz, i), sz, bzl), z1 = fmaf(PG_QB(whz, i), sz, bzh);              \
+        const float cmin = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), tmin));    \
+        const float cmax = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), tcull));   \
+        r[i] = __float_as_int(rf.c);                                                                  \
+        k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
+    }
+#else
+            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
+            const float4 rf = np[6];
 #define PG_Q4_SLOT(i, c)                                                                              \
     {                                                                                                 \
         const float x0 = fmaf(lx.c, idir.x, aLo.x), x1 = fmaf(hx.c, idir.x, aHi.x);                   \
@@ -330,8 +358,10 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
         r[i] = __float_as_int(rf.c);                                                                  \
         k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
     }
+#endif
             PG_Q4_SLOT(0, x) PG_Q4_SLOT(1, y) PG_Q4_SLOT(2, z) PG_Q4_SLOT(3, w)
 #undef PG_Q4_SLOT
+#undef PG_QB
             cxch(k[0], r[0], k[1], r[1]);
             cxch(k[2], r[2], k[3], r[3]);
             cxch(k[0], r[0], k[2], r[2]);

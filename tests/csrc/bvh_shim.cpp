@@ -43,11 +43,7 @@ bool triHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax,
 }
 
 const float *qnode(int32_t n) { return &g_bvh.nodes[(size_t)n * 4 * PG_QNODE_F4]; }
-int32_t qref(int32_t n, int s) {
-    int32_t r;
-    std::memcpy(&r, &qnode(n)[24 + s], 4);
-    return r;
-}
+int32_t qref(int32_t n, int s) { return pg_qnode_ref(qnode(n), s); }
 }  // namespace
 
 extern "C" {
@@ -86,10 +82,7 @@ void shim_check(uint32_t nt, uint32_t *out) {
             const int32_t r = qref(t.n, s);
             if (r == PG_QNODE_EMPTY) continue;
             float lo[3], hi[3];
-            for (int a = 0; a < 3; ++a) {
-                lo[a] = o[8 * a + s];
-                hi[a] = o[8 * a + 4 + s];
-            }
+            pg_qnode_box(o, s, lo, hi);
             // triangles of the child's subtree
             std::vector<int32_t> sub{r};
             while (!sub.empty()) {
@@ -183,10 +176,11 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
             float key[4];
             int32_t ref[4];
             for (int s = 0; s < 4; ++s) {
-                float cmin = r[3], cmax = tcull;
+                float cmin = r[3], cmax = tcull, blo[3], bhi[3];
+                pg_qnode_box(q, s, blo, bhi);  // the decoded planes (quantised nodes: origin + q 2^e)
                 for (int a = 0; a < 3; ++a) {
-                    const float t0 = std::fma(q[8 * a + s], idir[a], addLo[a]);
-                    const float t1 = std::fma(q[8 * a + 4 + s], idir[a], addHi[a]);
+                    const float t0 = std::fma(blo[a], idir[a], addLo[a]);
+                    const float t1 = std::fma(bhi[a], idir[a], addHi[a]);
                     cmin = std::fmax(cmin, std::fmin(t0, t1));
                     cmax = std::fmin(cmax, std::fmax(t0, t1));
                 }

@@ -7,8 +7,9 @@ O=gpurun_out/r04f
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_volume.py tests/test_gpu_tail.py tests/test_gpu_configs.py -x -q --timeout 250 --timeout-method thread > $O/gpu_tests.log 2>&1; s=$?; grep -E "passed|failed|FAILED|^E " $O/gpu_tests.log | head -20; [ $s -eq 0 ] || exit 1
 for i in 1 2; do
-  for v in tri woop; do
+  for v in tri woop q64; do
     L=""; [ $v = woop ] && L=mitsuba-path-guiding_amd/build_woop/libpgamd.so
+    [ $v = q64 ] && L=mitsuba-path-guiding_amd/build_q64/libpgamd.so
     PG_LIB=$L timeout -k 10 200 python bench.py --no-cpu --no-quality > $O/c3_${v}_$i.log 2>&1 || { echo "bench $v failed"; tail -5 $O/c3_${v}_$i.log; exit 1; }
     grep "^{" $O/c3_${v}_$i.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('c3 $v', d['value'], d['ms_per_step'], d['roofline']['kernels']['k_rays']['avg_launch_ms'], d['segments_per_path'])"
   done
