@@ -48,6 +48,12 @@ BYTES_SHADE_RECORD = 40        # + training record (recording passes only)
 BYTES_SHADOW_PER_RAY = 32      # shadow-queue read 32
 assert BYTES_TRACE_PER_RAY + BYTES_SHADE_PER_VERTEX + BYTES_SHADE_RECORD + BYTES_SHADOW_PER_RAY == BYTES_SEGMENT
 BYTES_DENSITY_LOOKUP = 32      # k_volpath (C5): one trilinear lookup gathers 8 f32 voxels
+# the volumetric wavefront's SoA path state (pg_kernels.h VolWave) moved per item: a free flight reads
+# origin, direction, its / medium record and random stream (64 B), writes the stream and the interaction
+# point (32 B) and moves its two queue entries (8 B); an interaction reads the whole state and the
+# interaction point (112 B), writes it back (96 B) and moves its queue entries (8 B)
+BYTES_VOL_FLIGHT = 104
+BYTES_VOL_VERTEX = 216
 GT_C3 = os.path.join(ROOT, "tests", "golden", "c3_gt.npz")
 GT_C3_CPU = os.path.join(ROOT, "tests", "golden", "c3_cpu_gt_tiles.npz")  # make_c3_cpu_gt.py
 
@@ -226,7 +232,7 @@ def main():
                     "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
                     "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
                     "note": "density-grid gathers of k_volpath over the timed wall clock, all ranks"}
-        roofline = volume_roofline(d)
+        roofline = volume_roofline(d, pg, scene, integ, device, a)
     else:
         # §8d's 420 B per segment, split by what each segment does: every segment is traced, escaped
         # ones are not shaded, only recording passes write training records, and only NEE vertices
@@ -374,11 +380,16 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
             "kernels": out}
 
 
-def volume_roofline(d):
-    """k_volpath (C5) roofline from the timed job itself: the volumetric path runs one launch at a time
-    on the context stream, so its HIP-event durations are exact.  Algorithmic bytes = density-grid
-    gathers (8 voxels x 4 B per lookup); the 64 MiB grid stays in the 256 MiB Infinity Cache, so
-    this is an on-die gather rate measured against the HBM peak."""
+def volume_roofline(d, pg=None, scene=None, integ=None, local=0, a=None, spp=64):
+    """C5 roofline.  The volumetric wavefront (default): a calibration context after the timed region
+    (same scene, the job's trained tree, a 64-spp final-render pass, pg_config.kernel_timing) times
+    every free-flight (k_vflight) and interaction (k_vvertex) launch with a HIP event pair on its one
+    stream; algorithmic bytes = density gathers (32 B per trilinear lookup) + the SoA path state each
+    launch moves (BYTES_VOL_FLIGHT / BYTES_VOL_VERTEX per item); the kernel with the most bytes is
+    reported.  With PG_VOL_WAVEFRONT=0: k_volpath from the timed job itself (one launch at a time on
+    the context stream), density gathers only."""
+    if os.environ.get("PG_VOL_WAVEFRONT", "1") != "0" and integ is not None:
+        return wavefront_roofline(pg, scene, integ, local, a, spp)
     ms, launches = d["volume_ms"], max(d["volume_launches"], 1)
     nbytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
@@ -401,6 +412,61 @@ def volume_roofline(d):
             "avg_launch_ms": round(ms / launches, 4),
             "density_lookups_per_launch": int(d["density_lookups"] / launches),
             "measured": "timed job, HIP events around every k_volpath launch (one stream)"}
+
+
+def wavefront_roofline(pg, scene, integ, local, a, spp):
+    from mitsuba_path_guiding_amd.integrator import Device
+    cfg = type(integ.dev.cfg).from_buffer_copy(integ.dev.cfg)  # the job's configuration, stage timing on
+    cfg.kernel_timing = 1
+    dev = Device(cfg)
+    dev.upload(scene)
+    dev.put_sdtree(integ.dev.get_sdtree())
+    s0 = dev.stats()
+    dev.render_pass(spp, 2 ** a.train - 1)
+    s1 = dev.stats()
+    dev.close()
+    d = {k: s1[k] - s0[k] for k in s1}
+    kernels = {
+        "k_vflight": (d["vol_flight_ms"], d["vol_flights"] * BYTES_VOL_FLIGHT + d["vol_flight_lookups"] * BYTES_DENSITY_LOOKUP,
+                      d["vol_flight_launches"], d["vol_flight_lookups"]),
+        "k_vvertex": (d["vol_vertex_ms"], d["vol_vertices"] * BYTES_VOL_VERTEX + d["vol_vertex_lookups"] * BYTES_DENSITY_LOOKUP,
+                      d["vol_vertex_launches"], d["vol_vertex_lookups"]),
+    }
+    measured, source = {}, None
+    pmc = os.path.join(ROOT, "profiles", "pmc_volpath_latest.json")
+    if os.path.exists(pmc):
+        try:
+            pj = json.load(open(pmc))
+            measured = pj.get("kernels", {})
+            source = {"file": "profiles/pmc_volpath_latest.json", "profiled": pj.get("source"), "revision": pj.get("revision")}
+        except (OSError, ValueError):
+            measured = {}
+    out = {}
+    total_ms = sum(v[0] for v in kernels.values()) or 1.0
+    for k, (ms, nbytes, launches, lookups) in kernels.items():
+        e = {"ms": round(ms, 2), "launches": int(launches), "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
+             "density_lookups_per_launch": int(lookups / max(launches, 1)),
+             "avg_launch_ms": round(ms / max(launches, 1), 4), "time_share": round(ms / total_ms, 3),
+             "achieved_gbs": round(nbytes / (ms / 1e3) / 1e9, 2) if ms > 0 else 0.0,
+             "frac": round(nbytes / (ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if ms > 0 else 0.0}
+        m = measured.get(k, {})
+        if m.get("hbm_bytes_per_launch") and launches:
+            e["traffic_bytes_per_launch"] = m["hbm_bytes_per_launch"]
+            e["traffic_over_algorithmic"] = round(m["hbm_bytes_per_launch"] / (nbytes / launches), 3)
+        out[k] = e
+    dom = max(kernels, key=lambda k: kernels[k][1])
+    ms, nbytes, launches, _ = kernels[dom]
+    achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
+    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel": dom,
+            "traffic": out[dom].get("traffic_bytes_per_launch"), "traffic_source": source,
+            "traffic_over_algorithmic": out[dom].get("traffic_over_algorithmic"),
+            "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)), "avg_launch_ms": round(ms / max(launches, 1), 4),
+            "bytes_model": {"k_vflight": f"{BYTES_VOL_FLIGHT} B state per flight + {BYTES_DENSITY_LOOKUP} B per density lookup",
+                            "k_vvertex": f"{BYTES_VOL_VERTEX} B state per interaction + {BYTES_DENSITY_LOOKUP} B per density lookup"},
+            "measured": f"calibration context after the timed region: {scene.width}x{scene.height} x {spp} spp final-render "
+                        "pass with the job's tree, HIP events around every stage launch (one stream)",
+            "kernels": out}
 
 
 def load_gt(path=GT_C3):

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 10
+#define PG_ABI_VERSION 11
 
 typedef int32_t pg_status;
 enum {
@@ -282,6 +282,17 @@ typedef struct pg_stats {
     uint64_t rays_launches;   /* k_rays launches (a bounce's shadow rays + the next bounce's closest hits) */
     uint64_t shadow_launches; /* unfused shadow-ray launches (PG_NO_RAYS_FUSION) */
     uint64_t tail_launches;   /* chunk tails finished in one launch (k_tail) */
+    /* ABI 11: the volumetric wavefront's stages (integrator = volpath, PG_VOL_WAVEFRONT): device time
+     * (HIP events; pg_config.kernel_timing), launches, items processed and density lookups made by the
+     * free-flight launches (k_vflight) and the interaction launches (k_vvertex) */
+    double vol_flight_ms;
+    uint64_t vol_flight_launches;
+    uint64_t vol_flights;
+    uint64_t vol_flight_lookups;
+    double vol_vertex_ms;
+    uint64_t vol_vertex_launches;
+    uint64_t vol_vertices;
+    uint64_t vol_vertex_lookups;
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */

@@ -101,7 +101,11 @@ class pg_stats(C.Structure):
                 ("trace_launches", C.c_uint64), ("stree_nodes", C.c_uint64), ("dtree_nodes", C.c_uint64),
                 ("shade_launches", C.c_uint64), ("volume_ms", C.c_double), ("volume_launches", C.c_uint64),
                 ("density_lookups", C.c_uint64), ("escaped", C.c_uint64), ("rays_ms", C.c_double),
-                ("rays_launches", C.c_uint64), ("shadow_launches", C.c_uint64), ("tail_launches", C.c_uint64)]
+                ("rays_launches", C.c_uint64), ("shadow_launches", C.c_uint64), ("tail_launches", C.c_uint64),
+                # ABI 11: the volumetric wavefront's stages
+                ("vol_flight_ms", C.c_double), ("vol_flight_launches", C.c_uint64), ("vol_flights", C.c_uint64),
+                ("vol_flight_lookups", C.c_uint64), ("vol_vertex_ms", C.c_double),
+                ("vol_vertex_launches", C.c_uint64), ("vol_vertices", C.c_uint64), ("vol_vertex_lookups", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -185,7 +189,7 @@ SIGNATURES = [
 ]
 
 
-PG_ABI_VERSION = 10  # include/pg_capi.h
+PG_ABI_VERSION = 11  # include/pg_capi.h
 PG_COMM_ID_BYTES = 128
 
 

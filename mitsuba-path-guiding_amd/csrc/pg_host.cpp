@@ -181,6 +181,7 @@ struct Ctx {
     DevBuf vw_state, vw_items, vw_counts;
     PinnedBuf vw_host;                  // counter readback
     uint32_t vw_cap = 0;
+    hipEvent_t vw_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // stage timing (kernel_timing)
     uint32_t vol_cap = 0;
     uint32_t num_tris = 0, num_mats = 0;
     uint32_t bvh_top_nodes = 0;  // breadth-first top levels of the binary BVH (staged in LDS by k_trace)
@@ -740,6 +741,8 @@ pg_status pg_destroy(void *ctx) {
     if (!c) return PG_OK;
     (void)hipSetDevice(c->cfg.device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (hipEvent_t &e : c->vw_ev)
+        if (e) (void)hipEventDestroy(e);
     for (Lane &l : c->lanes) {
         if (l.stream) (void)hipStreamSynchronize(l.stream);
         for (auto &pool : l.ev)
@@ -1165,11 +1168,31 @@ pg_status volWavefrontChunk(Ctx *c, const GParams &g, const SceneDev &sc, const 
         HIPC(c, hipMemsetAsync(q[nxt].counts, 0, PG_QSHARDS * 4, c->stream));
         HIPC(c, hipMemsetAsync(q[2 + nxt].counts, 0, PG_QSHARDS * 4, c->stream));
         HIPC(c, hipMemsetAsync(q[4].counts, 0, PG_QSHARDS * 4, c->stream));
+        // per-stage device time (pg_config.kernel_timing): events around each launch, read at the
+        // next iteration's synchronisation
+        const bool evt = c->cfg.kernel_timing != 0;
+        if (evt && !c->vw_ev[0])
+            for (hipEvent_t &e : c->vw_ev) HIPC(c, hipEventCreate(&e));
+        if (evt) HIPC(c, hipEventRecord(c->vw_ev[0], c->stream));
         pg_launch_vol_flight(c->stream, g, v, sd, w, q[cur], f.first, q[4], q[2 + cur]);
+        if (evt) HIPC(c, hipEventRecord(c->vw_ev[1], c->stream));
         // shard bounds without a readback: a medium vertex came from a flight; a surface vertex from a
         // flight or from the previous iteration's interactions; no shard exceeds the queue stride
         const uint32_t mm = f.first, ms = std::min(stride, f.first + su.first);
         pg_launch_vol_vertex(c->stream, g, sc, v, sd, w, q[4], mm, q[2 + cur], ms, q[nxt], q[2 + nxt]);
+        if (evt) {
+            HIPC(c, hipEventRecord(c->vw_ev[2], c->stream));
+            HIPC(c, hipEventSynchronize(c->vw_ev[2]));
+            float a = 0, b = 0;
+            if (f.first) {
+                HIPC(c, hipEventElapsedTime(&a, c->vw_ev[0], c->vw_ev[1]));
+                c->stats.vol_flight_ms += a;
+                c->stats.vol_flight_launches++;
+            }
+            HIPC(c, hipEventElapsedTime(&b, c->vw_ev[1], c->vw_ev[2]));
+            c->stats.vol_vertex_ms += b;
+            c->stats.vol_vertex_launches++;
+        }
         HIPC(c, hipGetLastError());
     }
     return PG_OK;
@@ -1192,8 +1215,8 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
         c->vol_vtx_cap = (uint64_t)want * maxV;
     }
     if (!c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
-    if (!c->vol_work.p) HIPC(c, c->vol_work.alloc(64));
-    HIPC(c, hipMemsetAsync(c->vol_work.p, 0, 64, c->stream));
+    HIPC(c, c->vol_work.alloc(128));  // work counter, then 7 u64 statistics from byte 16
+    HIPC(c, hipMemsetAsync(c->vol_work.p, 0, 128, c->stream));
     GParams g = c->g;
     g.max_depth = c->cfg.max_depth;
     g.rr_depth = c->cfg.rr_depth;
@@ -1279,8 +1302,12 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
         layer += nl;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
-    unsigned long long st[3];
-    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 24, hipMemcpyDeviceToHost));
+    unsigned long long st[7];
+    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 56, hipMemcpyDeviceToHost));
+    c->stats.vol_flights += st[3];
+    c->stats.vol_flight_lookups += st[4];
+    c->stats.vol_vertices += st[5];
+    c->stats.vol_vertex_lookups += st[6];
     c->stats.segments += st[0];
     c->stats.shadow_rays += st[1];
     c->stats.density_lookups += st[2];

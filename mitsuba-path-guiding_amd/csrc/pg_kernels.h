@@ -63,7 +63,8 @@ struct VolDev {
     int32_t grid;              // 1: majorant-grid tracking, 0: the global majorant
     float4 *rad;               // per work item (layer-major: item = layer * npix + lp), radiance
     uint32_t *next;            // work counter (zeroed by the launcher)
-    unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries, [2] density lookups
+    unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries, [2] density lookups;
+                               // wavefront: [3] flights, [4] their lookups, [5] interactions, [6] their lookups
     uint32_t *stack_ovf;       // pg_stack_overflow_words(0) words
     float4 *vtx;               // guided training vertices [max_vertices][vtx_P][PG_VTX_F4] (PathDev::vtx layout)
     uint32_t vtx_P;            // slot stride of vtx (>= items per launch)

@@ -919,6 +919,18 @@ __device__ __forceinline__ void volStats(const VolDev &v, uint32_t segs, uint32_
         atomicAdd(v.stats + 2, s2);
     }
 }
+// wavefront stage counters (VolDev.stats[k], [k + 1]): items processed, density lookups made
+__device__ __forceinline__ void volStageStats(const VolDev &v, int k, uint32_t items, uint32_t lookups) {
+    unsigned long long a = items, b = lookups;
+    for (int off = 32; off > 0; off >>= 1) {
+        a += __shfl_xor(a, off);
+        b += __shfl_xor(b, off);
+    }
+    if ((threadIdx.x & 63) == 0 && (a | b)) {
+        atomicAdd(v.stats + k, a);
+        atomicAdd(v.stats + k + 1, b);
+    }
+}
 // a path that ended: its radiance and training-vertex count (k_film / k_commit), its lookups counted
 __device__ __forceinline__ void volEnd(const VolDev &v, uint32_t slot, const VPath &P, const VRng &rng,
                                        uint32_t &lookups) {
@@ -972,6 +984,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vflight(GParams g, VolDev v, SD
                                                          Queue qs) {
     const uint32_t sh = blockIdx.x & (PG_QSHARDS - 1), rows = gridDim.x / PG_QSHARDS;
     const uint32_t n = qf.counts[sh];
+    uint32_t flights = 0, lookups = 0;
     for (uint32_t base = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
         bool toM = false, toS = false;
@@ -992,6 +1005,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vflight(GParams g, VolDev v, SD
             f3 mp = mk1(0.f);
             toM = volFlight<GUIDED>(v, sd, P, rng, mp);
             toS = !toM;
+            flights++;
+            lookups += rng.lookups - r.w;
             w.r[slot] = make_uint4(rng.key, rng.sample, rng.dim, rng.lookups);
             if (wT) w.T[slot] = f4(P.T, w.T[slot].w);
             if (toM) w.mp[slot] = f4(mp, 0.0f);
@@ -999,6 +1014,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vflight(GParams g, VolDev v, SD
         waveAppend(toM, slot, qm.items + (size_t)sh * qm.stride, qm.counts + sh);
         waveAppend(toS, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
     }
+    volStageStats(v, 3, flights, lookups);
 }
 
 // interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices
@@ -1014,7 +1030,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vvertex(GParams g
     const Queue &q = medium ? qm : qs;
     const uint32_t sh = b & (PG_QSHARDS - 1), rows = nb / PG_QSHARDS;
     const uint32_t n = q.counts[sh];
-    uint32_t segs = 0, shadows = 0, lookups = 0;
+    uint32_t segs = 0, shadows = 0, lookups = 0, vertices = 0, vlookups = 0;
     for (uint32_t base = (b / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
         bool toF = false, toS = false;
@@ -1024,8 +1040,11 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vvertex(GParams g
             VPath P;
             VRng rng;
             loadPath(w, slot, P, rng);
+            const uint32_t l0 = rng.lookups;
             const bool alive = medium ? volMedium<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, xyz(w.mp[slot]))
                                       : volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+            vertices++;
+            vlookups += rng.lookups - l0;
             if (alive && volDepthOk(g, P)) {
                 storePath(w, slot, P, rng);
                 toF = P.medium >= 0;
@@ -1038,6 +1057,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vvertex(GParams g
         waveAppend(toS, slot, ns.items + (size_t)sh * ns.stride, ns.counts + sh);
     }
     volStats(v, segs, shadows, lookups);
+    volStageStats(v, 5, vertices, vlookups);
 }
 
 // the chunk's last paths: each thread runs one to its end (paths of `qf` start with their flight, those

@@ -104,7 +104,8 @@ def main(src, dst_prefix):
         out["kernels"][k] = e
     os.makedirs(os.path.dirname(dst_prefix) or ".", exist_ok=True)
     json.dump(out, open(dst_prefix + "_pmc.json", "w"), indent=1)
-    latest = "pmc_volpath_latest.json" if "k_volpath" in out["kernels"] else "pmc_latest.json"  # read by bench.py
+    vol = "k_volpath" in out["kernels"] or "k_vflight" in out["kernels"]
+    latest = "pmc_volpath_latest.json" if vol else "pmc_latest.json"  # read by bench.py
     json.dump(out, open(os.path.join(os.path.dirname(dst_prefix), latest), "w"), indent=1)
     with open(dst_prefix + "_kernel_stats.csv", "w") as f:
         f.write(open(os.path.join(src, "trace", "run_kernel_stats.csv")).read())
