@@ -1108,12 +1108,12 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
 // (read per chunk, so tests can compare both in one process)
 bool volWavefront() {
     const char *e = std::getenv("PG_VOL_WAVEFRONT");
-    return e ? std::atoi(e) != 0 : true;
+    return e && *e ? std::atoi(e) != 0 : true;
 }
 // below this many live paths a chunk's remaining paths finish in one k_vtail launch (PG_VOL_TAIL_PATHS)
 uint32_t volTailPaths() {
     const char *e = std::getenv("PG_VOL_TAIL_PATHS");
-    return e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 16;
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 16;
 }
 
 // One chunk (np pixels from pb, nl layers) through the wavefront: camera rays, then per iteration the

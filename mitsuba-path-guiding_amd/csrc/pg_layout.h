@@ -151,7 +151,7 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 // plane = origin + q * 2^e, rounded outward (floor / ceil, checked against the fp32 reconstruction);
 // an empty slot has lo = 255, hi = 0 (an inverted box) and the PG_QNODE_EMPTY ref
 #ifndef PG_QNODE_QUANT
-#define PG_QNODE_QUANT 0
+#define PG_QNODE_QUANT 1
 #endif
 #if PG_QNODE_QUANT
 #define PG_QNODE_F4 4
