@@ -979,9 +979,16 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
 }
 
 // free flights: medium interaction -> med, the flight reached its surface (or left the medium) -> surf
+// waves per SIMD the stage kernels are built for (A/B knobs; 0 = the compiler's choice)
+#ifndef PG_VFLIGHT_WAVES
+#define PG_VFLIGHT_WAVES 0
+#endif
+#ifndef PG_VVERTEX_WAVES
+#define PG_VVERTEX_WAVES PG_VOL_WAVES
+#endif
 template <bool GUIDED>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm,
-                                                         Queue qs) {
+__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_VFLIGHT_WAVES > 0 ? PG_VFLIGHT_WAVES : 1)))
+void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm, Queue qs) {
     const uint32_t sh = blockIdx.x & (PG_QSHARDS - 1), rows = gridDim.x / PG_QSHARDS;
     const uint32_t n = qf.counts[sh];
     uint32_t flights = 0, lookups = 0;
@@ -1019,7 +1026,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vflight(GParams g, VolDev v, SD
 
 // interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices
 template <bool GUIDED>
-__global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
+__global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
                                                                        VolWave w, Queue qm, Queue qs, uint32_t mblocks,
                                                                        Queue nf, Queue ns) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];

@@ -19,7 +19,7 @@ import subprocess
 import sys
 from collections import defaultdict
 
-PATH_KERNELS = ("k_trace", "k_shade", "k_shadow", "k_shade_all", "k_rays")
+PATH_KERNELS = ("k_trace", "k_shade", "k_shadow", "k_shade_all", "k_rays", "k_vflight", "k_vvertex")
 
 
 def base_name(n):
@@ -31,7 +31,11 @@ def rows_of(path):
 
 
 def calibration_stream(rows):
+    """the stream of the last k_trace launch (surface path) or, for the volumetric wavefront, of the last
+    k_vflight launch: bench.py's calibration context runs after the timed region"""
     tr = [r for r in rows if base_name(r["Kernel_Name"]) == "k_trace" and "Stream_Id" in r]
+    if not tr:
+        tr = [r for r in rows if base_name(r["Kernel_Name"]) == "k_vflight" and "Stream_Id" in r]
     if not tr:
         return None
     return max(tr, key=lambda r: int(r.get("Start_Timestamp", r.get("Dispatch_Id", 0))))["Stream_Id"]
