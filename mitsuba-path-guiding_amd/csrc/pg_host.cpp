@@ -1113,7 +1113,7 @@ bool volWavefront() {
 // below this many live paths a chunk's remaining paths finish in one k_vtail launch (PG_VOL_TAIL_PATHS)
 uint32_t volTailPaths() {
     const char *e = std::getenv("PG_VOL_TAIL_PATHS");
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 16;
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 18;
 }
 
 // One chunk (np pixels from pb, nl layers) through the wavefront: camera rays, then per iteration the

@@ -66,7 +66,7 @@ static_assert(sizeof(GEnv) == 128, "GEnv layout");
 // bx * by bricks per z layer; inside a brick x, then y, then z): the 2x2x2 corners of a trilinear
 // lookup then touch ~2.3 cache lines instead of 4 rows of the linear layout.
 #ifndef PG_MAJORANT_CELL
-#define PG_MAJORANT_CELL 8  // voxels per majorant cell and axis (oracle: orc_medium.h kCell)
+#define PG_MAJORANT_CELL 16  // voxels per majorant cell and axis (oracle: orc_medium.h kCell)
 #endif
 #ifndef PG_DENSITY_CORNERS
 #define PG_DENSITY_CORNERS 1  // corner-packed density (below); 0: linear voxels (or bricks)

@@ -77,7 +77,7 @@ struct Medium {
     // over [c * kCell - 1, (c + 1) * kCell + 1] (every trilinear lookup whose base voxel lies in the
     // cell, with one voxel of margin for the rounding of the traversal's cell boundaries)
 #ifndef ORC_MAJORANT_CELL
-#define ORC_MAJORANT_CELL 8  // = the kernels' PG_MAJORANT_CELL (ASan runs build other sizes, tools/oracle_asan.sh)
+#define ORC_MAJORANT_CELL 16  // = the kernels' PG_MAJORANT_CELL (ASan runs build other sizes, tools/oracle_asan.sh)
 #endif
     static constexpr int kCell = ORC_MAJORANT_CELL;
     int mres[3] = {1, 1, 1};

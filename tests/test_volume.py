@@ -161,7 +161,9 @@ def test_majorant_grid_matches_global(pg, O):
     assert abs(pa - pb) < 5 * se
     ha, hb = a[:, 0] > 0.5, b[:, 0] > 0.5
     assert stats.ks_2samp(a[ha, 1], b[hb, 1]).pvalue > 1e-3
-    assert b[:, 2].mean() < 0.5 * a[:, 2].mean()  # empty space is skipped
+    # empty space is skipped: 16^3-voxel cells (pg_layout.h PG_MAJORANT_CELL) draw ~0.7x the global
+    # majorant's numbers here (8^3 cells: ~0.5x, but twice the DDA steps)
+    assert b[:, 2].mean() < 0.8 * a[:, 2].mean()
     ta = osc.medium_sample(0, rays, keys, transmittance=True)[:, 0]
     tb = osc.medium_sample(0, rays, keys, transmittance=True, grid=True)[:, 0]
     se = np.sqrt(ta.var() / n + tb.var() / n)

@@ -75,12 +75,12 @@ def main():
         integ = GuidedPathTracer(p, device=0)
         integ.preprocess(scene)
         tbest, img = float("inf"), None
-        for _ in range(3):  # the first run warms up
+        for run in range(3):  # the first run warms up
             integ.reset()
             t = time.perf_counter()
-            rgbw, _ = integ.render(spp)
+            rgbw, _sq = integ.render(spp)
             el = time.perf_counter() - t
-            if img is not None or _ > 0:
+            if run > 0:
                 tbest = min(tbest, el)
             img = bench.image(rgbw)
         integ.postprocess()
