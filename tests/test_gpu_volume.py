@@ -275,3 +275,39 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
         if base[2] is not None:
             assert np.array_equal(o[2], base[2])
         assert o[3] == base[3], (o[3], base[3])
+
+
+def test_volpath_wavefront_tile_shard(pg):
+    """C5's multi-GPU form (image tiles sharded over ranks, building statistics all-
+    reduced before each refit) on the volumetric wavefront, emulated with two shard contexts on one
+    GPU: every training iteration's summed statistics give the single-rank tree bit for bit, and the
+    two ranks' final films add up to the single-rank film bit for bit (the random streams are keyed by
+    the global pixel)."""
+    sc = pg.scenes.smoke(96, 96, res=48)
+    cfg = dict(guiding=1, s_tree_threshold=300.0)
+    full = make_dev(pg, sc, **cfg)
+    parts = [make_dev(pg, sc, rank=r, world_size=2, **cfg) for r in range(2)]
+    off = 0
+    for it in range(3):
+        full.render_pass(2 ** it, off, True)
+        full.splat_local()
+        full.refit(it)
+        for d in parts:
+            d.render_pass(2 ** it, off, True)
+            d.splat_local()
+        total = parts[0].get_tree_stats() + parts[1].get_tree_stats()
+        for d in parts:
+            d.put_tree_stats(total)
+            d.refit(it)
+        off += 2 ** it
+    t = full.get_sdtree()
+    assert all(np.array_equal(d.get_sdtree(), t) for d in parts)
+    for d in parts + [full]:
+        d.reset_film()
+        d.render_pass(8, off)
+    f = full.read_film()[0]
+    p0, p1 = parts[0].read_film()[0], parts[1].read_film()[0]
+    assert np.array_equal(p0 + p1, f)
+    assert ((p0[..., 3] > 0) ^ (p1[..., 3] > 0)).all()
+    for d in parts + [full]:
+        d.close()
