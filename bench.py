@@ -504,7 +504,7 @@ def quality_block(pg, scene, final, job_s, a):
            "guided": errors(image(final), gt)}
     dev = Device(pg.capi.default_config())
     dev.upload(scene)
-    dev.render_pass(a.spp, 0)  # warm-up + equal-spp image (independent of the guided streams' offsets)
+    dev.render_pass(a.spp, 0)  # warm-up + equal-spp image (sample indices 0.., the guided final pass 31..: paired)
     ug = image(dev.read_film()[0])
     best = float("inf")  # best of two warm runs, like the timed job's steady state
     for _ in range(2):

@@ -6,7 +6,9 @@ tracer at the spp each guided job's wall clock buys, and compares relMSE (bench.
 exposed to mean 1; trim999; dark median) against the 65,536-spp ground truth.  The per-pixel breakdown
 splits the summed relMSE of each image into pixel classes -- the ground truth's dark pixels (the camera
 room lit through the door gap) and bright pixels, and the glint pixels (the 0.1 % of pixels with the
-largest unguided equal-spp error) -- so the classes where guiding wins and loses are visible.
+largest unguided equal-spp error) -- so the classes where guiding wins and loses are visible.  The glint class is chosen on the unguided
+image, so the class ratios are selection-biased; tools/outlier_paths_c3.py has the
+unbiased per-sample decomposition.
 
   python tools/guiding_breakdown_c3.py OUT.json
 """
