@@ -158,6 +158,23 @@ struct Lane {
     uint32_t b = 0, bound = 0, n = 0, pb = 0, np = 0, nl = 0, layer0 = 0;
 };
 
+// One in-flight chunk of the volumetric wavefront (renderVolpath): its own stream, SoA path state
+// (VolWave, 7 x 16 B per slot), five sharded queues (flight / surface for two iterations, medium
+// vertices) with their counters and host copy, per-item radiance and stack overflow ring.  Several
+// lanes overlap one chunk's sparse late iterations and k_vtail with the next chunk's full ones.
+struct VolLane {
+    hipStream_t stream = nullptr;
+    hipEvent_t ready = nullptr;  // the counters' host copy landed
+    DevBuf state, items, counts, rad, ovf;
+    PinnedBuf host;
+    uint32_t cap = 0;
+    // the chunk in flight
+    bool active = false, waved = false;  // waved: its paths are done, its film waits for its turn
+    uint32_t chunk = 0, pb = 0, np = 0, nl = 0, sample_base = 0;
+    int it = 0;
+    EventPair span;                      // chunk start .. film (pg_stats volume_ms; moved to the pass's list)
+};
+
 struct Ctx {
     pg_config cfg{};
     std::string err;
@@ -176,11 +193,8 @@ struct Ctx {
     DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
     DevBuf vol_vtx;                     // guided volpath training vertices (48 B each)
     uint64_t vol_vtx_cap = 0;
-    // volumetric wavefront (PG_VOL_WAVEFRONT): SoA path state (VolWave, 7 x 16 B per slot) and five
-    // sharded queues (flight / surface for two iterations, medium vertices) + their counters
-    DevBuf vw_state, vw_items, vw_counts;
-    PinnedBuf vw_host;                  // counter readback
-    uint32_t vw_cap = 0;
+    // volumetric wavefront (PG_VOL_WAVEFRONT) lanes
+    VolLane vlanes[PG_MAX_LANES];
     hipEvent_t vw_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // stage timing (kernel_timing)
     uint32_t vol_cap = 0;
     uint32_t num_tris = 0, num_mats = 0;
@@ -743,6 +757,11 @@ pg_status pg_destroy(void *ctx) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (hipEvent_t &e : c->vw_ev)
         if (e) (void)hipEventDestroy(e);
+    for (VolLane &l : c->vlanes) {
+        if (l.stream) (void)hipStreamSynchronize(l.stream);
+        if (l.ready) (void)hipEventDestroy(l.ready);
+        if (l.stream) (void)hipStreamDestroy(l.stream);
+    }
     for (Lane &l : c->lanes) {
         if (l.stream) (void)hipStreamSynchronize(l.stream);
         for (auto &pool : l.ev)
@@ -1116,72 +1135,180 @@ uint32_t volTailPaths() {
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 18;
 }
 
-// One chunk (np pixels from pb, nl layers) through the wavefront: camera rays, then per iteration the
+// chunks of a volumetric pass: np pixels from pb, nl sample layers from sample_base
+struct VChunk {
+    uint32_t pb, np, nl, sample_base;
+};
+// volumetric wavefront lanes in flight: pg_config.path_lanes, default 2 (C5: 310 / 347 / 330 Mpaths/s with
+// 1 / 2 / 3 lanes, profiles/r04q_vol_lanes/); PG_VOL_LANES overrides (A/B)
+int volLanes(const Ctx *c) {
+    const char *e = std::getenv("PG_VOL_LANES");
+    const int n = e && *e ? std::atoi(e) : (c->cfg.path_lanes ? c->cfg.path_lanes : 2);
+    return std::max(1, std::min(PG_MAX_LANES, n));
+}
+
+// The chunks of one pass through the wavefront: per chunk the camera rays, then per iteration the
 // free flights and the interactions, until at most volTailPaths() paths live; the tail finishes them.
-// The host reads the queue counters once per iteration (grid sizes; the kernels read the counts).
-pg_status volWavefrontChunk(Ctx *c, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                            uint32_t pb, uint32_t np, uint32_t nl, uint32_t sample_base) {
-    const uint32_t n = np * nl;
-    const uint32_t stride = pg_queue_stride(n);
-    if (c->vw_cap < n) {
-        HIPC(c, c->vw_state.alloc((size_t)n * 16 * 7));
-        HIPC(c, c->vw_items.alloc((size_t)stride * PG_QSHARDS * 4 * 5));
-        c->vw_cap = n;
-    }
-    HIPC(c, c->vw_counts.alloc((size_t)PG_QSHARDS * 4 * 5));
-    HIPC(c, c->vw_host.reserve((size_t)PG_QSHARDS * 4 * 5));
-    float4 *st = c->vw_state.as<float4>();
-    const size_t cap = c->vw_cap;
-    VolWave w{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
-              reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap};
-    // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices
-    const size_t qstride = (size_t)pg_queue_stride(c->vw_cap) * PG_QSHARDS;
-    Queue q[5];
-    for (int k = 0; k < 5; ++k)
-        q[k] = Queue{c->vw_items.as<uint32_t>() + k * qstride, c->vw_counts.as<uint32_t>() + k * PG_QSHARDS, stride};
-    uint32_t *hc = reinterpret_cast<uint32_t *>(c->vw_host.p);
-    auto maxShard = [&](int k) {
-        uint32_t m = 0, t = 0;
-        for (int i = 0; i < PG_QSHARDS; ++i) {
-            m = std::max(m, hc[k * PG_QSHARDS + i]);
-            t += hc[k * PG_QSHARDS + i];
+// The host reads a chunk's queue counters once per iteration (grid sizes; the kernels read the counts)
+// and advances whichever lane's counters have landed, so one chunk's readback and sparse last
+// iterations overlap another's full ones.  Films (and record commits) run in chunk order, so every
+// pixel's float sums are those of one lane.  Recording passes and per-stage timing use one lane.
+pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                           const PathDev &pv, const std::vector<VChunk> &chunks, uint32_t want, int maxV,
+                           std::vector<EventPair> &evs) {
+    const bool evt = c->cfg.kernel_timing != 0;
+    const int nl = (g.record || evt) ? 1 : std::min<int>(volLanes(c), (int)chunks.size());
+    const size_t cbytes = (size_t)PG_QSHARDS * 4 * 5;
+    HIPC(c, hipEventRecord(c->pass_start, c->stream));  // lanes start after the context stream's work
+    for (int li = 0; li < nl; ++li) {
+        VolLane &l = c->vlanes[li];
+        if (!l.stream) {
+            HIPC(c, hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
+            HIPC(c, hipEventCreateWithFlags(&l.ready, hipEventDisableTiming));
         }
-        return std::make_pair(m, t);
-    };
-    HIPC(c, hipMemsetAsync(c->vw_counts.p, 0, (size_t)PG_QSHARDS * 4 * 5, c->stream));
-    pg_launch_vol_camera(c->stream, g, sc, v, w, c->d_local_pixels.as<uint32_t>(), pb, np, nl, sample_base, q[0], q[2]);
-    HIPC(c, hipGetLastError());
+        if (l.cap < want) {
+            HIPC(c, l.state.alloc((size_t)want * 16 * 7));
+            HIPC(c, l.items.alloc((size_t)pg_queue_stride(want) * PG_QSHARDS * 4 * 5));
+            HIPC(c, l.rad.alloc((size_t)want * 16));
+            l.cap = want;
+        }
+        HIPC(c, l.counts.alloc(cbytes));
+        HIPC(c, l.host.reserve(cbytes));
+        if (!l.ovf.p) HIPC(c, l.ovf.alloc(pg_stack_overflow_words(0) * 4));
+        HIPC(c, hipStreamWaitEvent(l.stream, c->pass_start, 0));
+        l.active = l.waved = false;
+    }
+    HIPC(c, hipEventRecord(c->film_order, c->stream));
     const uint32_t tail = volTailPaths();
-    for (int it = 0;; ++it) {
-        const int cur = it & 1, nxt = cur ^ 1;
-        HIPC(c, hipMemcpyAsync(hc, c->vw_counts.p, (size_t)PG_QSHARDS * 4 * 5, hipMemcpyDeviceToHost, c->stream));
-        HIPC(c, hipStreamSynchronize(c->stream));
+    uint32_t next = 0, filmNext = 0;
+    auto views = [&](VolLane &l, VolDev &lv, VolWave &w, Queue *q) {
+        lv = v;
+        lv.rad = l.rad.as<float4>();
+        lv.stack_ovf = l.ovf.as<uint32_t>();
+        float4 *st = l.state.as<float4>();
+        const size_t cap = l.cap;
+        w = VolWave{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
+                    reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap};
+        // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices
+        const size_t qstride = (size_t)pg_queue_stride(l.cap) * PG_QSHARDS;
+        const uint32_t stride = pg_queue_stride(l.np * l.nl);
+        for (int k = 0; k < 5; ++k)
+            q[k] = Queue{l.items.as<uint32_t>() + k * qstride, l.counts.as<uint32_t>() + k * PG_QSHARDS, stride};
+    };
+    auto readback = [&](VolLane &l) -> pg_status {
+        HIPC(c, hipMemcpyAsync(l.host.p, l.counts.p, cbytes, hipMemcpyDeviceToHost, l.stream));
+        HIPC(c, hipEventRecord(l.ready, l.stream));
+        return PG_OK;
+    };
+    auto start = [&](VolLane &l) -> pg_status {
+        if (next >= chunks.size()) {
+            l.active = false;
+            return PG_OK;
+        }
+        const VChunk &ch = chunks[next];
+        l.chunk = next++;
+        l.pb = ch.pb, l.np = ch.np, l.nl = ch.nl, l.sample_base = ch.sample_base;
+        l.it = 0;
+        l.active = true;
+        l.waved = false;
+        HIPC(c, hipEventCreate(&l.span.a));
+        HIPC(c, hipEventCreate(&l.span.b));
+        HIPC(c, hipEventRecord(l.span.a, l.stream));
+        VolDev lv;
+        VolWave w;
+        Queue q[5];
+        views(l, lv, w, q);
+        HIPC(c, hipMemsetAsync(l.counts.p, 0, cbytes, l.stream));
+        pg_launch_vol_camera(l.stream, g, sc, lv, w, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, l.sample_base,
+                             q[0], q[2]);
+        HIPC(c, hipGetLastError());
+        return readback(l);
+    };
+    // record commit + film of a chunk whose paths are done (its turn in chunk order), then its next chunk
+    auto finish = [&](VolLane &l) -> pg_status {
+        HIPC(c, hipStreamWaitEvent(l.stream, c->film_order, 0));
+        PathDev lp = pv;
+        lp.rad = l.rad.as<float4>();
+        if (g.record) {
+            const uint64_t items = (uint64_t)l.np * l.nl, add = items * (uint64_t)maxV;
+            if (c->rec_bound + add > c->rec_capacity) {
+                unsigned long long rc = 0;
+                HIPC(c, hipStreamSynchronize(l.stream));
+                HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
+                c->stats.records += rc - c->rec_host_count;
+                c->rec_host_count = c->rec_bound = rc;
+                pg_status st;
+                if ((st = ensureRecords(c, rc + add))) return st;
+            }
+            c->rec_bound += add;
+            pg_launch_commit(l.stream, lp, (uint32_t)items, maxV, c->records.as<pg_record>(),
+                             c->rec_count.as<unsigned long long>(), c->rec_capacity, 0);
+        }
+        pg_launch_film(l.stream, g, sc, lp, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
+                       c->film_sq.as<float4>());
+        HIPC(c, hipGetLastError());
+        HIPC(c, hipEventRecord(c->film_order, l.stream));
+        HIPC(c, hipEventRecord(l.span.b, l.stream));
+        evs.push_back(l.span);
+        l.span = EventPair{};
+        c->stats.paths += (uint64_t)l.np * l.nl;
+        return start(l);
+    };
+    // one iteration of lane l (its counters are on the host)
+    auto advance = [&](VolLane &l) -> pg_status {
         if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+        const uint32_t *hc = reinterpret_cast<const uint32_t *>(l.host.p);
+        auto maxShard = [&](int k) {
+            uint32_t m = 0, t = 0;
+            for (int i = 0; i < PG_QSHARDS; ++i) {
+                m = std::max(m, hc[k * PG_QSHARDS + i]);
+                t += hc[k * PG_QSHARDS + i];
+            }
+            return std::make_pair(m, t);
+        };
+        VolDev lv;
+        VolWave w;
+        Queue q[5];
+        views(l, lv, w, q);
+        const int cur = l.it & 1, nxt = cur ^ 1;
         const auto f = maxShard(cur), su = maxShard(2 + cur);
-        if (f.second + su.second == 0) break;
         if (f.second + su.second <= tail) {
-            pg_launch_vol_tail(c->stream, g, sc, v, sd, w, q[cur], f.first, q[2 + cur], su.first);
-            HIPC(c, hipGetLastError());
-            break;
+            if (f.second + su.second) {
+                pg_launch_vol_tail(l.stream, g, sc, lv, sd, w, q[cur], f.first, q[2 + cur], su.first);
+                HIPC(c, hipGetLastError());
+            }
+            l.waved = true;
+            // finish this chunk and every waiting one whose turn comes after it
+            for (bool progress = true; progress;) {
+                progress = false;
+                for (int k = 0; k < nl; ++k) {
+                    VolLane &o = c->vlanes[k];
+                    if (o.active && o.waved && o.chunk == filmNext) {
+                        ++filmNext;
+                        pg_status st = finish(o);
+                        if (st) return st;
+                        progress = true;
+                    }
+                }
+            }
+            return PG_OK;
         }
         // the next iteration's output queues and the medium queue start empty
-        HIPC(c, hipMemsetAsync(q[nxt].counts, 0, PG_QSHARDS * 4, c->stream));
-        HIPC(c, hipMemsetAsync(q[2 + nxt].counts, 0, PG_QSHARDS * 4, c->stream));
-        HIPC(c, hipMemsetAsync(q[4].counts, 0, PG_QSHARDS * 4, c->stream));
-        // per-stage device time (pg_config.kernel_timing): events around each launch, read at the
-        // next iteration's synchronisation
-        const bool evt = c->cfg.kernel_timing != 0;
+        HIPC(c, hipMemsetAsync(q[nxt].counts, 0, PG_QSHARDS * 4, l.stream));
+        HIPC(c, hipMemsetAsync(q[2 + nxt].counts, 0, PG_QSHARDS * 4, l.stream));
+        HIPC(c, hipMemsetAsync(q[4].counts, 0, PG_QSHARDS * 4, l.stream));
+        // per-stage device time (pg_config.kernel_timing, one lane): events around each launch
         if (evt && !c->vw_ev[0])
             for (hipEvent_t &e : c->vw_ev) HIPC(c, hipEventCreate(&e));
-        if (evt) HIPC(c, hipEventRecord(c->vw_ev[0], c->stream));
-        pg_launch_vol_flight(c->stream, g, v, sd, w, q[cur], f.first, q[4], q[2 + cur]);
-        if (evt) HIPC(c, hipEventRecord(c->vw_ev[1], c->stream));
+        if (evt) HIPC(c, hipEventRecord(c->vw_ev[0], l.stream));
+        pg_launch_vol_flight(l.stream, g, lv, sd, w, q[cur], f.first, q[4], q[2 + cur]);
+        if (evt) HIPC(c, hipEventRecord(c->vw_ev[1], l.stream));
         // shard bounds without a readback: a medium vertex came from a flight; a surface vertex from a
         // flight or from the previous iteration's interactions; no shard exceeds the queue stride
-        const uint32_t mm = f.first, ms = std::min(stride, f.first + su.first);
-        pg_launch_vol_vertex(c->stream, g, sc, v, sd, w, q[4], mm, q[2 + cur], ms, q[nxt], q[2 + nxt]);
+        const uint32_t mm = f.first, ms = std::min(q[0].stride, f.first + su.first);
+        pg_launch_vol_vertex(l.stream, g, sc, lv, sd, w, q[4], mm, q[2 + cur], ms, q[nxt], q[2 + nxt]);
         if (evt) {
-            HIPC(c, hipEventRecord(c->vw_ev[2], c->stream));
+            HIPC(c, hipEventRecord(c->vw_ev[2], l.stream));
             HIPC(c, hipEventSynchronize(c->vw_ev[2]));
             float a = 0, b = 0;
             if (f.first) {
@@ -1194,7 +1321,31 @@ pg_status volWavefrontChunk(Ctx *c, const GParams &g, const SceneDev &sc, const 
             c->stats.vol_vertex_launches++;
         }
         HIPC(c, hipGetLastError());
+        ++l.it;
+        return readback(l);
+    };
+    pg_status s;
+    for (int li = 0; li < nl; ++li)
+        if ((s = start(c->vlanes[li]))) return s;
+    // advance whichever lane has its counters first
+    for (uint32_t rr = 0;; ++rr) {
+        int active = 0, picked = -1;
+        for (int k = 0; k < nl; ++k) {
+            VolLane &l = c->vlanes[(rr + k) % nl];
+            if (!l.active) continue;
+            ++active;
+            if (l.waved) continue;  // waiting for an earlier chunk's film
+            const hipError_t qr = hipEventQuery(l.ready);
+            if (qr == hipSuccess) {
+                picked = (int)((rr + k) % nl);
+                break;
+            }
+            if (qr != hipErrorNotReady) HIPC(c, qr);
+        }
+        if (!active) break;
+        if (picked >= 0 && (s = advance(c->vlanes[picked]))) return s;
     }
+    for (int li = 0; li < nl; ++li) HIPC(c, hipStreamSynchronize(c->vlanes[li].stream));
     return PG_OK;
 }
 
@@ -1205,7 +1356,8 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     // against 2^22, profiles/r01h_c5_*.log); 50 GB of training vertices when guided
     const uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
     const uint32_t want = (uint32_t)std::min<uint64_t>((uint64_t)npix * spp, cap);
-    if (c->vol_cap < want) {
+    const bool wave = volWavefront();  // the wavefront's lanes hold their own radiance and overflow rings
+    if (!wave && c->vol_cap < want) {
         HIPC(c, c->vol_rad.alloc((size_t)want * 16));
         c->vol_cap = want;
     }
@@ -1214,7 +1366,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
         HIPC(c, c->vol_vtx.alloc((size_t)want * maxV * 16 * PG_VTX_F4));
         c->vol_vtx_cap = (uint64_t)want * maxV;
     }
-    if (!c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
+    if (!wave && !c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
     HIPC(c, c->vol_work.alloc(128));  // work counter, then 7 u64 statistics from byte 16
     HIPC(c, hipMemsetAsync(c->vol_work.p, 0, 128, c->stream));
     GParams g = c->g;
@@ -1260,46 +1412,47 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     pv.vtxP = want;
     pv.pinfo = nullptr;  // k_commit reads the vertex count from rad[item].w
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix), pixPer = std::min(npix, want);
-    std::vector<EventPair> evs;
+    std::vector<VChunk> chunks;
     for (uint32_t layer = 0; layer < spp;) {
         const uint32_t nl = npix > want ? 1 : std::min(layersPer, spp - layer);
-        for (uint32_t pb = 0; pb < npix; pb += pixPer) {
-            if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
-            const uint32_t np = std::min(pixPer, npix - pb);
-            EventPair e;
-            HIPC(c, hipEventCreate(&e.a));
-            HIPC(c, hipEventCreate(&e.b));
-            evs.push_back(e);
-            HIPC(c, hipEventRecord(e.a, c->stream));
-            if (volWavefront()) {
-                pg_status ws = volWavefrontChunk(c, g, sc, v, sd, pb, np, nl, sample_offset + layer);
-                if (ws) return ws;
-            } else {
-                pg_launch_volpath(c->stream, g, sc, v, sd, c->d_local_pixels.as<uint32_t>(), pb, np, nl,
-                                  sample_offset + layer);
-            }
-            HIPC(c, hipEventRecord(e.b, c->stream));
-            if (g.record) {
-                const uint64_t items = (uint64_t)np * nl, add = items * (uint64_t)maxV;
-                if (c->rec_bound + add > c->rec_capacity) {
-                    unsigned long long rc = 0;
-                    HIPC(c, hipStreamSynchronize(c->stream));
-                    HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
-                    c->stats.records += rc - c->rec_host_count;
-                    c->rec_host_count = c->rec_bound = rc;
-                    pg_status st;
-                    if ((st = ensureRecords(c, rc + add))) return st;
-                }
-                c->rec_bound += add;
-                pg_launch_commit(c->stream, pv, (uint32_t)items, maxV, c->records.as<pg_record>(),
-                                 c->rec_count.as<unsigned long long>(), c->rec_capacity, 0);
-            }
-            pg_launch_film(c->stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
-                           c->film_sq.as<float4>());
-            HIPC(c, hipGetLastError());
-            c->stats.paths += (uint64_t)np * nl;
-        }
+        for (uint32_t pb = 0; pb < npix; pb += pixPer)
+            chunks.push_back(VChunk{pb, std::min(pixPer, npix - pb), nl, sample_offset + layer});
         layer += nl;
+    }
+    std::vector<EventPair> evs;
+    if (wave) {
+        pg_status ws = volWavefrontPass(c, g, sc, v, sd, pv, chunks, want, maxV, evs);
+        if (ws) return ws;
+    }
+    for (size_t ci = 0; !wave && ci < chunks.size(); ++ci) {  // the persistent megakernel
+        if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
+        const uint32_t pb = chunks[ci].pb, np = chunks[ci].np, nl = chunks[ci].nl;
+        EventPair e;
+        HIPC(c, hipEventCreate(&e.a));
+        HIPC(c, hipEventCreate(&e.b));
+        evs.push_back(e);
+        HIPC(c, hipEventRecord(e.a, c->stream));
+        pg_launch_volpath(c->stream, g, sc, v, sd, c->d_local_pixels.as<uint32_t>(), pb, np, nl, chunks[ci].sample_base);
+        HIPC(c, hipEventRecord(e.b, c->stream));
+        if (g.record) {
+            const uint64_t items = (uint64_t)np * nl, add = items * (uint64_t)maxV;
+            if (c->rec_bound + add > c->rec_capacity) {
+                unsigned long long rc = 0;
+                HIPC(c, hipStreamSynchronize(c->stream));
+                HIPC(c, hipMemcpy(&rc, c->rec_count.p, 8, hipMemcpyDeviceToHost));
+                c->stats.records += rc - c->rec_host_count;
+                c->rec_host_count = c->rec_bound = rc;
+                pg_status st;
+                if ((st = ensureRecords(c, rc + add))) return st;
+            }
+            c->rec_bound += add;
+            pg_launch_commit(c->stream, pv, (uint32_t)items, maxV, c->records.as<pg_record>(),
+                             c->rec_count.as<unsigned long long>(), c->rec_capacity, 0);
+        }
+        pg_launch_film(c->stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), pb, np, nl, c->film.as<float4>(),
+                       c->film_sq.as<float4>());
+        HIPC(c, hipGetLastError());
+        c->stats.paths += (uint64_t)np * nl;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
     unsigned long long st[7];
