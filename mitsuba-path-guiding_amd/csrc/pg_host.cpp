@@ -166,6 +166,7 @@ struct VolLane {
     hipStream_t stream = nullptr;
     hipEvent_t ready = nullptr;  // the counters' host copy landed
     DevBuf state, items, counts, rad, ovf;
+    DevBuf keys, sorted, hist;  // flight order keys of both flight queues, a sorted copy, histograms (PG_VOL_SORT)
     PinnedBuf host;
     uint32_t cap = 0;
     // the chunk in flight
@@ -1139,6 +1140,12 @@ uint32_t volTailPaths() {
 struct VChunk {
     uint32_t pb, np, nl, sample_base;
 };
+// flight queues sorted by the 16^3 cell of the flight's start before k_vflight (PG_VOL_SORT, A/B): shards
+// of at least this many flights
+uint32_t volSortMin() {
+    const char *e = std::getenv("PG_VOL_SORT");
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+}
 // volumetric wavefront lanes in flight: pg_config.path_lanes, default 2 (C5: 310 / 347 / 330 Mpaths/s with
 // 1 / 2 / 3 lanes, profiles/r04q_vol_lanes/); PG_VOL_LANES overrides (A/B)
 int volLanes(const Ctx *c) {
@@ -1159,6 +1166,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
     const bool evt = c->cfg.kernel_timing != 0;
     const int nl = (g.record || evt) ? 1 : std::min<int>(volLanes(c), (int)chunks.size());
     const size_t cbytes = (size_t)PG_QSHARDS * 4 * 5;
+    const uint32_t sortMin = volSortMin();
     HIPC(c, hipEventRecord(c->pass_start, c->stream));  // lanes start after the context stream's work
     for (int li = 0; li < nl; ++li) {
         VolLane &l = c->vlanes[li];
@@ -1174,6 +1182,12 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         }
         HIPC(c, l.counts.alloc(cbytes));
         HIPC(c, l.host.reserve(cbytes));
+        if (sortMin) {
+            const size_t qstride = (size_t)pg_queue_stride(l.cap) * PG_QSHARDS;
+            HIPC(c, l.keys.alloc(qstride * 2 * 2));
+            HIPC(c, l.sorted.alloc(qstride * 4));
+            HIPC(c, l.hist.alloc((size_t)PG_QSHARDS * PG_RAY_SORT_BINS * 4));
+        }
         if (!l.ovf.p) HIPC(c, l.ovf.alloc(pg_stack_overflow_words(0) * 4));
         HIPC(c, hipStreamWaitEvent(l.stream, c->pass_start, 0));
         l.active = l.waved = false;
@@ -1194,6 +1208,8 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         const uint32_t stride = pg_queue_stride(l.np * l.nl);
         for (int k = 0; k < 5; ++k)
             q[k] = Queue{l.items.as<uint32_t>() + k * qstride, l.counts.as<uint32_t>() + k * PG_QSHARDS, stride};
+        if (sortMin)
+            for (int k = 0; k < 2; ++k) q[k].keys = l.keys.as<uint16_t>() + k * qstride;
     };
     auto readback = [&](VolLane &l) -> pg_status {
         HIPC(c, hipMemcpyAsync(l.host.p, l.counts.p, cbytes, hipMemcpyDeviceToHost, l.stream));
@@ -1300,8 +1316,13 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         // per-stage device time (pg_config.kernel_timing, one lane): events around each launch
         if (evt && !c->vw_ev[0])
             for (hipEvent_t &e : c->vw_ev) HIPC(c, hipEventCreate(&e));
+        Queue fq = q[cur];
+        if (sortMin && f.first >= sortMin) {  // the flights in cell order (same shards and counts)
+            pg_launch_ray_sort(l.stream, fq, f.first, l.sorted.as<uint32_t>(), l.hist.as<uint32_t>());
+            fq.items = l.sorted.as<uint32_t>();
+        }
         if (evt) HIPC(c, hipEventRecord(c->vw_ev[0], l.stream));
-        pg_launch_vol_flight(l.stream, g, lv, sd, w, q[cur], f.first, q[4], q[2 + cur]);
+        pg_launch_vol_flight(l.stream, g, lv, sd, w, fq, f.first, q[4], q[2 + cur]);
         if (evt) HIPC(c, hipEventRecord(c->vw_ev[1], l.stream));
         // shard bounds without a readback: a medium vertex came from a flight; a surface vertex from a
         // flight or from the previous iteration's interactions; no shard exceeds the queue stride

@@ -269,22 +269,6 @@ __device__ __forceinline__ uint32_t rayOrderKey(const SDDev &sd, f3 o, f3 d) {
     const uint32_t oct = (d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u);
     return (oct << 9) | m;
 }
-// waveAppend that also stores each entry's ray order key
-__device__ __forceinline__ void waveAppendKey(bool pred, uint32_t value, uint16_t key, uint32_t *q, uint16_t *keys,
-                                              uint32_t *count) {
-    unsigned long long m = __ballot(pred);
-    if (m == 0) return;
-    int lane = threadIdx.x & 63;
-    int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (pred) {
-        const uint32_t at = base + __popcll(m & ((1ull << lane) - 1ull));
-        q[at] = value;
-        keys[at] = key;
-    }
-}
 
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
 // MODEL >= 0 compiles only that BSDF model's code (material-class queues filled by k_trace);

@@ -543,6 +543,22 @@ __device__ __forceinline__ void waveAppend(bool pred, uint32_t value, uint32_t *
         q[base + __popcll(below)] = value;
     }
 }
+// waveAppend that also stores each entry's order key (counting-sorted by pg_launch_ray_sort)
+__device__ __forceinline__ void waveAppendKey(bool pred, uint32_t value, uint16_t key, uint32_t *q, uint16_t *keys,
+                                              uint32_t *count) {
+    unsigned long long m = __ballot(pred);
+    if (m == 0) return;
+    int lane = threadIdx.x & 63;
+    int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = __shfl(base, leader);
+    if (pred) {
+        const uint32_t at = base + __popcll(m & ((1ull << lane) - 1ull));
+        q[at] = value;
+        keys[at] = key;
+    }
+}
 
 __device__ __forceinline__ SDView sdv(const SDDev &sd) {
     return SDView{sd.snodes, sd.meta, sd.qsum, sd.qchild, sd.jump, make_float3(sd.lo[0], sd.lo[1], sd.lo[2]),

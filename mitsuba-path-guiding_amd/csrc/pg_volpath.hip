@@ -939,6 +939,34 @@ __device__ __forceinline__ void volEnd(const VolDev &v, uint32_t slot, const VPa
 }
 __device__ __forceinline__ uint32_t slotShard(uint32_t slot) { return (slot >> 6) & (PG_QSHARDS - 1); }
 
+// flight order key (PG_VOL_SORT): the Morton code of the 16^3 cell of the medium's box that holds o, so
+// a sorted flight queue walks the density grid region by region (12 bits: PG_RAY_SORT_BINS);
+// PG_VOL_SORT_KEY = 1: the direction octant, then an 8^3 cell (A/B)
+#ifndef PG_VOL_SORT_KEY
+#define PG_VOL_SORT_KEY 0
+#endif
+__device__ __forceinline__ uint16_t flightKey(const VolDev &v, int m, f3 o, f3 d) {
+    const GMedium &M = v.media[m];
+    constexpr int bits = PG_VOL_SORT_KEY ? 3 : 4;
+    constexpr float res = (float)(1 << bits);
+    const float fx = (o.x - M.lo[0]) / (M.hi[0] - M.lo[0]), fy = (o.y - M.lo[1]) / (M.hi[1] - M.lo[1]),
+                fz = (o.z - M.lo[2]) / (M.hi[2] - M.lo[2]);
+    const uint32_t cx = (uint32_t)fminf(fmaxf(fx * res, 0.0f), res - 1.0f), cy = (uint32_t)fminf(fmaxf(fy * res, 0.0f), res - 1.0f),
+                   cz = (uint32_t)fminf(fmaxf(fz * res, 0.0f), res - 1.0f);
+    uint32_t k = 0;
+    for (int b = 0; b < bits; ++b)
+        k |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
+    if (PG_VOL_SORT_KEY) k |= ((d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u)) << 9;
+    return (uint16_t)k;
+}
+// append to a flight queue, with the order key when the queue carries keys
+__device__ __forceinline__ void flightAppend(bool pred, uint32_t slot, uint16_t key, const Queue &q, uint32_t sh) {
+    if (q.keys)
+        waveAppendKey(pred, slot, key, q.items + (size_t)sh * q.stride, q.keys + (size_t)sh * q.stride, q.counts + sh);
+    else
+        waveAppend(pred, slot, q.items + (size_t)sh * q.stride, q.counts + sh);
+}
+
 }  // namespace
 
 // ---- volumetric wavefront (the volpath loop as a wavefront of path states) -----
@@ -959,6 +987,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
     for (uint32_t base = blockIdx.x * TRACE_BLOCK; base < n; base += gridDim.x * TRACE_BLOCK) {
         const uint32_t slot = base + threadIdx.x;
         bool toF = false, toS = false;
+        uint16_t key = 0;
         if (slot < n) {
             VPath P;
             VRng rng;
@@ -969,10 +998,11 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
                 storePath(w, slot, P, rng);
                 toF = P.medium >= 0;
                 toS = !toF;
+                if (toF && qf.keys) key = flightKey(v, P.medium, P.o, P.d);
             }
         }
         const uint32_t sh = slotShard(base + (threadIdx.x & ~63u));
-        waveAppend(toF, slot, qf.items + (size_t)sh * qf.stride, qf.counts + sh);
+        flightAppend(toF, slot, key, qf, sh);
         waveAppend(toS, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
     }
     volStats(v, segs, 0, lookups);
@@ -1042,6 +1072,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
         const uint32_t i = base + threadIdx.x;
         bool toF = false, toS = false;
         uint32_t slot = 0;
+        uint16_t key = 0;
         if (i < n) {
             slot = q.items[(size_t)sh * q.stride + i];
             VPath P;
@@ -1056,11 +1087,12 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
                 storePath(w, slot, P, rng);
                 toF = P.medium >= 0;
                 toS = !toF;
+                if (toF && nf.keys) key = flightKey(v, P.medium, P.o, P.d);
             } else {
                 volEnd(v, slot, P, rng, lookups);
             }
         }
-        waveAppend(toF, slot, nf.items + (size_t)sh * nf.stride, nf.counts + sh);
+        flightAppend(toF, slot, key, nf, sh);
         waveAppend(toS, slot, ns.items + (size_t)sh * ns.stride, ns.counts + sh);
     }
     volStats(v, segs, shadows, lookups);

@@ -242,7 +242,9 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
     megakernel's volFlight / volMedium / volSurface on the same random streams, each path in its own
     slot: films, sums of squares, training records (through the trees) and path counters must be the
     megakernel's bit for bit -- whether every iteration runs as launches (tail threshold 0), the
-    default tail threshold, or the tail kernel takes the whole chunk after the camera rays."""
+    default tail threshold, or the tail kernel takes the whole chunk after the camera rays; with one,
+    two (default) or three lanes of chunks in flight (films in chunk order), and with the flight
+    queues sorted by cell (PG_VOL_SORT)."""
     from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer, ProgressiveVolumetricPathTracer
     sc = pg.scenes.smoke(96, 96, res=48)
     props = {"trainingIterations": 3, "samplesPerProgression": 8}
@@ -253,12 +255,15 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
     if case == "guided_exact_chunked":
         props.update({"exactMis": True, "maxPathsInFlight": 4096 + 512})
     out = []
-    for wf, tail in (("0", None), ("1", "0"), ("1", None), ("1", str(1 << 30))):
+    runs = (("0", None, None, None), ("1", "0", None, None), ("1", None, None, None), ("1", str(1 << 30), None, None),
+            ("1", None, "1", None), ("1", "0", "3", "1"))
+    for wf, tail, lanes, sort in runs:
         monkeypatch.setenv("PG_VOL_WAVEFRONT", wf)
-        if tail is None:
-            monkeypatch.delenv("PG_VOL_TAIL_PATHS", raising=False)
-        else:
-            monkeypatch.setenv("PG_VOL_TAIL_PATHS", tail)
+        for var, val in (("PG_VOL_TAIL_PATHS", tail), ("PG_VOL_LANES", lanes), ("PG_VOL_SORT", sort)):
+            if val is None:
+                monkeypatch.delenv(var, raising=False)
+            else:
+                monkeypatch.setenv(var, val)
         t = Tracer(dict(props))
         if case == "plain_global":  # the reference's single majorant (heterogeneous.cpp:589-660)
             t.cfg.volume_majorant = pg.capi.PG_MAJORANT_GLOBAL
