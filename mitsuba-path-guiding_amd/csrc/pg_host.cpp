@@ -1140,11 +1140,12 @@ uint32_t volTailPaths() {
 struct VChunk {
     uint32_t pb, np, nl, sample_base;
 };
-// flight queues sorted by the 16^3 cell of the flight's start before k_vflight (PG_VOL_SORT, A/B): shards
-// of at least this many flights
+// flight queues sorted by the 16^3 cell of the flight's start before k_vflight, for shards of at least this
+// many flights (PG_VOL_SORT overrides; 0 = off): C5 351.5 / 350.0 against 346.3 / 345.7 Mpaths/s unsorted;
+// an octant + 8^3-cell key measured the same (profiles/r04s_vol_sort/, r04t_vol_ab/)
 uint32_t volSortMin() {
     const char *e = std::getenv("PG_VOL_SORT");
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 4096u;
 }
 // volumetric wavefront lanes in flight: pg_config.path_lanes, default 2 (C5: 310 / 347 / 330 Mpaths/s with
 // 1 / 2 / 3 lanes, profiles/r04q_vol_lanes/); PG_VOL_LANES overrides (A/B)

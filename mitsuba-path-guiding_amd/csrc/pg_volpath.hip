@@ -1009,9 +1009,11 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
 }
 
 // free flights: medium interaction -> med, the flight reached its surface (or left the medium) -> surf
-// waves per SIMD the stage kernels are built for (A/B knobs; 0 = the compiler's choice)
+// waves per SIMD the stage kernels are built for (A/B knobs; 0 = the compiler's choice).  k_vflight at 4:
+// 128 VGPRs without scratch (the compiler's 132 gave 3 waves); C5 363.6 / 363.4 against 351.9 / 350.5
+// Mpaths/s (profiles/r04t_vol_ab/)
 #ifndef PG_VFLIGHT_WAVES
-#define PG_VFLIGHT_WAVES 0
+#define PG_VFLIGHT_WAVES 4
 #endif
 #ifndef PG_VVERTEX_WAVES
 #define PG_VVERTEX_WAVES PG_VOL_WAVES
