@@ -453,12 +453,17 @@ def wavefront_roofline(pg, scene, integ, local, a, spp):
         if m.get("hbm_bytes_per_launch") and launches:
             e["traffic_bytes_per_launch"] = m["hbm_bytes_per_launch"]
             e["traffic_over_algorithmic"] = round(m["hbm_bytes_per_launch"] / (nbytes / launches), 3)
+        cal = m.get("calibration_avg_ns")
+        if cal and launches:  # the profiled calibration context's average duration (rocprofv3 kernel trace)
+            e["avg_launch_ms_rocprof"] = round(cal / 1e6, 4)
+            e["frac_rocprof"] = round(nbytes / launches / (cal / 1e9) / 1e9 / HBM_PEAK_GBS, 5)
         out[k] = e
     dom = max(kernels, key=lambda k: kernels[k][1])
     ms, nbytes, launches, _ = kernels[dom]
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
     return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel": dom,
+            "frac_rocprof": out[dom].get("frac_rocprof"), "avg_launch_ms_rocprof": out[dom].get("avg_launch_ms_rocprof"),
             "traffic": out[dom].get("traffic_bytes_per_launch"), "traffic_source": source,
             "traffic_over_algorithmic": out[dom].get("traffic_over_algorithmic"),
             "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)), "avg_launch_ms": round(ms / max(launches, 1), 4),
@@ -648,6 +653,15 @@ def cpu_baseline(pg, scene, integ, final, a):
                          "pixels_diverged_frac": round(float((rel > 1e-3).mean()), 6),
                          "note": "GPU and CPU final renders with one tree and the same RNG streams; a path whose "
                                  "fp32 libm/FMA rounding flips one branch diverges"}
+    # single-sample glints set the figure: the worst pixel's share and the figure without
+    # the worst 3 pixels
+    d2 = ((g - s) ** 2).sum(-1)
+    keep = np.ones(len(d2), bool)
+    keep[np.argsort(d2)[::-1][:3]] = False
+    rmse["same_tree"].update({
+        "worst_pixel_share_of_squared_difference": round(float(d2.max() / max(d2.sum(), 1e-30)), 4),
+        "gpu_vs_cpu_relative_rmse_without_worst_3_pixels": round(float(
+            np.sqrt(np.mean((g[keep] - s[keep]) ** 2)) / max(float(np.sqrt(np.mean(s[keep] ** 2))), 1e-12)), 6)})
     if gt is not None:
         # the paired form of the RMSE ratio: both renders draw the same paths, so only the diverged
         # pixels separate them and the jackknife error over the tiles is small
