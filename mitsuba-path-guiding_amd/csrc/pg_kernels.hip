@@ -598,7 +598,10 @@ __global__ __launch_bounds__(SHADE_BLOCK) void k_shade(GParams g, SceneDev sc, S
 struct ShadeRanges {
     uint32_t end[PG_NUM_CLASSES];
 };
-__global__ __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void k_shade_all(
+#ifndef PG_SHADE_WAVES
+#define PG_SHADE_WAVES 4
+#endif
+__global__ __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_SHADE_WAVES))) void k_shade_all(
     GParams g, SceneDev sc, SDDev sd, PathDev p, ClassQueues in, Queue out, Queue shq, ShadeRanges r) {
     static_assert(PG_NUM_CLASSES == 6, "class ranges");
     const uint32_t b = blockIdx.x;
