@@ -1319,7 +1319,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
             for (hipEvent_t &e : c->vw_ev) HIPC(c, hipEventCreate(&e));
         Queue fq = q[cur];
         if (sortMin && f.first >= sortMin) {  // the flights in cell order (same shards and counts)
-            pg_launch_ray_sort(l.stream, fq, f.first, l.sorted.as<uint32_t>(), l.hist.as<uint32_t>());
+            pg_launch_ray_sort(l.stream, fq, f.first, l.sorted.as<uint32_t>(), l.hist.as<uint32_t>(), PG_VOL_SORT_BINS);
             fq.items = l.sorted.as<uint32_t>();
         }
         if (evt) HIPC(c, hipEventRecord(c->vw_ev[0], l.stream));

@@ -132,7 +132,8 @@ void pg_launch_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const S
                     uint32_t max_shard, unsigned long long *stats);
 // counting sort of every shard of `q` by its keys into sorted_items (same shard layout and counts):
 // histogram, per-shard scan, scatter; hist: PG_QSHARDS * PG_RAY_SORT_BINS u32 of scratch (zeroed here)
-void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist);
+void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist,
+                        uint32_t bins = PG_RAY_SORT_BINS);  // bins: PG_RAY_SORT_BINS or 512
 // aov_albedo / aov_normal: per-pixel feature sums, read when p.aov is set
 void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels,
                     uint32_t pix_begin, uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq,

@@ -618,26 +618,28 @@ __global__ __launch_bounds__(SHADE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_
 // follows LDS/global atomics (nondeterministic), which is harmless: every path is a pure function of
 // (pixel, sample), whatever the order its bounces are traced in.
 #define RSORT_TILE 4096  // queue entries per block (256 threads x 16)
+template <uint32_t BINS>
 __global__ __launch_bounds__(256) void k_rsort_hist(Queue q, uint32_t *hist) {
-    __shared__ uint32_t h[PG_RAY_SORT_BINS];
+    __shared__ uint32_t h[BINS];
     const uint32_t s = blockIdx.x & (PG_QSHARDS - 1), tile = blockIdx.x / PG_QSHARDS;
     const uint32_t n = q.counts[s], b0 = tile * RSORT_TILE;
     if (b0 >= n) return;
-    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256) h[k] = 0;
+    for (uint32_t k = threadIdx.x; k < BINS; k += 256) h[k] = 0;
     __syncthreads();
     const uint16_t *keys = q.keys + (size_t)s * q.stride;
     const uint32_t e = min(n, b0 + RSORT_TILE);
     for (uint32_t i = b0 + threadIdx.x; i < e; i += 256) atomicAdd(&h[keys[i]], 1u);
     __syncthreads();
-    uint32_t *g = hist + (size_t)s * PG_RAY_SORT_BINS;
-    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256)
+    uint32_t *g = hist + (size_t)s * BINS;
+    for (uint32_t k = threadIdx.x; k < BINS; k += 256)
         if (h[k]) atomicAdd(&g[k], h[k]);
 }
 // exclusive scan of every shard's histogram in place (one block per shard)
+template <uint32_t BINS>
 __global__ __launch_bounds__(256) void k_rsort_scan(uint32_t *hist) {
     __shared__ uint32_t part[256];
-    uint32_t *g = hist + (size_t)blockIdx.x * PG_RAY_SORT_BINS;
-    constexpr int PER = PG_RAY_SORT_BINS / 256;
+    uint32_t *g = hist + (size_t)blockIdx.x * BINS;
+    constexpr int PER = BINS / 256;
     uint32_t v[PER], sum = 0;
     for (int j = 0; j < PER; ++j) {
         v[j] = g[threadIdx.x * PER + j];
@@ -657,12 +659,13 @@ __global__ __launch_bounds__(256) void k_rsort_scan(uint32_t *hist) {
         run += v[j];
     }
 }
+template <uint32_t BINS>
 __global__ __launch_bounds__(256) void k_rsort_scatter(Queue q, uint32_t *hist, uint32_t *sorted) {
-    __shared__ uint32_t cnt[PG_RAY_SORT_BINS];
+    __shared__ uint32_t cnt[BINS];
     const uint32_t s = blockIdx.x & (PG_QSHARDS - 1), tile = blockIdx.x / PG_QSHARDS;
     const uint32_t n = q.counts[s], b0 = tile * RSORT_TILE;
     if (b0 >= n) return;
-    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256) cnt[k] = 0;
+    for (uint32_t k = threadIdx.x; k < BINS; k += 256) cnt[k] = 0;
     __syncthreads();
     const uint16_t *keys = q.keys + (size_t)s * q.stride;
     const uint32_t *items = q.items + (size_t)s * q.stride;
@@ -676,8 +679,8 @@ __global__ __launch_bounds__(256) void k_rsort_scatter(Queue q, uint32_t *hist, 
         rank[j] = i < e ? atomicAdd(&cnt[key[j]], 1u) : 0u;
     }
     __syncthreads();
-    uint32_t *g = hist + (size_t)s * PG_RAY_SORT_BINS;
-    for (uint32_t k = threadIdx.x; k < PG_RAY_SORT_BINS; k += 256)  // this tile's range of every key
+    uint32_t *g = hist + (size_t)s * BINS;
+    for (uint32_t k = threadIdx.x; k < BINS; k += 256)  // this tile's range of every key
         if (cnt[k]) cnt[k] = atomicAdd(&g[k], cnt[k]);
     __syncthreads();
     uint32_t *out = sorted + (size_t)s * q.stride;
@@ -1286,13 +1289,19 @@ void pg_launch_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const S
     if (sc.env) hipLaunchKernelGGL(k_tail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, sd, p, q, stats);
     else hipLaunchKernelGGL(k_tail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, sd, p, q, stats);
 }
-void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist) {
-    if (!max_shard) return;
-    (void)hipMemsetAsync(hist, 0, (size_t)PG_QSHARDS * PG_RAY_SORT_BINS * 4, s);
+template <uint32_t BINS>
+static void raySort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist) {
+    (void)hipMemsetAsync(hist, 0, (size_t)PG_QSHARDS * BINS * 4, s);
     const dim3 grid(PG_QSHARDS * blocks(max_shard, RSORT_TILE));
-    hipLaunchKernelGGL(k_rsort_hist, grid, dim3(256), 0, s, q, hist);
-    hipLaunchKernelGGL(k_rsort_scan, dim3(PG_QSHARDS), dim3(256), 0, s, hist);
-    hipLaunchKernelGGL(k_rsort_scatter, grid, dim3(256), 0, s, q, hist, sorted_items);
+    hipLaunchKernelGGL(k_rsort_hist<BINS>, grid, dim3(256), 0, s, q, hist);
+    hipLaunchKernelGGL(k_rsort_scan<BINS>, dim3(PG_QSHARDS), dim3(256), 0, s, hist);
+    hipLaunchKernelGGL(k_rsort_scatter<BINS>, grid, dim3(256), 0, s, q, hist, sorted_items);
+}
+void pg_launch_ray_sort(hipStream_t s, Queue q, uint32_t max_shard, uint32_t *sorted_items, uint32_t *hist,
+                        uint32_t bins) {
+    if (!max_shard) return;
+    if (bins == 512) raySort<512>(s, q, max_shard, sorted_items, hist);
+    else raySort<PG_RAY_SORT_BINS>(s, q, max_shard, sorted_items, hist);
 }
 void pg_launch_film(hipStream_t s, const GParams &g, const SceneDev &sc, const PathDev &p, const uint32_t *local_pixels, uint32_t pix_begin,
                     uint32_t npix, uint32_t nlayers, float4 *film_rgbw, float4 *film_sumsq, float4 *aov_albedo,

@@ -114,6 +114,13 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 #define PG_TRIACCEL 1
 #endif
 
+// Volumetric flight order key (pg_volpath.hip flightKey): 0 = 16^3 cells (4096 sort bins), 1 = direction
+// octant + 8^3 cells (4096), 2 = 8^3 cells (512 bins: an eighth of the counting sort's per-tile atomics)
+#ifndef PG_VOL_SORT_KEY
+#define PG_VOL_SORT_KEY 2
+#endif
+#define PG_VOL_SORT_BINS (PG_VOL_SORT_KEY == 2 ? 512u : 4096u)
+
 // Per-triangle shading record (5 x float4 = 80 B), indexed by BVH-order triangle id:
 //   [0] p0.xyz, bits(material | (emitter + 1) << 16)
 //   [1] p1.xyz, n2.z

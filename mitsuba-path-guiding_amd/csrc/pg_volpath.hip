@@ -939,15 +939,12 @@ __device__ __forceinline__ void volEnd(const VolDev &v, uint32_t slot, const VPa
 }
 __device__ __forceinline__ uint32_t slotShard(uint32_t slot) { return (slot >> 6) & (PG_QSHARDS - 1); }
 
-// flight order key (PG_VOL_SORT): the Morton code of the 16^3 cell of the medium's box that holds o, so
-// a sorted flight queue walks the density grid region by region (12 bits: PG_RAY_SORT_BINS);
-// PG_VOL_SORT_KEY = 1: the direction octant, then an 8^3 cell (A/B)
-#ifndef PG_VOL_SORT_KEY
-#define PG_VOL_SORT_KEY 0
-#endif
+// flight order key (PG_VOL_SORT; pg_layout.h PG_VOL_SORT_KEY): the Morton code of the cell of the medium's
+// box that holds o -- 8^3 cells (9 bits, 512 bins) or 16^3 (12 bits), or the direction octant and an
+// 8^3 cell -- so a sorted flight queue walks the density grid region by region
 __device__ __forceinline__ uint16_t flightKey(const VolDev &v, int m, f3 o, f3 d) {
     const GMedium &M = v.media[m];
-    constexpr int bits = PG_VOL_SORT_KEY ? 3 : 4;
+    constexpr int bits = PG_VOL_SORT_KEY == 0 ? 4 : 3;
     constexpr float res = (float)(1 << bits);
     const float fx = (o.x - M.lo[0]) / (M.hi[0] - M.lo[0]), fy = (o.y - M.lo[1]) / (M.hi[1] - M.lo[1]),
                 fz = (o.z - M.lo[2]) / (M.hi[2] - M.lo[2]);
@@ -956,7 +953,7 @@ __device__ __forceinline__ uint16_t flightKey(const VolDev &v, int m, f3 o, f3 d
     uint32_t k = 0;
     for (int b = 0; b < bits; ++b)
         k |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
-    if (PG_VOL_SORT_KEY) k |= ((d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u)) << 9;
+    if (PG_VOL_SORT_KEY == 1) k |= ((d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u)) << 9;
     return (uint16_t)k;
 }
 // append to a flight queue, with the order key when the queue carries keys
