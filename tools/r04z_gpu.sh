@@ -4,11 +4,11 @@
 # suite, smoke() and both bench lines at this revision.  usage: PG_REVISION=<hash> tools/r04z_gpu.sh
 set -o pipefail
 cd "$(dirname "$0")/.."
-O=gpurun_out/r04z
+O=gpurun_out/${CHECKPOINT:-r04z}
 mkdir -p $O
-timeout -k 10 420 bash tools/profile.sh gpurun_out/prof_r04z_c3 && python tools/pmc_summary.py gpurun_out/prof_r04z_c3 $O/c3 > $O/c3_summary.txt 2>&1 || { echo "c3 profile failed"; exit 1; }
+timeout -k 10 420 bash tools/profile.sh gpurun_out/prof_${CHECKPOINT:-r04z}_c3 && python tools/pmc_summary.py gpurun_out/prof_${CHECKPOINT:-r04z}_c3 $O/c3 > $O/c3_summary.txt 2>&1 || { echo "c3 profile failed"; exit 1; }
 cp $O/pmc_latest.json profiles/pmc_latest.json
-timeout -k 10 420 bash tools/profile.sh gpurun_out/prof_r04z_c5 --scene smoke && python tools/pmc_summary.py gpurun_out/prof_r04z_c5 $O/c5 > $O/c5_summary.txt 2>&1 || { echo "c5 profile failed"; exit 1; }
+timeout -k 10 420 bash tools/profile.sh gpurun_out/prof_${CHECKPOINT:-r04z}_c5 --scene smoke && python tools/pmc_summary.py gpurun_out/prof_${CHECKPOINT:-r04z}_c5 $O/c5 > $O/c5_summary.txt 2>&1 || { echo "c5 profile failed"; exit 1; }
 cp $O/pmc_volpath_latest.json profiles/pmc_volpath_latest.json
 head -8 $O/c3_summary.txt $O/c5_summary.txt
 timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 250 --timeout-method thread > $O/gpu_tests.log 2>&1; s=$?; grep -E "passed|failed|FAILED" $O/gpu_tests.log | head; [ $s -eq 0 ] || exit 1
