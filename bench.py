@@ -224,14 +224,18 @@ def main():
     # ---- §8d pipeline figure over the timed wall clock
     d = {k: s1[k] - s0[k] for k in s1}
     if world > 1:
-        for k in ("segments", "escaped", "records", "shadow_rays", "density_lookups"):
+        for k in ("segments", "escaped", "records", "shadow_rays", "density_lookups", "vol_flights", "vol_vertices"):
             d[k] = int(D.sum_over_ranks(d[k], on_dev))
     if vol:
-        pipe_bytes = d["density_lookups"] * BYTES_DENSITY_LOOKUP
+        # density gathers (every lookup: k_vcam / k_vflight / k_vvertex / k_vtail, or k_volpath) plus the
+        # wavefront's state traffic per flight and interaction (0 with the megakernel, PG_VOL_WAVEFRONT=0)
+        pipe_bytes = (d["density_lookups"] * BYTES_DENSITY_LOOKUP + d.get("vol_flights", 0) * BYTES_VOL_FLIGHT +
+                      d.get("vol_vertices", 0) * BYTES_VOL_VERTEX)
         pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
                     "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
                     "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
-                    "note": "density-grid gathers of k_volpath over the timed wall clock, all ranks"}
+                    "note": "density-grid gathers plus the wavefront stages' path-state bytes (bytes_model) over "
+                            "the timed wall clock, all ranks"}
         roofline = volume_roofline(d, pg, scene, integ, device, a)
     else:
         # §8d's 420 B per segment, split by what each segment does: every segment is traced, escaped
