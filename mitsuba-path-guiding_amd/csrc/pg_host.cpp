@@ -1160,12 +1160,17 @@ int volLanes(const Ctx *c) {
 // The host reads a chunk's queue counters once per iteration (grid sizes; the kernels read the counts)
 // and advances whichever lane's counters have landed, so one chunk's readback and sparse last
 // iterations overlap another's full ones.  Films (and record commits) run in chunk order, so every
-// pixel's float sums are those of one lane.  Recording passes and per-stage timing use one lane.
+// pixel's float sums are those of one lane.  Recording passes use two lanes (each with its own region of
+// training vertices), per-stage timing one.
 pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                            const PathDev &pv, const std::vector<VChunk> &chunks, uint32_t want, int maxV,
-                           std::vector<EventPair> &evs) {
+                           uint32_t vtxLanes, std::vector<EventPair> &evs) {
     const bool evt = c->cfg.kernel_timing != 0;
-    const int nl = (g.record || evt) ? 1 : std::min<int>(volLanes(c), (int)chunks.size());
+    const int nl = evt ? 1 : std::min<int>(g.record ? (int)vtxLanes : volLanes(c), (int)chunks.size());
+    // training vertices of lane li (recording passes): region li of vtxLanes, want items each
+    auto laneVtx = [&](const VolLane &l) -> float4 * {
+        return v.vtx ? v.vtx + (size_t)(&l - c->vlanes) * want * (size_t)maxV * PG_VTX_F4 : nullptr;
+    };
     const size_t cbytes = (size_t)PG_QSHARDS * 4 * 5;
     const uint32_t sortMin = volSortMin();
     HIPC(c, hipEventRecord(c->pass_start, c->stream));  // lanes start after the context stream's work
@@ -1200,6 +1205,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         lv = v;
         lv.rad = l.rad.as<float4>();
         lv.stack_ovf = l.ovf.as<uint32_t>();
+        lv.vtx = laneVtx(l);
         float4 *st = l.state.as<float4>();
         const size_t cap = l.cap;
         w = VolWave{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
@@ -1246,6 +1252,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         HIPC(c, hipStreamWaitEvent(l.stream, c->film_order, 0));
         PathDev lp = pv;
         lp.rad = l.rad.as<float4>();
+        lp.vtx = laneVtx(l);
         if (g.record) {
             const uint64_t items = (uint64_t)l.np * l.nl, add = items * (uint64_t)maxV;
             if (c->rec_bound + add > c->rec_capacity) {
@@ -1377,16 +1384,24 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     // 2^25 items per launch: fewer persistent-kernel tails (C5 guided: 177.8 -> 189.8 Mpaths/s
     // against 2^22, profiles/r01h_c5_*.log); 50 GB of training vertices when guided
     const uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
-    const uint32_t want = (uint32_t)std::min<uint64_t>((uint64_t)npix * spp, cap);
+    const uint64_t total = (uint64_t)npix * spp;
+    uint32_t want = (uint32_t)std::min<uint64_t>(total, cap);
     const bool wave = volWavefront();  // the wavefront's lanes hold their own radiance and overflow rings
+    const int maxV = std::min(std::max(c->cfg.record_max_vertices, 0), 64);
+    // a recording pass through the wavefront runs as (at least) two chunks on two lanes, each lane with
+    // its own region of training vertices (indexed by item within the chunk): the same vertex memory as
+    // one chunk of the whole pass
+    const char *rl = std::getenv("PG_VOL_REC_LANES");  // 1: one lane (A/B)
+    const uint32_t vtxLanes = (wave && rec && maxV > 0 && !c->cfg.kernel_timing && volLanes(c) >= 2 && total > 1 &&
+                               !(rl && std::atoi(rl) == 1)) ? 2u : 1u;
+    if (vtxLanes == 2) want = (uint32_t)std::min<uint64_t>(want, (total + 1) / 2);
     if (!wave && c->vol_cap < want) {
         HIPC(c, c->vol_rad.alloc((size_t)want * 16));
         c->vol_cap = want;
     }
-    const int maxV = std::min(std::max(c->cfg.record_max_vertices, 0), 64);
-    if (rec && maxV > 0 && c->vol_vtx_cap < (uint64_t)want * maxV) {
-        HIPC(c, c->vol_vtx.alloc((size_t)want * maxV * 16 * PG_VTX_F4));
-        c->vol_vtx_cap = (uint64_t)want * maxV;
+    if (rec && maxV > 0 && c->vol_vtx_cap < (uint64_t)want * maxV * vtxLanes) {
+        HIPC(c, c->vol_vtx.alloc((size_t)want * maxV * vtxLanes * 16 * PG_VTX_F4));
+        c->vol_vtx_cap = (uint64_t)want * maxV * vtxLanes;
     }
     if (!wave && !c->vol_ovf.p) HIPC(c, c->vol_ovf.alloc(pg_stack_overflow_words(0) * 4));
     HIPC(c, c->vol_work.alloc(128));  // work counter, then 7 u64 statistics from byte 16
@@ -1443,7 +1458,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     }
     std::vector<EventPair> evs;
     if (wave) {
-        pg_status ws = volWavefrontPass(c, g, sc, v, sd, pv, chunks, want, maxV, evs);
+        pg_status ws = volWavefrontPass(c, g, sc, v, sd, pv, chunks, want, maxV, vtxLanes, evs);
         if (ws) return ws;
     }
     for (size_t ci = 0; !wave && ci < chunks.size(); ++ci) {  // the persistent megakernel
