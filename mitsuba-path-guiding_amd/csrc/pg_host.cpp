@@ -1171,7 +1171,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
     auto laneVtx = [&](const VolLane &l) -> float4 * {
         return v.vtx ? v.vtx + (size_t)(&l - c->vlanes) * want * (size_t)maxV * PG_VTX_F4 : nullptr;
     };
-    const size_t cbytes = (size_t)PG_QSHARDS * 4 * 5;
+    const size_t cbytes = (size_t)PG_QSHARDS * 4 * 7;
     const uint32_t sortMin = volSortMin();
     HIPC(c, hipEventRecord(c->pass_start, c->stream));  // lanes start after the context stream's work
     for (int li = 0; li < nl; ++li) {
@@ -1182,7 +1182,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         }
         if (l.cap < want) {
             HIPC(c, l.state.alloc((size_t)want * 16 * 7));
-            HIPC(c, l.items.alloc((size_t)pg_queue_stride(want) * PG_QSHARDS * 4 * 5));
+            HIPC(c, l.items.alloc((size_t)pg_queue_stride(want) * PG_QSHARDS * 4 * 7));
             HIPC(c, l.rad.alloc((size_t)want * 16));
             l.cap = want;
         }
@@ -1201,7 +1201,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
     HIPC(c, hipEventRecord(c->film_order, c->stream));
     const uint32_t tail = volTailPaths();
     uint32_t next = 0, filmNext = 0;
-    auto views = [&](VolLane &l, VolDev &lv, VolWave &w, Queue *q) {
+    auto views = [&](VolLane &l, VolDev &lv, VolWave &w, Queue *q) {  // q: 7 queues
         lv = v;
         lv.rad = l.rad.as<float4>();
         lv.stack_ovf = l.ovf.as<uint32_t>();
@@ -1210,10 +1210,10 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         const size_t cap = l.cap;
         w = VolWave{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
                     reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap};
-        // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices
+        // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices, 5/6: delta surface
         const size_t qstride = (size_t)pg_queue_stride(l.cap) * PG_QSHARDS;
         const uint32_t stride = pg_queue_stride(l.np * l.nl);
-        for (int k = 0; k < 5; ++k)
+        for (int k = 0; k < 7; ++k)
             q[k] = Queue{l.items.as<uint32_t>() + k * qstride, l.counts.as<uint32_t>() + k * PG_QSHARDS, stride};
         if (sortMin)
             for (int k = 0; k < 2; ++k) q[k].keys = l.keys.as<uint16_t>() + k * qstride;
@@ -1239,11 +1239,11 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         HIPC(c, hipEventRecord(l.span.a, l.stream));
         VolDev lv;
         VolWave w;
-        Queue q[5];
+        Queue q[7];
         views(l, lv, w, q);
         HIPC(c, hipMemsetAsync(l.counts.p, 0, cbytes, l.stream));
         pg_launch_vol_camera(l.stream, g, sc, lv, w, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, l.sample_base,
-                             q[0], q[2]);
+                             q[0], q[2], q[5]);
         HIPC(c, hipGetLastError());
         return readback(l);
     };
@@ -1292,13 +1292,14 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         };
         VolDev lv;
         VolWave w;
-        Queue q[5];
+        Queue q[7];
         views(l, lv, w, q);
         const int cur = l.it & 1, nxt = cur ^ 1;
-        const auto f = maxShard(cur), su = maxShard(2 + cur);
-        if (f.second + su.second <= tail) {
-            if (f.second + su.second) {
-                pg_launch_vol_tail(l.stream, g, sc, lv, sd, w, q[cur], f.first, q[2 + cur], su.first);
+        const auto f = maxShard(cur), su = maxShard(2 + cur), sdl = maxShard(5 + cur);
+        if (f.second + su.second + sdl.second <= tail) {
+            if (f.second + su.second + sdl.second) {
+                pg_launch_vol_tail(l.stream, g, sc, lv, sd, w, q[cur], f.first, q[2 + cur], su.first, q[5 + cur],
+                                   sdl.first);
                 HIPC(c, hipGetLastError());
             }
             l.waved = true;
@@ -1321,6 +1322,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         HIPC(c, hipMemsetAsync(q[nxt].counts, 0, PG_QSHARDS * 4, l.stream));
         HIPC(c, hipMemsetAsync(q[2 + nxt].counts, 0, PG_QSHARDS * 4, l.stream));
         HIPC(c, hipMemsetAsync(q[4].counts, 0, PG_QSHARDS * 4, l.stream));
+        HIPC(c, hipMemsetAsync(q[5 + nxt].counts, 0, PG_QSHARDS * 4, l.stream));
         // per-stage device time (pg_config.kernel_timing, one lane): events around each launch
         if (evt && !c->vw_ev[0])
             for (hipEvent_t &e : c->vw_ev) HIPC(c, hipEventCreate(&e));
@@ -1330,12 +1332,13 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
             fq.items = l.sorted.as<uint32_t>();
         }
         if (evt) HIPC(c, hipEventRecord(c->vw_ev[0], l.stream));
-        pg_launch_vol_flight(l.stream, g, lv, sd, w, fq, f.first, q[4], q[2 + cur]);
+        pg_launch_vol_flight(l.stream, g, sc, lv, sd, w, fq, f.first, q[4], q[2 + cur], q[5 + cur]);
         if (evt) HIPC(c, hipEventRecord(c->vw_ev[1], l.stream));
         // shard bounds without a readback: a medium vertex came from a flight; a surface vertex from a
         // flight or from the previous iteration's interactions; no shard exceeds the queue stride
-        const uint32_t mm = f.first, ms = std::min(q[0].stride, f.first + su.first);
-        pg_launch_vol_vertex(l.stream, g, sc, lv, sd, w, q[4], mm, q[2 + cur], ms, q[nxt], q[2 + nxt]);
+        const uint32_t mm = f.first, ms = std::min(q[0].stride, f.first + su.first + sdl.first);
+        pg_launch_vol_vertex(l.stream, g, sc, lv, sd, w, q[4], mm, q[2 + cur], ms, q[5 + cur], ms, q[nxt], q[2 + nxt],
+                             q[5 + nxt]);
         if (evt) {
             HIPC(c, hipEventRecord(c->vw_ev[2], l.stream));
             HIPC(c, hipEventSynchronize(c->vw_ev[2]));

@@ -159,14 +159,16 @@ void pg_launch_volpath(hipStream_t s, const GParams &g, const SceneDev &sc, cons
 // of `flight` and `surf` one thread each.  max_*: upper bounds of the largest shard counts.
 void pg_launch_vol_camera(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w,
                           const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
-                          uint32_t sample_base, Queue flight, Queue surf);
-void pg_launch_vol_flight(hipStream_t s, const GParams &g, const VolDev &v, const SDDev &sd, const VolWave &w,
-                          Queue flight, uint32_t max_flight, Queue med, Queue surf);
+                          uint32_t sample_base, Queue flight, Queue surf, Queue dsurf);
+// surf / dsurf: surface vertices on other / delta-class surfaces (and escaped rays), pg_volpath.hip PG_VOL_SPLIT_SURF
+void pg_launch_vol_flight(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                          const VolWave &w, Queue flight, uint32_t max_flight, Queue med, Queue surf, Queue dsurf);
 void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf,
-                          Queue next_flight, Queue next_surf);
+                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
+                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf);
 void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                        const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf);
+                        const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf, Queue dsurf,
+                        uint32_t max_dsurf);
 void pg_launch_phase_query(hipStream_t s, const GMedium *medium, const float *in, const float *wog, uint32_t n,
                            float *out);
 // corner-packed density of a linear grid (pg_layout.h PG_DENSITY_CORNERS); out: 8 floats per cell

@@ -956,6 +956,20 @@ __device__ __forceinline__ uint16_t flightKey(const VolDev &v, int m, f3 o, f3 d
     if (PG_VOL_SORT_KEY == 1) k |= ((d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u)) << 9;
     return (uint16_t)k;
 }
+// surface vertices split by the hit's material class (PG_VOL_SPLIT_SURF): delta surfaces (the null
+// boundaries of media, smooth conductors and dielectrics: no emitter sample, no shadow walk) and escaped
+// rays go to their own queue, so the waves of the other surfaces' shadow walks carry no idle lanes
+#ifndef PG_VOL_SPLIT_SURF
+#define PG_VOL_SPLIT_SURF 1
+#endif
+__device__ __forceinline__ bool cheapSurface(const SceneDev &sc, bool valid, uint32_t tri) {
+    return PG_VOL_SPLIT_SURF && (!valid || sc.tclass[tri] == PG_CLASS_DELTA);
+}
+__device__ __forceinline__ void surfAppend(bool pred, bool cheap, uint32_t slot, const Queue &qs, const Queue &qd,
+                                           uint32_t sh) {
+    waveAppend(pred && !cheap, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
+    if (PG_VOL_SPLIT_SURF) waveAppend(pred && cheap, slot, qd.items + (size_t)sh * qd.stride, qd.counts + sh);
+}
 // append to a flight queue, with the order key when the queue carries keys
 __device__ __forceinline__ void flightAppend(bool pred, uint32_t slot, uint16_t key, const Queue &q, uint32_t sh) {
     if (q.keys)
@@ -976,14 +990,14 @@ template <bool GUIDED>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, VolDev v, VolWave w,
                                                       const uint32_t *__restrict__ local_pixels, uint32_t pix_begin,
                                                       uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue qf,
-                                                      Queue qs) {
+                                                      Queue qs, Queue qd) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, v.stack_ovf);
     const uint32_t n = npix * nlayers;
     uint32_t segs = 0, lookups = 0;
     for (uint32_t base = blockIdx.x * TRACE_BLOCK; base < n; base += gridDim.x * TRACE_BLOCK) {
         const uint32_t slot = base + threadIdx.x;
-        bool toF = false, toS = false;
+        bool toF = false, toS = false, cheap = false;
         uint16_t key = 0;
         if (slot < n) {
             VPath P;
@@ -996,11 +1010,12 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
                 toF = P.medium >= 0;
                 toS = !toF;
                 if (toF && qf.keys) key = flightKey(v, P.medium, P.o, P.d);
+                if (toS) cheap = cheapSurface(sc, P.its.valid, P.its.tri);
             }
         }
         const uint32_t sh = slotShard(base + (threadIdx.x & ~63u));
         flightAppend(toF, slot, key, qf, sh);
-        waveAppend(toS, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
+        surfAppend(toS, cheap, slot, qs, qd, sh);
     }
     volStats(v, segs, 0, lookups);
 }
@@ -1017,13 +1032,13 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
 #endif
 template <bool GUIDED>
 __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_VFLIGHT_WAVES > 0 ? PG_VFLIGHT_WAVES : 1)))
-void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm, Queue qs) {
+void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm, Queue qs, Queue qd) {
     const uint32_t sh = blockIdx.x & (PG_QSHARDS - 1), rows = gridDim.x / PG_QSHARDS;
     const uint32_t n = qf.counts[sh];
     uint32_t flights = 0, lookups = 0;
     for (uint32_t base = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
-        bool toM = false, toS = false;
+        bool toM = false, toS = false, cheap = false;
         uint32_t slot = 0;
         if (i < n) {
             slot = qf.items[(size_t)sh * qf.stride + i];
@@ -1041,6 +1056,7 @@ void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm, Que
             f3 mp = mk1(0.f);
             toM = volFlight<GUIDED>(v, sd, P, rng, mp);
             toS = !toM;
+            if (toS) cheap = cheapSurface(sc, P.its.valid, s.y);
             flights++;
             lookups += rng.lookups - r.w;
             w.r[slot] = make_uint4(rng.key, rng.sample, rng.dim, rng.lookups);
@@ -1048,7 +1064,7 @@ void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm, Que
             if (toM) w.mp[slot] = f4(mp, 0.0f);
         }
         waveAppend(toM, slot, qm.items + (size_t)sh * qm.stride, qm.counts + sh);
-        waveAppend(toS, slot, qs.items + (size_t)sh * qs.stride, qs.counts + sh);
+        surfAppend(toS, cheap, slot, qs, qd, sh);
     }
     volStageStats(v, 3, flights, lookups);
 }
@@ -1056,20 +1072,22 @@ void k_vflight(GParams g, VolDev v, SDDev sd, VolWave w, Queue qf, Queue qm, Que
 // interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices
 template <bool GUIDED>
 __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
-                                                                       VolWave w, Queue qm, Queue qs, uint32_t mblocks,
-                                                                       Queue nf, Queue ns) {
+                                                                       VolWave w, Queue qm, Queue qs, Queue qd,
+                                                                       uint32_t mblocks, uint32_t dblocks, Queue nf,
+                                                                       Queue ns, Queue nd) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, v.stack_ovf);
-    const bool medium = blockIdx.x < mblocks;
-    const uint32_t b = medium ? blockIdx.x : blockIdx.x - mblocks;
-    const uint32_t nb = medium ? mblocks : gridDim.x - mblocks;
-    const Queue &q = medium ? qm : qs;
+    // blocks [0, mblocks): medium vertices; [mblocks, mblocks + dblocks): delta surfaces; the rest: surfaces
+    const bool medium = blockIdx.x < mblocks, delta = !medium && blockIdx.x < mblocks + dblocks;
+    const uint32_t b = medium ? blockIdx.x : (delta ? blockIdx.x - mblocks : blockIdx.x - mblocks - dblocks);
+    const uint32_t nb = medium ? mblocks : (delta ? dblocks : gridDim.x - mblocks - dblocks);
+    const Queue &q = medium ? qm : (delta ? qd : qs);
     const uint32_t sh = b & (PG_QSHARDS - 1), rows = nb / PG_QSHARDS;
     const uint32_t n = q.counts[sh];
     uint32_t segs = 0, shadows = 0, lookups = 0, vertices = 0, vlookups = 0;
     for (uint32_t base = (b / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
-        bool toF = false, toS = false;
+        bool toF = false, toS = false, cheap = false;
         uint32_t slot = 0;
         uint16_t key = 0;
         if (i < n) {
@@ -1087,12 +1105,13 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
                 toF = P.medium >= 0;
                 toS = !toF;
                 if (toF && nf.keys) key = flightKey(v, P.medium, P.o, P.d);
+                if (toS) cheap = cheapSurface(sc, P.its.valid, P.its.tri);
             } else {
                 volEnd(v, slot, P, rng, lookups);
             }
         }
         flightAppend(toF, slot, key, nf, sh);
-        waveAppend(toS, slot, ns.items + (size_t)sh * ns.stride, ns.counts + sh);
+        surfAppend(toS, cheap, slot, ns, nd, sh);
     }
     volStats(v, segs, shadows, lookups);
     volStageStats(v, 5, vertices, vlookups);
@@ -1102,13 +1121,15 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
 // of `qs` with their surface interaction)
 template <bool GUIDED>
 __global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vtail(GParams g, SceneDev sc, VolDev v, SDDev sd,
-                                                                     VolWave w, Queue qf, Queue qs, uint32_t fblocks) {
+                                                                     VolWave w, Queue qf, Queue qs, Queue qd,
+                                                                     uint32_t fblocks, uint32_t dblocks) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, v.stack_ovf);
-    const bool flight = blockIdx.x < fblocks;
-    const uint32_t b = flight ? blockIdx.x : blockIdx.x - fblocks;
-    const uint32_t nb = flight ? fblocks : gridDim.x - fblocks;
-    const Queue &q = flight ? qf : qs;
+    // blocks [0, fblocks): flights; [fblocks, fblocks + dblocks): delta surfaces; the rest: surfaces
+    const bool flight = blockIdx.x < fblocks, delta = !flight && blockIdx.x < fblocks + dblocks;
+    const uint32_t b = flight ? blockIdx.x : (delta ? blockIdx.x - fblocks : blockIdx.x - fblocks - dblocks);
+    const uint32_t nb = flight ? fblocks : (delta ? dblocks : gridDim.x - fblocks - dblocks);
+    const Queue &q = flight ? qf : (delta ? qd : qs);
     const uint32_t sh = b & (PG_QSHARDS - 1), rows = nb / PG_QSHARDS;
     const uint32_t n = q.counts[sh];
     uint32_t segs = 0, shadows = 0, lookups = 0;
@@ -1133,50 +1154,59 @@ static inline uint32_t vrows(uint32_t max_shard, uint32_t cap) {
 
 void pg_launch_vol_camera(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w,
                           const uint32_t *local_pixels, uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
-                          uint32_t sample_base, Queue flight, Queue surf) {
+                          uint32_t sample_base, Queue flight, Queue surf, Queue dsurf) {
     const uint64_t n = (uint64_t)npix * nlayers;
     if (!n) return;
     const uint64_t want = (n + TRACE_BLOCK - 1) / TRACE_BLOCK;
     const dim3 grid((uint32_t)(want < TRACE_MAX_BLOCKS ? want : TRACE_MAX_BLOCKS));  // the overflow ring's size
     if (g.guiding)
         hipLaunchKernelGGL(k_vcam<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, w, local_pixels, pix_begin, npix,
-                           nlayers, sample_base, flight, surf);
+                           nlayers, sample_base, flight, surf, dsurf);
     else
         hipLaunchKernelGGL(k_vcam<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, w, local_pixels, pix_begin, npix,
-                           nlayers, sample_base, flight, surf);
+                           nlayers, sample_base, flight, surf, dsurf);
 }
-void pg_launch_vol_flight(hipStream_t s, const GParams &g, const VolDev &v, const SDDev &sd, const VolWave &w,
-                          Queue flight, uint32_t max_flight, Queue med, Queue surf) {
+void pg_launch_vol_flight(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                          const VolWave &w, Queue flight, uint32_t max_flight, Queue med, Queue surf, Queue dsurf) {
     if (!max_flight) return;
     const dim3 grid(PG_QSHARDS * vrows(max_flight, TRACE_MAX_BLOCKS / PG_QSHARDS));
-    if (g.guiding) hipLaunchKernelGGL(k_vflight<true>, grid, dim3(TRACE_BLOCK), 0, s, g, v, sd, w, flight, med, surf);
-    else hipLaunchKernelGGL(k_vflight<false>, grid, dim3(TRACE_BLOCK), 0, s, g, v, sd, w, flight, med, surf);
+    if (g.guiding)
+        hipLaunchKernelGGL(k_vflight<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, med, surf, dsurf);
+    else
+        hipLaunchKernelGGL(k_vflight<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, med, surf, dsurf);
 }
 void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf,
-                          Queue next_flight, Queue next_surf) {
-    // both block ranges within TRACE_MAX_BLOCKS (the traversal stacks' overflow ring)
-    const uint32_t mr = max_med ? vrows(max_med, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
-    const uint32_t sr = max_surf ? vrows(max_surf, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
-    if (mr + sr == 0) return;
-    const dim3 grid(PG_QSHARDS * (mr + sr));
+                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
+                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf) {
+    // the three block ranges within TRACE_MAX_BLOCKS (the traversal stacks' overflow ring)
+    const uint32_t cap = TRACE_MAX_BLOCKS / PG_QSHARDS / 4;
+    const uint32_t mr = max_med ? vrows(max_med, cap) : 0;
+    const uint32_t sr = max_surf ? vrows(max_surf, cap) : 0;
+    const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
+    if (mr + sr + dr == 0) return;
+    const dim3 grid(PG_QSHARDS * (mr + dr + sr));
     if (g.guiding)
-        hipLaunchKernelGGL(k_vvertex<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, PG_QSHARDS * mr,
-                           next_flight, next_surf);
+        hipLaunchKernelGGL(k_vvertex<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, dsurf,
+                           PG_QSHARDS * mr, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf);
     else
-        hipLaunchKernelGGL(k_vvertex<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, PG_QSHARDS * mr,
-                           next_flight, next_surf);
+        hipLaunchKernelGGL(k_vvertex<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, dsurf,
+                           PG_QSHARDS * mr, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf);
 }
 void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                        const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf) {
-    const uint32_t fr = max_flight ? vrows(max_flight, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
-    const uint32_t sr = max_surf ? vrows(max_surf, TRACE_MAX_BLOCKS / PG_QSHARDS / 2) : 0;
-    if (fr + sr == 0) return;
-    const dim3 grid(PG_QSHARDS * (fr + sr));
+                        const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf, Queue dsurf,
+                        uint32_t max_dsurf) {
+    const uint32_t cap = TRACE_MAX_BLOCKS / PG_QSHARDS / 4;
+    const uint32_t fr = max_flight ? vrows(max_flight, cap) : 0;
+    const uint32_t sr = max_surf ? vrows(max_surf, cap) : 0;
+    const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
+    if (fr + sr + dr == 0) return;
+    const dim3 grid(PG_QSHARDS * (fr + dr + sr));
     if (g.guiding)
-        hipLaunchKernelGGL(k_vtail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, PG_QSHARDS * fr);
+        hipLaunchKernelGGL(k_vtail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, dsurf,
+                           PG_QSHARDS * fr, PG_QSHARDS * dr);
     else
-        hipLaunchKernelGGL(k_vtail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, PG_QSHARDS * fr);
+        hipLaunchKernelGGL(k_vtail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, dsurf,
+                           PG_QSHARDS * fr, PG_QSHARDS * dr);
 }
 
 namespace {
