@@ -188,7 +188,7 @@ struct Ctx {
     DevBuf env, envtex, envtab;  // environment emitter: GEnv record, texels, CDFs + row weights
     bool has_env = false;
     // media (volpath)
-    DevBuf media, density, tmed, majorant;
+    DevBuf media, density, tmed, majorant, tcheap;
     int32_t cam_medium = -1;
     uint32_t num_media = 0;
     DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
@@ -859,11 +859,14 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     if (!pgh::buildBvh(d->positions, d->indices, nt, kStackDepth, bvh))
         return fail(c, PG_ERR_INVALID, "pg_upload_scene: BVH deeper than the traversal stack");
     std::vector<float> shade((size_t)20 * nt);
-    std::vector<uint8_t> tclass(nt);
+    std::vector<uint8_t> tclass(nt), tcheap(nt);
     for (uint32_t k = 0; k < nt; ++k) {
         uint32_t t = bvh.order[k];
         packShade(&shade[20 * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
         tclass[k] = (uint8_t)materialClass(d->materials[triBits[t] & 0xFFFFu].type);
+        // volumetric wavefront: surfaces whose interaction skips the shadow walk through media (delta
+        // BSDFs) or ends the path at once (emitters: black in the scenes here) -- VolDev::tcheap
+        tcheap[k] = tclass[k] == PG_CLASS_DELTA || (triBits[t] >> 16) != 0;
     }
     // per BVH-order triangle: the shape's medium transition, (interior + 1) | (exterior + 1) << 16
     std::vector<uint32_t> tmed(nt, 0);
@@ -939,7 +942,7 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||
         (s = upload(c, c->mats, c->host_mats)) || (s = upload(c, c->ems, ems)) || (s = upload(c, c->emtri, emtri)) ||
-        (s = upload(c, c->emcdf, emcdf)) || (s = upload(c, c->tmed, tmed)))
+        (s = upload(c, c->emcdf, emcdf)) || (s = upload(c, c->tmed, tmed)) || (s = upload(c, c->tcheap, tcheap)))
         return s;
     // densities: one buffer, each grid 256-B aligned (bricked, see pg_layout.h GMedium)
     {
@@ -1430,6 +1433,7 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     v.grid = c->cfg.volume_majorant == PG_MAJORANT_GRID ? 1 : 0;
     v.media = c->media.as<GMedium>();
     v.tmed = c->tmed.as<uint32_t>();
+    v.tcheap = c->tcheap.as<uint8_t>();
     v.cam_medium = c->cam_medium;
     v.num_media = c->num_media;
     v.rad = c->vol_rad.as<float4>();

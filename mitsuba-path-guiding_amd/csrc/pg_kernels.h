@@ -70,6 +70,7 @@ struct VolDev {
     uint32_t vtx_P;            // slot stride of vtx (>= items per launch)
     float dist_beta;           // pg_config.distance_guiding
     uint32_t refill_min;       // k_volpath refills a wave's finished lanes once at least this many are idle
+    const uint8_t *tcheap;     // per BVH-order triangle: 1 = delta BSDF or emitter (the wavefront's cheap surface queue)
 };
 
 // Volumetric wavefront (pg_volpath.hip k_vcam, k_vflight, k_vvertex, k_vtail): the megakernel's per-lane

@@ -956,14 +956,19 @@ __device__ __forceinline__ uint16_t flightKey(const VolDev &v, int m, f3 o, f3 d
     if (PG_VOL_SORT_KEY == 1) k |= ((d.x < 0 ? 1u : 0u) | (d.y < 0 ? 2u : 0u) | (d.z < 0 ? 4u : 0u)) << 9;
     return (uint16_t)k;
 }
-// surface vertices split by the hit's material class (PG_VOL_SPLIT_SURF): delta surfaces (the null
-// boundaries of media, smooth conductors and dielectrics: no emitter sample, no shadow walk) and escaped
-// rays go to their own queue, so the waves of the other surfaces' shadow walks carry no idle lanes
+// surface vertices split by the hit triangle (PG_VOL_SPLIT_SURF): delta surfaces (the null boundaries of
+// media, smooth conductors and dielectrics: no emitter sample, no shadow walk), emitters (PG_VOL_SPLIT_EMIT:
+// black in the scenes here, so the path ends there) and escaped rays go to their own queue, so the waves
+// of the other surfaces' shadow walks carry no idle lanes
 #ifndef PG_VOL_SPLIT_SURF
 #define PG_VOL_SPLIT_SURF 1
 #endif
-__device__ __forceinline__ bool cheapSurface(const SceneDev &sc, bool valid, uint32_t tri) {
-    return PG_VOL_SPLIT_SURF && (!valid || sc.tclass[tri] == PG_CLASS_DELTA);
+#ifndef PG_VOL_SPLIT_EMIT
+#define PG_VOL_SPLIT_EMIT 1
+#endif
+__device__ __forceinline__ bool cheapSurface(const SceneDev &sc, const VolDev &v, bool valid, uint32_t tri) {
+    return PG_VOL_SPLIT_SURF &&
+           (!valid || (PG_VOL_SPLIT_EMIT ? v.tcheap[tri] != 0 : sc.tclass[tri] == PG_CLASS_DELTA));
 }
 __device__ __forceinline__ void surfAppend(bool pred, bool cheap, uint32_t slot, const Queue &qs, const Queue &qd,
                                            uint32_t sh) {
@@ -1010,7 +1015,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_vcam(GParams g, SceneDev sc, Vo
                 toF = P.medium >= 0;
                 toS = !toF;
                 if (toF && qf.keys) key = flightKey(v, P.medium, P.o, P.d);
-                if (toS) cheap = cheapSurface(sc, P.its.valid, P.its.tri);
+                if (toS) cheap = cheapSurface(sc, v, P.its.valid, P.its.tri);
             }
         }
         const uint32_t sh = slotShard(base + (threadIdx.x & ~63u));
@@ -1056,7 +1061,7 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
             f3 mp = mk1(0.f);
             toM = volFlight<GUIDED>(v, sd, P, rng, mp);
             toS = !toM;
-            if (toS) cheap = cheapSurface(sc, P.its.valid, s.y);
+            if (toS) cheap = cheapSurface(sc, v, P.its.valid, s.y);
             flights++;
             lookups += rng.lookups - r.w;
             w.r[slot] = make_uint4(rng.key, rng.sample, rng.dim, rng.lookups);
@@ -1105,7 +1110,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
                 toF = P.medium >= 0;
                 toS = !toF;
                 if (toF && nf.keys) key = flightKey(v, P.medium, P.o, P.d);
-                if (toS) cheap = cheapSurface(sc, P.its.valid, P.its.tri);
+                if (toS) cheap = cheapSurface(sc, v, P.its.valid, P.its.tri);
             } else {
                 volEnd(v, slot, P, rng, lookups);
             }
