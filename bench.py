@@ -72,7 +72,7 @@ def parse():
     ap.add_argument("--train", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-quality", action="store_true")
-    ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3; volpath wavefront 2)")
+    ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3)")
     ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = auto: 2^25)")
     ap.add_argument("--exchange", default=None, choices=["allreduce", "allgather", "capi", "capi-allgather"],
                     help="postprogression exchange (N > 1): the library's own RCCL communicator (pg_comm_*, the C++ "

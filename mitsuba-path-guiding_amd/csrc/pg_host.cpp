@@ -1150,11 +1150,12 @@ uint32_t volSortMin() {
     const char *e = std::getenv("PG_VOL_SORT");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 4096u;
 }
-// volumetric wavefront lanes in flight: pg_config.path_lanes, default 2 (C5: 310 / 347 / 330 Mpaths/s with
-// 1 / 2 / 3 lanes, profiles/r04q_vol_lanes/); PG_VOL_LANES overrides (A/B)
+// volumetric wavefront lanes in flight: pg_config.path_lanes (default 3, as for the path integrator; C5 at
+// the round-4 kernels: 393.7 / 397.0 / 389.7 Mpaths/s with 2 / 3 / 4 lanes, profiles/r04aj_vol_lanes/);
+// PG_VOL_LANES overrides (A/B)
 int volLanes(const Ctx *c) {
     const char *e = std::getenv("PG_VOL_LANES");
-    const int n = e && *e ? std::atoi(e) : (c->cfg.path_lanes ? c->cfg.path_lanes : 2);
+    const int n = e && *e ? std::atoi(e) : c->nlanes;
     return std::max(1, std::min(PG_MAX_LANES, n));
 }
 
