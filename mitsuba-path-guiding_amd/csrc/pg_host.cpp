@@ -1133,10 +1133,11 @@ bool volWavefront() {
     const char *e = std::getenv("PG_VOL_WAVEFRONT");
     return e && *e ? std::atoi(e) != 0 : true;
 }
-// below this many live paths a chunk's remaining paths finish in one k_vtail launch (PG_VOL_TAIL_PATHS)
+// below this many live paths a chunk's remaining paths finish in one k_vtail launch (PG_VOL_TAIL_PATHS): 2^17
+// with three lanes (C5 398.7 / 399.4 against 396.6 / 397.5 at 2^18, profiles/r04al_vol_tail/)
 uint32_t volTailPaths() {
     const char *e = std::getenv("PG_VOL_TAIL_PATHS");
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 18;
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 17;
 }
 
 // chunks of a volumetric pass: np pixels from pb, nl sample layers from sample_base
