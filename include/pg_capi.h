@@ -196,7 +196,9 @@ typedef struct pg_config {
     int32_t world_size;
     uint32_t tile_size;           /* 32 (Scene::setBlockSize default) */
     uint32_t max_paths_in_flight; /* paths per chunk; 0 = auto: 2^25 */
-    int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024) */
+    int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024; the path integrator
+                                     clamps it to 1098, and pg_create rejects a path-integrator max_depth above
+                                     1097 with PG_ERR_INVALID; the volpath integrator honours both exactly) */
     int32_t path_lanes;           /* path chunks in flight on separate streams, 1..4 (0 = auto: 3) */
     int32_t integrator;           /* PG_INTEGRATOR_PATH (progressive_path) or _VOLPATH (progressive_volpath) */
     int32_t volume_majorant;      /* volpath free-flight / transmittance tracking: PG_MAJORANT_GRID (default:

@@ -17,7 +17,7 @@ PG_MEDIUM_HETEROGENEOUS = 0
 PG_INTEGRATOR_PATH, PG_INTEGRATOR_VOLPATH = 0, 1
 PG_MAJORANT_GRID, PG_MAJORANT_GLOBAL = 0, 1
 PG_FRACTION_FIXED, PG_FRACTION_ALBEDO, PG_FRACTION_THROUGHPUT, PG_FRACTION_LEARNED = 0, 1, 2, 3
-MAJORANT_CELL = 8  # voxels per majorant-grid cell edge (pg_host.cpp / oracle/orc_medium.h)
+MAJORANT_CELL = 16  # voxels per majorant-grid cell edge (pg_layout.h PG_MAJORANT_CELL / oracle/orc_medium.h)
 PG_DIST_BECKMANN, PG_DIST_GGX = 0, 1
 PG_MAT_TWOSIDED, PG_MAT_NONLINEAR, PG_MAT_SAMPLE_ALL = 1, 2, 4
 

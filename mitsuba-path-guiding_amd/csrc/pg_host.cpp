@@ -35,11 +35,14 @@ constexpr uint32_t kBounceWords = 640;
 constexpr uint32_t kShadowCounts = PG_QSHARDS, kClassCounts = 2 * PG_QSHARDS;
 static_assert(kClassCounts + (PG_NUM_CLASSES + 1) * PG_QSHARDS <= kBounceWords, "counter layout");
 constexpr uint32_t kCounterWords = kBounceWords * (kMaxBounces + 1);
-// the device's bounce cap (GParams::depth_cap): max_depth + 1 or gpu_depth_cap, at most kMaxBounces - 2,
-// so the bounce-by-bounce loop (maxBounces = depth_cap + 2 <= kMaxBounces) and k_tail, which loops until
-// shadeOne's depth_cap test ends the path, stop at the same bounce
+// the device's bounce cap (GParams::depth_cap): max_depth + 1 or gpu_depth_cap.  The surface path keeps
+// one counter block per bounce, so its cap is at most kMaxBounces - 2 (pg_create rejects a larger
+// max_depth and clamps gpu_depth_cap there), and the bounce-by-bounce loop (maxBounces = depth_cap + 2 <=
+// kMaxBounces) and k_tail, which loops until shadeOne's depth_cap test ends the path, stop at the same
+// bounce.  The volumetric path has no per-bounce buffer and honours max_depth exactly.
 static uint32_t deviceDepthCap(const pg_config &cfg) {
     const int64_t cap = cfg.max_depth > 0 ? (int64_t)cfg.max_depth + 1 : (int64_t)cfg.gpu_depth_cap;
+    if (cfg.integrator == PG_INTEGRATOR_VOLPATH) return (uint32_t)std::min<int64_t>(cap, 0x7fffffff);
     return (uint32_t)std::min<int64_t>(cap, (int64_t)kMaxBounces - 2);
 }
 
@@ -715,7 +718,15 @@ pg_status pg_create(const pg_config *cfg, void **out) {
     c->cfg = *cfg;
     if (c->cfg.tile_size == 0) c->cfg.tile_size = 32;
     if (c->cfg.gpu_depth_cap <= 0) c->cfg.gpu_depth_cap = 1024;
-    if (c->cfg.gpu_depth_cap > (int32_t)kMaxBounces - 2) c->cfg.gpu_depth_cap = (int32_t)kMaxBounces - 2;
+    if (c->cfg.integrator == PG_INTEGRATOR_PATH) {  // the surface wavefront's per-bounce counter blocks
+        if (c->cfg.gpu_depth_cap > (int32_t)kMaxBounces - 2) c->cfg.gpu_depth_cap = (int32_t)kMaxBounces - 2;
+        if (c->cfg.max_depth > (int32_t)kMaxBounces - 3) {
+            delete c;
+            return fail(nullptr, PG_ERR_INVALID,
+                        "pg_create: max_depth above " + std::to_string(kMaxBounces - 3) +
+                            " is not supported by the path integrator (use -1 for unbounded paths)");
+        }
+    }
     if (c->cfg.path_lanes < 0 || c->cfg.path_lanes > PG_MAX_LANES) {
         delete c;
         return fail(nullptr, PG_ERR_INVALID, "pg_create: path_lanes must be 0..4");
@@ -1466,6 +1477,15 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
         layer += nl;
     }
     std::vector<EventPair> evs;
+    struct EventsGuard {  // the chunk spans, on every exit (an error or cancellation returns early)
+        std::vector<EventPair> &v;
+        ~EventsGuard() {
+            for (EventPair &e : v) {
+                (void)hipEventDestroy(e.a);
+                (void)hipEventDestroy(e.b);
+            }
+        }
+    } evsGuard{evs};
     if (wave) {
         pg_status ws = volWavefrontPass(c, g, sc, v, sd, pv, chunks, want, maxV, vtxLanes, evs);
         if (ws) return ws;
@@ -1521,11 +1541,28 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
         (void)hipEventElapsedTime(&ms, e.a, e.b);
         c->stats.volume_ms += ms;
         c->stats.volume_launches++;
-        (void)hipEventDestroy(e.a);
-        (void)hipEventDestroy(e.b);
     }
     return PG_OK;
 }
+
+// Every exit of a pass that did not complete (cancellation, a HIP error): the lane streams are created
+// non-blocking, so nothing queued later on c->stream (pg_read_film, pg_reset_film) orders after them.
+// Wait for them, so that no lane kernel still writes the film or the records once pg_render_pass has
+// returned, and release the chunk span events a volumetric lane had not handed over yet.
+static void drainLanes(Ctx *c) {
+    for (int li = 0; li < c->nlanes; ++li)
+        if (c->lanes[li].stream) (void)hipStreamSynchronize(c->lanes[li].stream);
+    for (VolLane &l : c->vlanes) {
+        if (l.stream) (void)hipStreamSynchronize(l.stream);
+        if (l.span.a) (void)hipEventDestroy(l.span.a);
+        if (l.span.b) (void)hipEventDestroy(l.span.b);
+        l.span = EventPair{};
+        l.active = l.waved = false;
+    }
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+}
+
+static pg_status renderPass(Ctx *c, uint32_t spp, uint32_t sample_offset, int32_t record);
 
 pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_t record) {
     Ctx *c = (Ctx *)ctx;
@@ -1533,6 +1570,12 @@ pg_status pg_render_pass(void *ctx, uint32_t spp, uint32_t sample_offset, int32_
     if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_render_pass: no scene uploaded");
     if (c->cancel.load()) return fail(c, PG_ERR_CANCELLED, "cancelled");
     HIPC(c, hipSetDevice(c->cfg.device));
+    const pg_status s = renderPass(c, spp, sample_offset, record);
+    if (s) drainLanes(c);
+    return s;
+}
+
+static pg_status renderPass(Ctx *c, uint32_t spp, uint32_t sample_offset, int32_t record) {
     const uint32_t npix = (uint32_t)c->local_pixels.size();
     if (npix == 0 || spp == 0) return PG_OK;
     if (c->cfg.integrator == PG_INTEGRATOR_VOLPATH) return renderVolpath(c, spp, sample_offset, record && c->cfg.guiding);

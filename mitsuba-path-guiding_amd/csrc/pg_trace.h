@@ -119,6 +119,20 @@ __device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t
 #endif
 }
 
+// Closest-hit accept rule of every walk: a smaller t, or an equal t (shared edges, coplanar triangles)
+// on the lower ORIGINAL triangle index (TriAccel row 2, .z; pg_bvh.cpp triAccelRecord), the oracle's
+// rule (orc_scene.h Scene::traverse / bruteForce), so a tie resolves the same way on both sides and
+// whatever the BVH order.  The ids are loaded only on a tie.
+__device__ __forceinline__ bool acceptHit(const float4 *__restrict__ tris, float tt, float tmax, uint32_t tr,
+                                          uint32_t hitTri) {
+    if (tt < tmax || hitTri == 0xFFFFFFFFu) return true;
+#if PG_TRIACCEL
+    return __float_as_uint(tris[3 * tr + 2].z) < __float_as_uint(tris[3 * hitTri + 2].z);
+#else
+    return tr < hitTri;  // Woop rows carry no original id: BVH order (A/B builds only)
+#endif
+}
+
 __device__ __forceinline__ float qbyte(uint32_t lo, uint32_t hi, int s) {
     return (float)(((s < 4 ? lo : hi) >> (8 * (s & 3))) & 0xFFu);
 }
@@ -213,7 +227,7 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
             const uint32_t tr = T.x + (uint32_t)(__ffs(T.y) - 1);
             T.y &= T.y - 1u;
             float tt, bu, bv;
-            if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {  // ties: lower index
+            if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tr, hitTri)) {
                 found = true;
                 if (ANY) return true;
                 tmax = tt;
@@ -240,8 +254,8 @@ __device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int le
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t tr = first + k;
         float tt, bu, bv;
-        // equal distances: the lower triangle index (see traverseBin)
-        if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {
+        // equal distances: the lower original triangle index (acceptHit)
+        if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tr, hitTri)) {
             found = true;
             if (ANY) return true;
             tmax = tt;
@@ -465,10 +479,10 @@ __device__ __forceinline__ bool traverseBin(const float4 *__restrict__ nodes, co
             for (uint32_t k = 0; k < cnt; ++k) {
                 const uint32_t tr = first + k;
                 float tt, bu, bv;
-                // equal distances (shared edges, coplanar triangles) go to the lower triangle index, so
-                // the closest hit does not depend on the order in which the wave's postponed leaves are
-                // visited (and thus on which paths share the wave)
-                if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && (tt < tmax || tr < hitTri)) {
+                // equal distances (shared edges, coplanar triangles) go to the lower original triangle
+                // index (acceptHit), so the closest hit depends neither on the BVH nor on the order in
+                // which the wave's postponed leaves are visited (and thus on which paths share the wave)
+                if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tr, hitTri)) {
                     found = true;
                     if (ANY) return true;
                     tmax = tt;

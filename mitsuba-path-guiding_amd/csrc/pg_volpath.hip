@@ -378,10 +378,13 @@ __device__ __forceinline__ float mediumTransmittance(const VolDev &v, int m, f3 
 }
 
 // ---- scene queries ----------------------------------------------------------------------------
-// o + d t with explicit FMAs: the emitter walk's second pass must reproduce its first pass's origins
-// bit for bit (with `o + d * t` the compiler may contract one site and not the other)
+// o + d t, the multiply and the add rounded separately as in the oracle (orc_volpath.h, built with
+// -ffp-contract=off): the emitter walk's second pass must reproduce its first pass's origins bit for bit,
+// and both must equal the oracle's (scalar expressions under the pragma: the f3 operators' bodies lie
+// outside its scope; the Makefile builds this file without contraction anyway)
 __device__ __forceinline__ f3 advance(f3 o, f3 d, float t) {
-    return mk(fmaf(d.x, t, o.x), fmaf(d.y, t, o.y), fmaf(d.z, t, o.z));
+#pragma clang fp contract(off)
+    return mk(o.x + d.x * t, o.y + d.y * t, o.z + d.z * t);
 }
 __device__ __forceinline__ float max3abs(f3 o) { return fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z)); }
 // ShapeKDTree::rayIntersect(ray, its) epsilon rule for mint == Epsilon (skdtree.cpp:125-128)

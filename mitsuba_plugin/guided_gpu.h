@@ -56,8 +56,10 @@ public:
         // denoise = true the film receives the denoised image
         m_cfg.aovs = props.getBoolean("aovs", false);
         m_denoise = props.getBoolean("denoise", false);
-        if (m_denoise) m_cfg.aovs = 1;
         m_denoiserFile = props.getString("denoiserFile", "");
+        if (volumetric && (m_cfg.aovs || m_denoise || !m_denoiserFile.empty()))  // pg_create: aovs need the path integrator
+            Log(EError, "guided_gpu_volpath: \"aovs\", \"denoise\" and \"denoiserFile\" are supported by guided_gpu only");
+        if (m_denoise || !m_denoiserFile.empty()) m_cfg.aovs = 1;
         // combination of the training iterations' images with the final render: "discard" (Mueller et al.
         // 2017's default: the final render only) or "inversevar" (each image weighted by the inverse of
         // its mean per-pixel variance; integrator.py combine_inverse_variance is the same arithmetic)
@@ -228,7 +230,9 @@ public:
         // the film read-out index of output pixel (x, y): a mirrored toWorld flips x
         auto src = [&](int x, int y) { return (size_t) y * size.x + (m_flat.mirrorX ? size.x - 1 - x : x); };
         std::unique_ptr<Denoiser> denoiser;
-        if (m_cfg.aovs) {                                         // Denoiser::add's inputs (denoiser.cpp:138-144)
+        // the OIDN filter runs only when its output is wanted (the film or the stored buffers); "aovs"
+        // alone keeps the feature buffers on the context (pg_read_aovs)
+        if (m_cfg.aovs && (m_denoise || !m_denoiserFile.empty())) {  // Denoiser::add's inputs (denoiser.cpp:138-144)
             std::vector<float> alb(4 * npix), nrm(4 * npix);
             check(pg_read_aovs(m_ctx, alb.data(), nrm.data()));
             denoiser.reset(new Denoiser());

@@ -2,7 +2,7 @@
 // Checks the 4-wide closest-hit layout (pg_layout.h PG_QNODE_*) for structure -- every triangle in
 // exactly one leaf, child boxes containing their subtrees, the stack bound -- and runs a scalar
 // restatement of the device walk (traverse4: slabRay's padded slab test, widened culling distance, nearest-first
-// order, lower-index tie rule) against a brute-force loop over the same triangle records (TriAccel).
+// order, tie rule on the lower original triangle id) against a brute-force loop over the same triangle records (TriAccel).
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -39,6 +39,19 @@ bool triHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax,
     if (!(a >= 0.0f && a <= 1.0f)) return false;
     const float b = (w[11] + o[0] * w[8] + o[1] * w[9] + o[2] * w[10]) + tt * (d[0] * w[8] + d[1] * w[9] + d[2] * w[10]);
     return b >= 0.0f && a + b <= 1.0f;
+#endif
+}
+
+// the device walks' accept rule (pg_trace.h acceptHit): smaller t, or a tie on the lower original id
+bool accept(float tt, float tmax, uint32_t tr, uint32_t best) {
+    if (tt < tmax || best == 0xFFFFFFFFu) return true;
+#if PG_TRIACCEL
+    uint32_t a, b;
+    std::memcpy(&a, &g_bvh.tris[12 * (size_t)tr + 10], 4);
+    std::memcpy(&b, &g_bvh.tris[12 * (size_t)best + 10], 4);
+    return a < b;
+#else
+    return tr < best;
 #endif
 }
 
@@ -132,7 +145,7 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
             uint32_t best = 0xFFFFFFFFu;
             for (uint32_t tr = 0; tr < nt; ++tr) {
                 float tt;
-                if (triHit(tr, o, d, r[3], tmax, tt) && (tt < tmax || tr < best)) {
+                if (triHit(tr, o, d, r[3], tmax, tt) && accept(tt, tmax, tr, best)) {
                     tmax = tt;
                     best = tr;
                 }
@@ -164,7 +177,7 @@ void shim_trace(const float *rays, uint32_t n, uint32_t *walk, uint32_t *brute, 
                 const uint32_t lr = ~(uint32_t)node, first = lr >> 4, cnt = lr & 15u;
                 for (uint32_t k = 0; k < cnt; ++k) {
                     float tt;
-                    if (triHit(first + k, o, d, r[3], tmax, tt) && (tt < tmax || first + k < best)) {
+                    if (triHit(first + k, o, d, r[3], tmax, tt) && accept(tt, tmax, first + k, best)) {
                         tmax = tt;
                         best = first + k;
                     }

@@ -44,12 +44,12 @@ def test_adapter_flattens_env_and_media():
 
 
 def test_adapter_feeds_denoiser_and_combines_iterations():
-    """INTEGRATION.md's promises: with `aovs` the adapter reads pg_read_aovs and feeds the per-pixel means
+    """INTEGRATION.md's promises: with `denoise` or `denoiserFile` the adapter reads pg_read_aovs and feeds the per-pixel means
     to the fork's Denoiser (denoiser.cpp:138-144, Denoiser::add / denoise); `sampleCombination =
     "inversevar"` keeps every training iteration's film (pg_read_film + pg_reset_film) and combines them
     with inverse-variance weights all-reduced over ranks."""
     t = adapter_text()
-    aov = t[t.index("if (m_cfg.aovs)"):]
+    aov = t[t.index("if (m_cfg.aovs && (m_denoise"):]
     assert "pg_read_aovs" in aov and "Denoiser" in aov and "->add(" in aov and "->denoise()" in aov
     assert '"sampleCombination"' in t and '"inversevar"' in t
     train = t[t.index("for (int it = 0; it < m_trainingIterations"):t.index("pg_render_time")]

@@ -1,6 +1,7 @@
 """GPU radiance loops pinned by the reference's analytic two-disk scenes (tests/test_bidir_pin.py has
 the fixture and the oracle side): the surface wavefront (k_camera / k_trace / k_shade / k_rays /
-k_film) on test_bidir_0, the volumetric megakernel (k_volpath) on test_bidir_0 and test_bidir_2,
+k_film) on test_bidir_0, the volumetric path (the default wavefront: k_vcam / k_vflight / k_vvertex /
+k_vtail) on test_bidir_0 and test_bidir_2,
 each per pixel and on the image mean against the float64 quadrature; and the guided surface path
 (SD-tree trained on the GPU) against the same analytic image (guiding is unbiased)."""
 import numpy as np

@@ -95,7 +95,9 @@ def test_c3_guided_full_resolution(pg, O):
     rel_trim = float(np.sqrt(se[keep].mean() / 3) / np.sqrt((mc[keep] ** 2).mean()))
     print(f"c3 same-tree relative RMSE {rel_full:.5f}, without the worst 0.1 % of pixels {rel_trim:.5f}")
     assert rel_trim < 0.01, rel_trim
-    assert rel_full < 0.5, rel_full
+    # round 5: the kernels round as the oracle does (no FP contraction, ties on the original triangle
+    # id), so single-sample glints no longer set the full figure
+    assert rel_full < 0.1, rel_full
 
 
 def test_c4_guided_four_rank_shard(pg, O):
@@ -135,10 +137,12 @@ def test_c4_guided_four_rank_shard(pg, O):
     assert (g[0][..., 3] == c[0][..., 3]).mean() > 0.999
     z, diverged = pixel_parity(g, c, np.arange(sc.width * sc.height))
     assert (np.abs(z) < 5).mean() > 0.999
-    # same tree and streams, but ~1 M triangles (edge ties between the GPU's BVH and the oracle's
-    # TriAccel kd-style test) and glass/plastic clutter make fp32 path divergence more frequent than
-    # on C3 (measured 2.6 % of pixels at 16 spp); the z-test above is the per-pixel parity bar
-    assert diverged < 0.05, diverged
+    # same tree and streams; ~1 M triangles with many shared edges and glass/plastic clutter.  Until
+    # round 4 edge ties went by BVH order on the GPU and by original index in the oracle, and the kernels
+    # contracted the BSDF arithmetic to FMAs: 2.6 % of pixels diverged at 16 spp.  Both now match the
+    # oracle (pg_trace.h acceptHit, Makefile FPC=off)
+    print(f"c4 kitchen: diverged {diverged:.6f}")
+    assert diverged < 0.01, diverged
     for d in shards + [full]:
         d.close()
 

@@ -126,7 +126,8 @@ def test_trace_matches_bruteforce(pg, O, tmp_path_factory, name):
     cpu = osc.trace(rays)
     cp = cpu[:, 1].view(np.uint32)
     same = gp == cp
-    assert same[ok].mean() >= 0.995, same[ok].mean()  # ties: BVH order on the GPU, original index in the oracle
+    # ties go to the lower original triangle index on both sides (pg_trace.h acceptHit): every ray agrees
+    np.testing.assert_array_equal(gp[ok], cp[ok])
     hit = same & (gp != 0xFFFFFFFF)
     np.testing.assert_array_equal(g[hit][:, [0, 2, 3]], cpu[hit][:, [0, 2, 3]])
 
