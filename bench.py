@@ -54,6 +54,10 @@ BYTES_DENSITY_LOOKUP = 32      # k_volpath (C5): one trilinear lookup gathers 8 
 # interaction point (112 B), writes it back (96 B) and moves its queue entries (8 B)
 BYTES_VOL_FLIGHT = 104
 BYTES_VOL_VERTEX = 216
+# round 5: the interactions' transmittance walks as a stage of their own (k_vnee): per walked slot the flags
+# word (16 B), the NEE record (48 B), the random stream (16 B), L read + write (32 B) and the queue entry
+# (4 B); an emitter walk through media adds its 48-B record (rare: not in the floor)
+BYTES_VOL_NEE = 116
 GT_C3 = os.path.join(ROOT, "tests", "golden", "c3_gt.npz")
 GT_C3_CPU = os.path.join(ROOT, "tests", "golden", "c3_cpu_gt_tiles.npz")  # make_c3_cpu_gt.py
 
@@ -230,7 +234,7 @@ def main():
         # density gathers (every lookup: k_vcam / k_vflight / k_vvertex / k_vtail, or k_volpath) plus the
         # wavefront's state traffic per flight and interaction (0 with the megakernel, PG_VOL_WAVEFRONT=0)
         pipe_bytes = (d["density_lookups"] * BYTES_DENSITY_LOOKUP + d.get("vol_flights", 0) * BYTES_VOL_FLIGHT +
-                      d.get("vol_vertices", 0) * BYTES_VOL_VERTEX)
+                      d.get("vol_vertices", 0) * BYTES_VOL_VERTEX + d.get("vol_nee_walks", 0) * BYTES_VOL_NEE)
         pipeline = {"achieved": round(pipe_bytes / elapsed / 1e9, 2), "unit": "GB/s",
                     "frac": round(pipe_bytes / elapsed / 1e9 / HBM_PEAK_GBS, 5),
                     "algorithmic_bytes_per_step": int(pipe_bytes / a.steps),
@@ -436,6 +440,9 @@ def wavefront_roofline(pg, scene, integ, local, a, spp):
         "k_vvertex": (d["vol_vertex_ms"], d["vol_vertices"] * BYTES_VOL_VERTEX + d["vol_vertex_lookups"] * BYTES_DENSITY_LOOKUP,
                       d["vol_vertex_launches"], d["vol_vertex_lookups"]),
     }
+    if d.get("vol_nee_launches"):
+        kernels["k_vnee"] = (d["vol_nee_ms"], d["vol_nee_walks"] * BYTES_VOL_NEE + d["vol_nee_lookups"] * BYTES_DENSITY_LOOKUP,
+                             d["vol_nee_launches"], d["vol_nee_lookups"])
     measured, source = {}, None
     pmc = os.path.join(ROOT, "profiles", "pmc_volpath_latest.json")
     if os.path.exists(pmc):
@@ -472,7 +479,8 @@ def wavefront_roofline(pg, scene, integ, local, a, spp):
             "traffic_over_algorithmic": out[dom].get("traffic_over_algorithmic"),
             "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)), "avg_launch_ms": round(ms / max(launches, 1), 4),
             "bytes_model": {"k_vflight": f"{BYTES_VOL_FLIGHT} B state per flight + {BYTES_DENSITY_LOOKUP} B per density lookup",
-                            "k_vvertex": f"{BYTES_VOL_VERTEX} B state per interaction + {BYTES_DENSITY_LOOKUP} B per density lookup"},
+                            "k_vvertex": f"{BYTES_VOL_VERTEX} B state per interaction + {BYTES_DENSITY_LOOKUP} B per density lookup",
+                            "k_vnee": f"{BYTES_VOL_NEE} B per deferred walk slot + {BYTES_DENSITY_LOOKUP} B per density lookup"},
             "measured": f"calibration context after the timed region: {scene.width}x{scene.height} x {spp} spp final-render "
                         "pass with the job's tree, HIP events around every stage launch (one stream)",
             "kernels": out}

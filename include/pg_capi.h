@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define PG_ABI_VERSION 11
+#define PG_ABI_VERSION 12
 
 typedef int32_t pg_status;
 enum {
@@ -295,6 +295,12 @@ typedef struct pg_stats {
     uint64_t vol_vertex_launches;
     uint64_t vol_vertices;
     uint64_t vol_vertex_lookups;
+    /* ABI 12: the interactions' deferred transmittance walks (k_vnee: NEE shadow walks and emitter walks
+     * through media, each on its own counter sub-stream): device time, launches, slots walked, lookups */
+    double vol_nee_ms;
+    uint64_t vol_nee_launches;
+    uint64_t vol_nee_walks;
+    uint64_t vol_nee_lookups;
 } pg_stats;
 
 /* ---- lifecycle ---------------------------------------------------------------------- */
@@ -422,8 +428,9 @@ pg_status pg_comm_reduce_film(void *ctx, int32_t root);
 pg_status pg_comm_allreduce_f64(void *ctx, double *values, uint64_t n);
 /* The record exchange SURVEY.md §5/§8e names (north_star: "RCCL all-gather of records"), the
  * alternative to pg_splat_local_records + pg_comm_allreduce_tree_stats in the postprogression slot:
- * every rank's record count (ncclAllGather of one u64), then every rank's records (ncclAllGather,
- * padded to the largest count), then every rank splats ALL records into its building tree, in rank
+ * every rank's record count (ncclAllGather of one u64), then every rank's records (ncclAllGather in
+ * slices of at most 2^22 records per rank, padded to whole slices, into one reused buffer of
+ * world_size slices), and every rank splats ALL records into its building tree, slice by slice in rank
  * order.  Integer splat sums commute, so every rank ends with the tree one GPU builds from all
  * records, bit for bit -- the same tree as the statistics all-reduce.  counts_out (may be NULL):
  * world_size record counts.  The local records stay until pg_refit. */

@@ -105,7 +105,9 @@ class pg_stats(C.Structure):
                 # ABI 11: the volumetric wavefront's stages
                 ("vol_flight_ms", C.c_double), ("vol_flight_launches", C.c_uint64), ("vol_flights", C.c_uint64),
                 ("vol_flight_lookups", C.c_uint64), ("vol_vertex_ms", C.c_double),
-                ("vol_vertex_launches", C.c_uint64), ("vol_vertices", C.c_uint64), ("vol_vertex_lookups", C.c_uint64)]
+                ("vol_vertex_launches", C.c_uint64), ("vol_vertices", C.c_uint64), ("vol_vertex_lookups", C.c_uint64),
+                ("vol_nee_ms", C.c_double), ("vol_nee_launches", C.c_uint64), ("vol_nee_walks", C.c_uint64),
+                ("vol_nee_lookups", C.c_uint64)]
 
 
 def default_config(**overrides):
@@ -189,7 +191,7 @@ SIGNATURES = [
 ]
 
 
-PG_ABI_VERSION = 11  # include/pg_capi.h
+PG_ABI_VERSION = 12  # include/pg_capi.h
 PG_COMM_ID_BYTES = 128
 
 

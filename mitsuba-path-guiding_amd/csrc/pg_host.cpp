@@ -168,6 +168,11 @@ struct Lane {
 struct VolLane {
     hipStream_t stream = nullptr;
     hipEvent_t ready = nullptr;  // the counters' host copy landed
+    // the deferred transmittance walks (k_vnee) on a stream of their own, overlapping the next iteration's
+    // free flights (PG_VOL_NEE_OVERLAP): vdone = this iteration's interactions done, ndone = its walks done
+    hipStream_t nstream = nullptr;
+    hipEvent_t vdone = nullptr, ndone = nullptr;
+    bool npending = false;
     DevBuf state, items, counts, rad, ovf;
     DevBuf keys, sorted, hist;  // flight order keys of both flight queues, a sorted copy, histograms (PG_VOL_SORT)
     PinnedBuf host;
@@ -770,8 +775,12 @@ pg_status pg_destroy(void *ctx) {
     for (hipEvent_t &e : c->vw_ev)
         if (e) (void)hipEventDestroy(e);
     for (VolLane &l : c->vlanes) {
+        if (l.nstream) (void)hipStreamSynchronize(l.nstream);
         if (l.stream) (void)hipStreamSynchronize(l.stream);
         if (l.ready) (void)hipEventDestroy(l.ready);
+        if (l.vdone) (void)hipEventDestroy(l.vdone);
+        if (l.ndone) (void)hipEventDestroy(l.ndone);
+        if (l.nstream) (void)hipStreamDestroy(l.nstream);
         if (l.stream) (void)hipStreamDestroy(l.stream);
     }
     for (Lane &l : c->lanes) {
@@ -1144,6 +1153,24 @@ bool volWavefront() {
     const char *e = std::getenv("PG_VOL_WAVEFRONT");
     return e && *e ? std::atoi(e) != 0 : true;
 }
+// the interactions' transmittance walks (NEE shadow walks, emitter walks through media) as a stage of their
+// own (k_vnee, after each k_vvertex; PG_VOL_NEE_STAGE=1) or inline at the end of each k_vvertex interaction
+// (default): both give the same films and trees (the walks draw from their own sub-streams either way).  The
+// stage takes the walks out of k_vvertex (medium interactions at 3 waves/SIMD, 166 VGPRs, no scratch) but the
+// walks then run 45 % slower on their own: C5 328.8 / 326.4 Mpaths/s as a stage, 334.7 / 335.6 with the stage
+// overlapping the next iteration's flights, 373.7 / 373.9 inline on one box (profiles/r05c_vol_nee_stage/)
+bool volNeeStage() {
+    const char *e = std::getenv("PG_VOL_NEE_STAGE");
+    return e && *e ? std::atoi(e) != 0 : false;
+}
+// VolLane path state: VolWave's 13 float4 per slot; its queues (pg_volpath.hip)
+constexpr int kVolStateF4 = 14, kVolQueues = 8;
+// k_vnee of iteration i on the lane's second stream, concurrent with iteration i + 1's k_vflight (which reads
+// no state the walks write); k_vvertex of i + 1 waits for it.  PG_VOL_NEE_OVERLAP=0: on the lane's stream
+bool volNeeOverlap() {
+    const char *e = std::getenv("PG_VOL_NEE_OVERLAP");
+    return e && *e ? std::atoi(e) != 0 : true;
+}
 // below this many live paths a chunk's remaining paths finish in one k_vtail launch (PG_VOL_TAIL_PATHS): 2^17
 // with three lanes (C5 398.7 / 399.4 against 396.6 / 397.5 at 2^18, profiles/r04al_vol_tail/)
 uint32_t volTailPaths() {
@@ -1187,7 +1214,15 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
     auto laneVtx = [&](const VolLane &l) -> float4 * {
         return v.vtx ? v.vtx + (size_t)(&l - c->vlanes) * want * (size_t)maxV * PG_VTX_F4 : nullptr;
     };
-    const size_t cbytes = (size_t)PG_QSHARDS * 4 * 7;
+    const size_t cbytes = (size_t)PG_QSHARDS * 4 * kVolQueues;
+    const bool neeStage = volNeeStage(), neeOverlap = neeStage && volNeeOverlap() && !evt;
+    auto joinNee = [&](VolLane &l) -> pg_status {  // the lane's stream waits for its pending walks
+        if (l.npending) {
+            HIPC(c, hipStreamWaitEvent(l.stream, l.ndone, 0));
+            l.npending = false;
+        }
+        return PG_OK;
+    };
     const uint32_t sortMin = volSortMin();
     HIPC(c, hipEventRecord(c->pass_start, c->stream));  // lanes start after the context stream's work
     for (int li = 0; li < nl; ++li) {
@@ -1195,10 +1230,14 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         if (!l.stream) {
             HIPC(c, hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
             HIPC(c, hipEventCreateWithFlags(&l.ready, hipEventDisableTiming));
+            HIPC(c, hipStreamCreateWithFlags(&l.nstream, hipStreamNonBlocking));
+            HIPC(c, hipEventCreateWithFlags(&l.vdone, hipEventDisableTiming));
+            HIPC(c, hipEventCreateWithFlags(&l.ndone, hipEventDisableTiming));
         }
+        l.npending = false;
         if (l.cap < want) {
-            HIPC(c, l.state.alloc((size_t)want * 16 * 7));
-            HIPC(c, l.items.alloc((size_t)pg_queue_stride(want) * PG_QSHARDS * 4 * 7));
+            HIPC(c, l.state.alloc((size_t)want * 16 * kVolStateF4));
+            HIPC(c, l.items.alloc((size_t)pg_queue_stride(want) * PG_QSHARDS * 4 * kVolQueues));
             HIPC(c, l.rad.alloc((size_t)want * 16));
             l.cap = want;
         }
@@ -1217,7 +1256,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
     HIPC(c, hipEventRecord(c->film_order, c->stream));
     const uint32_t tail = volTailPaths();
     uint32_t next = 0, filmNext = 0;
-    auto views = [&](VolLane &l, VolDev &lv, VolWave &w, Queue *q) {  // q: 7 queues
+    auto views = [&](VolLane &l, VolDev &lv, VolWave &w, Queue *q) {  // q: kVolQueues queues
         lv = v;
         lv.rad = l.rad.as<float4>();
         lv.stack_ovf = l.ovf.as<uint32_t>();
@@ -1225,11 +1264,13 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         float4 *st = l.state.as<float4>();
         const size_t cap = l.cap;
         w = VolWave{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
-                    reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap};
-        // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices, 5/6: delta surface
+                    reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap, st + 7 * cap, st + 8 * cap, st + 9 * cap,
+                    st + 10 * cap, st + 11 * cap, st + 12 * cap, reinterpret_cast<uint32_t *>(st + 13 * cap)};
+        // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices, 5/6: delta surface,
+        // 7: deferred transmittance walks (k_vnee)
         const size_t qstride = (size_t)pg_queue_stride(l.cap) * PG_QSHARDS;
         const uint32_t stride = pg_queue_stride(l.np * l.nl);
-        for (int k = 0; k < 7; ++k)
+        for (int k = 0; k < kVolQueues; ++k)
             q[k] = Queue{l.items.as<uint32_t>() + k * qstride, l.counts.as<uint32_t>() + k * PG_QSHARDS, stride};
         if (sortMin)
             for (int k = 0; k < 2; ++k) q[k].keys = l.keys.as<uint16_t>() + k * qstride;
@@ -1255,7 +1296,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         HIPC(c, hipEventRecord(l.span.a, l.stream));
         VolDev lv;
         VolWave w;
-        Queue q[7];
+        Queue q[kVolQueues];
         views(l, lv, w, q);
         HIPC(c, hipMemsetAsync(l.counts.p, 0, cbytes, l.stream));
         pg_launch_vol_camera(l.stream, g, sc, lv, w, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, l.sample_base,
@@ -1308,11 +1349,12 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         };
         VolDev lv;
         VolWave w;
-        Queue q[7];
+        Queue q[kVolQueues];
         views(l, lv, w, q);
         const int cur = l.it & 1, nxt = cur ^ 1;
         const auto f = maxShard(cur), su = maxShard(2 + cur), sdl = maxShard(5 + cur);
         if (f.second + su.second + sdl.second <= tail) {
+            if (pg_status js = joinNee(l)) return js;
             if (f.second + su.second + sdl.second) {
                 pg_launch_vol_tail(l.stream, g, sc, lv, sd, w, q[cur], f.first, q[2 + cur], su.first, q[5 + cur],
                                    sdl.first);
@@ -1353,12 +1395,26 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         // shard bounds without a readback: a medium vertex came from a flight; a surface vertex from a
         // flight or from the previous iteration's interactions; no shard exceeds the queue stride
         const uint32_t mm = f.first, ms = std::min(q[0].stride, f.first + su.first + sdl.first);
+        // the previous iteration's walks write L: done before this iteration's interactions read it
+        if (pg_status js = joinNee(l)) return js;
+        if (neeStage) HIPC(c, hipMemsetAsync(q[7].counts, 0, PG_QSHARDS * 4, l.stream));
         pg_launch_vol_vertex(l.stream, g, sc, lv, sd, w, q[4], mm, q[2 + cur], ms, q[5 + cur], ms, q[nxt], q[2 + nxt],
-                             q[5 + nxt]);
+                             q[5 + nxt], neeStage ? &q[7] : nullptr);
+        if (evt) HIPC(c, hipEventRecord(c->vw_ev[2], l.stream));
+        // the deferred walks: at most one entry per path live in this iteration (<= ms per shard)
+        if (neeOverlap) {
+            HIPC(c, hipEventRecord(l.vdone, l.stream));
+            HIPC(c, hipStreamWaitEvent(l.nstream, l.vdone, 0));
+            pg_launch_vol_nee(l.nstream, g, sc, lv, w, q[7], ms);
+            HIPC(c, hipEventRecord(l.ndone, l.nstream));
+            l.npending = true;
+        } else if (neeStage) {
+            pg_launch_vol_nee(l.stream, g, sc, lv, w, q[7], ms);
+        }
         if (evt) {
-            HIPC(c, hipEventRecord(c->vw_ev[2], l.stream));
-            HIPC(c, hipEventSynchronize(c->vw_ev[2]));
-            float a = 0, b = 0;
+            HIPC(c, hipEventRecord(c->vw_ev[3], l.stream));
+            HIPC(c, hipEventSynchronize(c->vw_ev[3]));
+            float a = 0, b = 0, e = 0;
             if (f.first) {
                 HIPC(c, hipEventElapsedTime(&a, c->vw_ev[0], c->vw_ev[1]));
                 c->stats.vol_flight_ms += a;
@@ -1367,6 +1423,11 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
             HIPC(c, hipEventElapsedTime(&b, c->vw_ev[1], c->vw_ev[2]));
             c->stats.vol_vertex_ms += b;
             c->stats.vol_vertex_launches++;
+            if (neeStage) {
+                HIPC(c, hipEventElapsedTime(&e, c->vw_ev[2], c->vw_ev[3]));
+                c->stats.vol_nee_ms += e;
+                c->stats.vol_nee_launches++;
+            }
         }
         HIPC(c, hipGetLastError());
         ++l.it;
@@ -1521,8 +1582,10 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
         c->stats.paths += (uint64_t)np * nl;
     }
     HIPC(c, hipStreamSynchronize(c->stream));
-    unsigned long long st[7];
-    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 56, hipMemcpyDeviceToHost));
+    unsigned long long st[9];
+    HIPC(c, hipMemcpy(st, c->vol_work.as<uint8_t>() + 16, 72, hipMemcpyDeviceToHost));
+    c->stats.vol_nee_walks += st[7];
+    c->stats.vol_nee_lookups += st[8];
     c->stats.vol_flights += st[3];
     c->stats.vol_flight_lookups += st[4];
     c->stats.vol_vertices += st[5];
@@ -1553,7 +1616,9 @@ static void drainLanes(Ctx *c) {
     for (int li = 0; li < c->nlanes; ++li)
         if (c->lanes[li].stream) (void)hipStreamSynchronize(c->lanes[li].stream);
     for (VolLane &l : c->vlanes) {
+        if (l.nstream) (void)hipStreamSynchronize(l.nstream);
         if (l.stream) (void)hipStreamSynchronize(l.stream);
+        l.npending = false;
         if (l.span.a) (void)hipEventDestroy(l.span.a);
         if (l.span.b) (void)hipEventDestroy(l.span.b);
         l.span = EventPair{};
@@ -2181,17 +2246,29 @@ pg_status pg_comm_allgather_records(void *ctx, uint64_t *counts_out) {
     const uint64_t maxn = *std::max_element(counts.begin(), counts.end());
     if (counts_out) std::copy(counts.begin(), counts.end(), counts_out);
     if (maxn == 0) return PG_OK;
-    // 2. the records, each rank's block padded to the largest count (the send buffer is the local
-    //    record buffer, grown to maxn: its tail past the local count is never splatted)
+    // 2. the records, all-gathered in slices of at most kGatherSlice records per rank: round k gathers
+    //    every rank's records [k S, (k + 1) S) (the local record buffer, padded to whole slices, is the
+    //    send buffer) into ext_records (W S records, allocated once and reused by every round and every
+    //    iteration), and every rank's valid part of the round is splatted, in rank order, before the next
+    //    round overwrites it (same stream).  A single padded all-gather would need W x the largest count:
+    //    ~13.6 GB per rank, re-allocated each iteration, for C3's 16-spp pass at W = 8.  Integer sums:
+    //    the tree does not depend on the splat order.
+    uint64_t slice = 1ull << 22;  // 128 MiB of records per rank and round
+    if (const char *e = std::getenv("PG_GATHER_SLICE")) slice = std::max<uint64_t>(1, std::strtoull(e, nullptr, 10));  // tests
+    const uint64_t S = std::min<uint64_t>(maxn, slice), rounds = (maxn + S - 1) / S;
     pg_status st;
-    if ((st = ensureRecords(c, maxn))) return st;
-    HIPC(c, c->ext_records.alloc((size_t)W * maxn * sizeof(pg_record)));
-    NCCLC(c, ncclAllGather(c->records.p, c->ext_records.p, maxn * sizeof(pg_record), ncclUint8, c->comm, c->stream));
-    // 3. splat every rank's records (rank order; integer sums, so the order does not change the tree)
+    if ((st = ensureRecords(c, rounds * S))) return st;
+    HIPC(c, c->ext_records.alloc((size_t)W * S * sizeof(pg_record)));
     const SDDev sd = sdView(c);
-    for (int r = 0; r < W; ++r)
-        if (counts[r]) pg_launch_splat(c->stream, sd, c->ext_records.as<pg_record>() + (size_t)r * maxn, counts[r]);
-    HIPC(c, hipGetLastError());
+    for (uint64_t k = 0; k < rounds; ++k) {
+        NCCLC(c, ncclAllGather(c->records.as<pg_record>() + k * S, c->ext_records.p, S * sizeof(pg_record), ncclUint8,
+                               c->comm, c->stream));
+        for (int r = 0; r < W; ++r) {
+            const uint64_t lo = k * S, n = counts[r] > lo ? std::min(S, counts[r] - lo) : 0;
+            if (n) pg_launch_splat(c->stream, sd, c->ext_records.as<pg_record>() + (size_t)r * S, n);
+        }
+        HIPC(c, hipGetLastError());
+    }
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }

@@ -64,7 +64,8 @@ struct VolDev {
     float4 *rad;               // per work item (layer-major: item = layer * npix + lp), radiance
     uint32_t *next;            // work counter (zeroed by the launcher)
     unsigned long long *stats; // [0] segments (closest-hit rays), [1] NEE transmittance queries, [2] density lookups;
-                               // wavefront: [3] flights, [4] their lookups, [5] interactions, [6] their lookups
+                               // wavefront: [3] flights, [4] their lookups, [5] interactions, [6] their lookups,
+                               // [7] deferred walk entries (k_vnee), [8] their lookups
     uint32_t *stack_ovf;       // pg_stack_overflow_words(0) words
     float4 *vtx;               // guided training vertices [max_vertices][vtx_P][PG_VTX_F4] (PathDev::vtx layout)
     uint32_t vtx_P;            // slot stride of vtx (>= items per launch)
@@ -83,6 +84,11 @@ struct VolWave {
     float4 *L;   // (radiance, bits(training vertices written))
     uint4 *r;    // random stream (key, sample, next dimension, density lookups so far)
     float4 *mp;  // the medium interaction point of the current iteration's free flight
+    // deferred transmittance walks of the current iteration's interactions (pg_volpath.hip VDefer, k_vnee):
+    // NEE (shadow walk origin, dim), (emitter point, max crossings), (contribution, flags); emitter hit
+    // (walk origin, mint), (direction, dim), (contribution, medium | crossings)
+    float4 *n0, *n1, *n2, *h0, *h1, *h2;
+    uint32_t *nflags;  // which of them are valid, whether the path ended, its vertex (pg_volpath.hip deferFlags)
 };
 
 // Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).
@@ -166,7 +172,10 @@ void pg_launch_vol_flight(hipStream_t s, const GParams &g, const SceneDev &sc, c
                           const VolWave &w, Queue flight, uint32_t max_flight, Queue med, Queue surf, Queue dsurf);
 void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                           const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
-                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf);
+                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf, const Queue *nee);
+// the interactions' deferred transmittance walks (k_vnee); max_nee bounds every shard of `nee`
+void pg_launch_vol_nee(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w, Queue nee,
+                       uint32_t max_nee);
 void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                         const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf, Queue dsurf,
                         uint32_t max_dsurf);

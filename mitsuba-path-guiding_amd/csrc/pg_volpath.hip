@@ -55,6 +55,32 @@ struct VRng {
     __device__ __forceinline__ void next2(float &a, float &b) { rng2(key, sample, dim++, a, b); }
 };
 
+// Transmittance sub-streams (oracle/orc_volpath.h subStream): the NEE shadow walk (kind 0) and the
+// re-walk of a sampled ray that found a lit emitter through media (kind 1) draw from the counter stream
+// at dimensions 0x80000000 | dim << 16 | kind << 15 | j, dim = the main-stream dimension at which the
+// interaction drew its light sample / started its emitter walk.  The main stream then does not depend
+// on the walks, so the wavefront runs them as a stage of their own (k_vnee).
+__device__ __forceinline__ VRng subStream(uint32_t key, uint32_t sample, uint32_t dim, uint32_t kind) {
+    return VRng{key, sample, 0x80000000u | (dim << 16) | (kind << 15), 0};
+}
+
+// What an interaction leaves for its transmittance walks (k_vnee in the wavefront, resolveDeferred
+// right after the step in k_vtail / k_volpath): the emitter hit's contribution before the transmittance
+// of its walk (hit) and the NEE's contribution before the shadow walk's transmittance (nee), added to L
+// in that order; the NEE also joins the training snapshot of the interaction's vertex k.
+struct VDefer {
+    f3 nC, n1, n2;  // NEE: contribution, shadow walk from n1 to the emitter point n2
+    int nMedium, nMaxInter;
+    uint32_t nDim;
+    bool nee, nOnSurface;
+    f3 hC, hO, hD;  // emitter hit: contribution, the walk's first ray (origin, direction, mint)
+    float hMint;
+    int hMedium, hInter;  // the walk's starting medium and null-surface crossings
+    uint32_t hDim;
+    bool hit;
+    int k;  // training vertex of the interaction (-1: none)
+};
+
 // ---- HG phase function (hg.cpp:74-106) --------------------------------------------------------
 __device__ __forceinline__ float hgEval(float g, f3 wi, f3 wo) {
     float temp = 1.0f + g * g + 2.0f * g * dot(wi, wo);
@@ -458,12 +484,18 @@ struct ItsRef {  // the caller's intersection record: closest hit of the current
 };
 
 // rayIntersectAndLookForEmitter (progressive_volpath.cpp:401-460).  `its` gets the FIRST hit.  The
-// walk through null surfaces is done once without the medium; only when it ends on a lit emitter
-// is it walked again to estimate the transmittance of its segments (the reference estimates it
-// on every walk and discards it otherwise: same estimator, oracle/orc_volpath.h "lazy").
+// walk through null surfaces is done once without the medium; `value` is the emitted radiance of the lit
+// emitter it ends on (unattenuated), and when it crossed a medium the segments' transmittance is left to
+// emitterWalkT (walk: its first ray and crossings), on the walk's own sub-stream (oracle/orc_volpath.h:
+// the reference estimates the transmittance on every walk and discards it unless it ends on an emitter,
+// the same estimator).
 // exact: qdist = the whole walk's length (pg_config.volpath_exact_mis) instead of the last segment's
+struct EmWalk {
+    int medium, interactions;
+    bool anyMedium;
+};
 __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev &v, int medium, int maxInteractions, f3 o0, f3 d,
-                               float mint0, ItsRef &its, f3 &value, f3 &qn, float &qdist, int &qem, VRng &rng,
+                               float mint0, ItsRef &its, f3 &value, f3 &qn, float &qdist, int &qem, EmWalk &walk,
                                const TStack &stk, uint32_t &segs, bool exact) {
     value = mk1(0.f);
     qem = -1;
@@ -499,41 +531,43 @@ __device__ __forceinline__ void lookForEmitter(const SceneDev &sc, const VolDev 
     fetchHit(sc, tri, u, w, d, h);
     if (!(dot(h.shN, -d) > 0)) return;  // AreaLight::eval: back side emits nothing
     const GEmitter &E = sc.ems[em];
-    float T = 1.0f;
-    if (anyMedium) {  // second walk: the transmittance estimate of every segment in a medium
-        f3 oo = o0;
-        float mt = mint0;
-        int mm = medium;
-        for (int k = 0; k <= interactions; ++k) {
-            float tt, uu, ww;
-            uint32_t tr;
-            const bool hitR = closestHit(sc, oo, d, mt, __int_as_float(0x7f800000), tt, tr, uu, ww, stk);
-            segs++;
-            // the re-walk repeats the first walk's rays, so it hits the same surfaces; were a rounding
-            // difference to make it miss, tr would be ~0 and v.tmed[tr] / fetchHit would read 16 GB
-            // past their arrays (the round-3 C5 faults): end the estimate instead
-            if (!VCHK(hitR, 1, k)) {
-                T = 0.0f;
-                break;
-            }
-            if (mm >= 0) {
-                T *= mediumTransmittance(v, mm, oo, d, tt, rng);
-                if (T == 0) break;
-            }
-            const uint32_t tm = v.tmed[tr];
-            if (tm) {
-                Hit hh;
-                fetchHit(sc, tr, uu, ww, d, hh);
-                mm = targetMedium(tm, d, hh.geoN);
-            }
-            oo = advance(oo, d, tt);
-            mt = itsMinT(oo);
-        }
-    }
-    value = mk(E.radiance[0], E.radiance[1], E.radiance[2]) * T;
+    walk = EmWalk{medium, interactions, anyMedium};
+    value = mk(E.radiance[0], E.radiance[1], E.radiance[2]);
     qn = h.shN;
     qdist = exact ? walked + t : t;  // setQuery: the LAST segment's length (records.inl:170-178)
     qem = em;
+}
+// the transmittance of an emitter walk's segments in media: the walk's rays again (origins advanced the
+// same way, so the same surfaces), tracking every segment in a medium on the walk's sub-stream
+__device__ __forceinline__ float emitterWalkT(const SceneDev &sc, const VolDev &v, int medium, int interactions, f3 o0,
+                                              f3 d, float mint0, VRng &rng, const TStack &stk, uint32_t &segs) {
+    float T = 1.0f;
+    f3 oo = o0;
+    float mt = mint0;
+    int mm = medium;
+    for (int k = 0; k <= interactions; ++k) {
+        float tt, uu, ww;
+        uint32_t tr;
+        const bool hitR = closestHit(sc, oo, d, mt, __int_as_float(0x7f800000), tt, tr, uu, ww, stk);
+        segs++;
+        // the re-walk repeats the first walk's rays, so it hits the same surfaces; were a rounding
+        // difference to make it miss, tr would be ~0 and v.tmed[tr] / fetchHit would read 16 GB
+        // past their arrays (the round-3 C5 faults): end the estimate instead
+        if (!VCHK(hitR, 1, k)) return 0.0f;
+        if (mm >= 0) {
+            T *= mediumTransmittance(v, mm, oo, d, tt, rng);
+            if (T == 0) break;
+        }
+        const uint32_t tm = v.tmed[tr];
+        if (tm) {
+            Hit hh;
+            fetchHit(sc, tr, uu, ww, d, hh);
+            mm = targetMedium(tm, d, hh.geoN);
+        }
+        oo = advance(oo, d, tt);
+        mt = itsMinT(oo);
+    }
+    return T;
 }
 
 // Scene::pdfEmitterDirect for a found emitter (area.cpp pdfDirect + shape.cpp:117-126)
@@ -567,6 +601,60 @@ __device__ __forceinline__ void writeVertex(const VolDev &v, uint32_t item, uint
     vb[1] = f4(Tn, __uint_as_float(packCanonical(cu, cv)));
     vb[2] = f4(L, 0.0f);
     vb[3] = make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+}
+
+// Deferred walks go to registers (VDefer; SINK false: k_vtail / k_volpath resolve them after the step) or
+// straight to the slot's VolWave record (SINK true: k_vvertex, for k_vnee), so they hold no registers across
+// the rest of the interaction.  Record: n0 (shadow walk origin, dim), n1 (emitter point, max crossings), n2
+// (NEE contribution, (medium + 1) | onSurface << 16), h0 (emitter walk origin, mint), h1 (its direction,
+// dim), h2 (its contribution, (medium + 1) | crossings << 16); the flags word (nflags, written by k_vvertex
+// after the interaction) says which are valid, whether the path ended, and the vertex.
+template <bool SINK>
+__device__ __forceinline__ void deferNeeWalk(VDefer &df, const VolWave &w, uint32_t slot, f3 p1, f3 p2, bool onSurface,
+                                             int medium, int maxInter, uint32_t dim) {
+    df.nOnSurface = onSurface;
+    df.nMedium = medium;
+    if (SINK) {
+        w.n0[slot] = f4(p1, __uint_as_float(dim));
+        w.n1[slot] = f4(p2, __int_as_float(maxInter));
+    } else {
+        df.n1 = p1;
+        df.n2 = p2;
+        df.nMaxInter = maxInter;
+        df.nDim = dim;
+    }
+}
+template <bool SINK>
+__device__ __forceinline__ void deferNeeC(VDefer &df, const VolWave &w, uint32_t slot, f3 C) {
+    df.nee = true;
+    if (SINK)
+        w.n2[slot] = f4(C, __uint_as_float(((uint32_t)(df.nMedium + 1) & 0xFFFFu) | (df.nOnSurface ? 1u << 16 : 0u)));
+    else
+        df.nC = C;
+}
+// the emitter hit of a sampled ray: with a medium on its walk, its transmittance is deferred (the walk's
+// first ray and crossings); without, the walk's transmittance is 1 and C * 1 joins L now
+template <bool SINK>
+__device__ __forceinline__ void deferHit(VDefer &df, const VolWave &w, uint32_t slot, f3 &L, f3 C, const EmWalk &walk,
+                                         f3 o, f3 d, float mint, uint32_t dim) {
+    if (!walk.anyMedium) {
+        L = L + C * 1.0f;
+        return;
+    }
+    df.hit = true;
+    if (SINK) {
+        w.h0[slot] = f4(o, mint);
+        w.h1[slot] = f4(d, __uint_as_float(dim));
+        w.h2[slot] = f4(C, __uint_as_float(((uint32_t)(walk.medium + 1) & 0xFFFFu) | ((uint32_t)walk.interactions << 16)));
+        return;
+    }
+    df.hC = C;
+    df.hO = o;
+    df.hD = d;
+    df.hMint = mint;
+    df.hMedium = walk.medium;
+    df.hInter = walk.interactions;
+    df.hDim = dim;
 }
 
 // One iteration of the Li loop, in three parts that the megakernel (volStep) and the wavefront
@@ -604,10 +692,10 @@ __device__ __forceinline__ bool volRoulette(const GParams &g, VPath &P, VRng &rn
     P.scattered = true;
     return true;
 }
-template <bool GUIDED>
+template <bool GUIDED, bool SINK>
 __device__ __forceinline__ bool volMedium(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                                           VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
-                                          uint32_t &shadows, f3 mp) {
+                                          uint32_t &shadows, f3 mp, VDefer &df, const VolWave &wk) {
     const int maxDepth = g.max_depth;
     const int maxInter = maxDepth - P.depth - 1;
     const bool guiding = GUIDED && sd.built;
@@ -624,31 +712,30 @@ __device__ __forceinline__ bool volMedium(const GParams &g, const SceneDev &sc, 
         uint4 meta = make_uint4(0, 0, 0, 0);
         if (guiding) meta = sd.meta[sdLookup(sv, mp)];
         const float alphaM = alpha + (1 - alpha) * fabsf(hg);  // anisotropy-raised phase fraction (oracle)
-        // NEE: the light sample and its transmittance now; with guiding its MIS weight waits for the
-        // D-tree pdf of the light direction, resolved in one lockstep walk with the direction (sdDual)
+        // NEE: the light sample now, its shadow walk deferred (VDefer); with guiding its MIS weight waits
+        // for the D-tree pdf of the light direction, resolved in one lockstep walk with the direction (sdDual)
         f3 neeV = mk1(0.f), dD = mk1(0.f);
         float neePdf = 0, neePhase = 0;
         bool neePending = false;
         if (g.use_nee) {
+            const uint32_t ndim = rng.dim;  // the shadow walk's sub-stream
             float s0, s1;
             rng.next2(s0, s1);
             f3 ep;
             float dist, pdf;
-            f3 value = sampleEmitter(g, sc, mp, mk1(0.f), s0, s1, dD, dist, pdf, &ep);
+            const f3 value = sampleEmitter(g, sc, mp, mk1(0.f), s0, s1, dD, dist, pdf, &ep);
             if (pdf != 0) {
                 shadows++;
-                value = value * sceneTransmittance(sc, v, mp, false, ep, P.medium, maxInter, rng, stk, segs);
-                if (!isZero(value)) {
-                    const float phaseVal = hgEval(hg, wi, dD);
-                    if (phaseVal != 0) {
-                        if (guiding) {
-                            neeV = P.T * value * phaseVal;
-                            neePdf = pdf;
-                            neePhase = phaseVal;
-                            neePending = true;
-                        } else {
-                            P.L = P.L + P.T * value * (phaseVal * miWeight(pdf, phaseVal));
-                        }
+                const float phaseVal = hgEval(hg, wi, dD);
+                if (phaseVal != 0 && !isZero(value)) {
+                    deferNeeWalk<SINK>(df, wk, item, mp, ep, false, P.medium, maxInter, ndim);
+                    if (guiding) {
+                        neeV = P.T * value;
+                        neePdf = pdf;
+                        neePhase = phaseVal;
+                        neePending = true;
+                    } else {
+                        deferNeeC<SINK>(df, wk, item, (P.T * value) * (phaseVal * miWeight(pdf, phaseVal)));
                     }
                 }
             }
@@ -674,7 +761,8 @@ __device__ __forceinline__ bool volMedium(const GParams &g, const SceneDev &sc, 
             float au = 0, aw = 0, aPdf, dPdf, cu, cv;
             if (neePending) dirToCanonical(dD, au, aw);
             sdDual(sv, meta, neePending, au, aw, aPdf, true, mode == 2, bu, bw, cu, cv, dPdf);
-            if (neePending) P.L = P.L + neeV * miWeight(neePdf, alphaM * neePhase + (1 - alphaM) * aPdf);
+            if (neePending)
+                deferNeeC<SINK>(df, wk, item, neeV * (neePhase * miWeight(neePdf, alphaM * neePhase + (1 - alphaM) * aPdf)));
             if (mode == 2) {
                 wo = canonicalToDir(cu, cv);
                 phasePdf = hgEval(hg, wi, wo);
@@ -683,26 +771,32 @@ __device__ __forceinline__ bool volMedium(const GParams &g, const SceneDev &sc, 
             if (!(woPdf > 0)) return false;
             pw = phasePdf / woPdf;
         }
-        if (record && P.nv < (uint32_t)g.max_vertices) writeVertex(v, item, P.nv++, mp, wo, woPdf, P.T * pw, P.L);
+        if (record && P.nv < (uint32_t)g.max_vertices) {
+            df.k = (int)P.nv;
+            writeVertex(v, item, P.nv++, mp, wo, woPdf, P.T * pw, P.L);
+        }
         P.T = P.T * pw;
         P.o = mp;
         P.d = wo;
         f3 value, qn;
         float qdist;
         int qem;
-        lookForEmitter(sc, v, P.medium, maxInter, mp, wo, 0.0f, P.its, value, qn, qdist, qem, rng, stk, segs, g.exact_mis != 0);
+        EmWalk walk;
+        const uint32_t hdim = rng.dim;  // the emitter walk's sub-stream
+        lookForEmitter(sc, v, P.medium, maxInter, mp, wo, 0.0f, P.its, value, qn, qdist, qem, walk, stk, segs, g.exact_mis != 0);
         if (!isZero(value) && fminf(value.x, fminf(value.y, value.z)) > 0.f) {
             const float emitterPdf = g.use_nee ? pdfEmitter(g, sc, qem, mk1(0.f), wo, qn, qdist) : 0.0f;
-            P.L = P.L + P.T * value * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
+            const f3 C = (P.T * value) * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
+            deferHit<SINK>(df, wk, item, P.L, C, walk, mp, wo, 0.0f, hdim);
         }
         P.emission = false;
     }
     return volRoulette(g, P, rng);
 }
-template <bool GUIDED>
+template <bool GUIDED, bool SINK>
 __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                                            VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
-                                           uint32_t &shadows) {
+                                           uint32_t &shadows, VDefer &df, const VolWave &wk) {
     const int maxDepth = g.max_depth;
     const int maxInter = maxDepth - P.depth - 1;
     const bool guiding = GUIDED && sd.built;
@@ -730,27 +824,28 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
         float neePdf = 0, neeBp = 0;
         bool neePending = false;
         if (g.use_nee && (M.type & ESmooth)) {
+            const uint32_t ndim = rng.dim;  // the shadow walk's sub-stream
             float s0, s1;
             rng.next2(s0, s1);
             f3 ep;
             float dist, pdf;
-            f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, dD, dist, pdf, &ep);
+            const f3 value = sampleEmitter(g, sc, h.p, refN, s0, s1, dD, dist, pdf, &ep);
             if (pdf != 0) {
                 const int m2 = tm ? targetMedium(tm, dD, h.geoN) : P.medium;
                 shadows++;
-                value = value * sceneTransmittance(sc, v, h.p, true, ep, m2, maxInter, rng, stk, segs);
                 if (!isZero(value)) {
                     const f3 woL = h.sh.toLocal(dD);
                     const f3 f = bsdfEval(M, h.wi, woL);
                     if (!isZero(f) && (!g.strict_normals || dot(h.geoN, dD) * woL.z > 0)) {
                         const float bp = bsdfPdf(M, h.wi, woL);
+                        deferNeeWalk<SINK>(df, wk, item, h.p, ep, true, m2, maxInter, ndim);
                         if (guide) {
-                            neeV = P.T * value * f;
+                            neeV = (P.T * value) * f;
                             neePdf = pdf;
                             neeBp = bp;
                             neePending = true;
                         } else {
-                            P.L = P.L + P.T * value * f * miWeight(pdf, bp);
+                            deferNeeC<SINK>(df, wk, item, ((P.T * value) * f) * miWeight(pdf, bp));
                         }
                     }
                 }
@@ -781,7 +876,7 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
             float au = 0, aw = 0, aPdf, dPdf, cu, cv;
             if (neePending) dirToCanonical(dD, au, aw);
             sdDual(sv, meta, neePending, au, aw, aPdf, mode != 0, mode == 2, bu, bw, cu, cv, dPdf);
-            if (neePending) P.L = P.L + neeV * miWeight(neePdf, alpha * neeBp + (1 - alpha) * aPdf);
+            if (neePending) deferNeeC<SINK>(df, wk, item, neeV * miWeight(neePdf, alpha * neeBp + (1 - alpha) * aPdf));
             if (mode == 0) return false;
             if (mode == 1) {
                 woPdf = alpha * bs.pdf + (1 - alpha) * dPdf;
@@ -804,8 +899,10 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
         if (isZero(weight)) return false;
         const f3 wo = h.sh.toWorld(bs.wo);
         if (g.strict_normals && dot(h.geoN, wo) * bs.wo.z <= 0) return false;
-        if (record && !(bs.type & EDelta) && bs.type != ENull && P.nv < (uint32_t)g.max_vertices)
+        if (record && !(bs.type & EDelta) && bs.type != ENull && P.nv < (uint32_t)g.max_vertices) {
+            df.k = (int)P.nv;
             writeVertex(v, item, P.nv++, h.p, wo, woPdf, P.T * weight, P.L);
+        }
         P.o = h.p;
         P.d = wo;
         P.T = P.T * weight;
@@ -824,26 +921,73 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
         f3 value, qn;
         float qdist;
         int qem;
-        lookForEmitter(sc, v, P.medium, maxInter, h.p, wo, itsMinT(h.p), P.its, value, qn, qdist, qem, rng, stk, segs,
+        EmWalk walk;
+        const uint32_t hdim = rng.dim;  // the emitter walk's sub-stream
+        const float mint0 = itsMinT(h.p);
+        lookForEmitter(sc, v, P.medium, maxInter, h.p, wo, mint0, P.its, value, qn, qdist, qem, walk, stk, segs,
                        g.exact_mis != 0);
         if (!isZero(value)) {
             const float emitterPdf =
                 (g.use_nee && !(bs.type & EDelta)) ? pdfEmitter(g, sc, qem, refN, wo, qn, qdist) : 0.0f;
-            P.L = P.L + P.T * value * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
+            const f3 C = (P.T * value) * (g.use_nee ? miWeight(woPdf, emitterPdf) : 1.0f);
+            deferHit<SINK>(df, wk, item, P.L, C, walk, h.p, wo, mint0, hdim);
         }
         P.emission = false;
     }
     return volRoulette(g, P, rng);
 }
+// an interaction's deferred walks, in the oracle's order: the emitter hit, then the NEE (into L and into
+// the snapshot of the interaction's training vertex); each on its own sub-stream of the path's key
+__device__ __forceinline__ void resolveDeferred(const SceneDev &sc, const VolDev &v, const VDefer &df, uint32_t key,
+                                                uint32_t sample, uint32_t item, f3 &L, const TStack &stk,
+                                                uint32_t &segs, uint32_t &lookups) {
+    if (df.hit) {
+        VRng sub = subStream(key, sample, df.hDim, 1);
+        const float T = emitterWalkT(sc, v, df.hMedium, df.hInter, df.hO, df.hD, df.hMint, sub, stk, segs);
+        lookups += sub.lookups;
+        if (T != 0) L = L + df.hC * T;
+    }
+    if (df.nee) {
+        VRng sub = subStream(key, sample, df.nDim, 0);
+        const float tr = sceneTransmittance(sc, v, df.n1, df.nOnSurface, df.n2, df.nMedium, df.nMaxInter, sub, stk, segs);
+        lookups += sub.lookups;
+        if (tr != 0) {
+            const f3 add = df.nC * tr;
+            L = L + add;
+            if (df.k >= 0) {
+                float4 *vb = v.vtx + ((size_t)df.k * v.vtx_P + item) * PG_VTX_F4;
+                vb[2] = f4(xyz(vb[2]) + add, 0.0f);
+            }
+        }
+    }
+}
+__device__ __forceinline__ void clearDefer(VDefer &df) {
+    df.nee = df.hit = false;
+    df.k = -1;
+}
+
 template <bool GUIDED>
 __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                                         VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
-                                        uint32_t &shadows) {
+                                        uint32_t &shadows, VDefer &df) {
     if (!volDepthOk(g, P)) return false;
     f3 mp = mk1(0.f);
+    const VolWave none{};
     if (P.medium >= 0 && volFlight<GUIDED>(v, sd, P, rng, mp))
-        return volMedium<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows, mp);
-    return volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows);
+        return volMedium<GUIDED, false>(g, sc, v, sd, P, rng, stk, item, segs, shadows, mp, df, none);
+    return volSurface<GUIDED, false>(g, sc, v, sd, P, rng, stk, item, segs, shadows, df, none);
+}
+// one step with its walks resolved right away (k_vtail, k_volpath): the same arithmetic as the wavefront's
+// k_vvertex + k_vnee
+template <bool GUIDED>
+__device__ __forceinline__ bool volStepResolved(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                                                VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
+                                                uint32_t &shadows) {
+    VDefer df;
+    clearDefer(df);
+    const bool alive = volStep<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows, df);
+    if (df.hit || df.nee) resolveDeferred(sc, v, df, rng.key, rng.sample, item, P.L, stk, segs, rng.lookups);
+    return alive;
 }
 
 // the camera ray of work item `item` (PerspectiveCamera::sampleRay, perspective.cpp:271-298) and its
@@ -908,6 +1052,40 @@ __device__ __forceinline__ void storePath(const VolWave &w, uint32_t slot, const
     w.L[slot] = f4(P.L, __uint_as_float(P.nv));
     w.r[slot] = make_uint4(rng.key, rng.sample, rng.dim, rng.lookups);
 }
+// the flags word of a slot's deferred record (VolWave nflags): nee | hit << 1 | ended << 2 | (vertex + 1) << 8
+__device__ __forceinline__ uint32_t deferFlags(const VDefer &df, bool ended) {
+    return (df.nee ? 1u : 0u) | (df.hit ? 2u : 0u) | (ended ? 4u : 0u) | ((uint32_t)(df.k + 1) << 8);
+}
+__device__ __forceinline__ void loadDefer(const VolWave &w, uint32_t slot, VDefer &df, bool &ended) {
+    const uint32_t flags = w.nflags[slot];
+    df.nee = flags & 1u;
+    df.hit = (flags >> 1) & 1u;
+    ended = (flags >> 2) & 1u;
+    df.k = (int)(flags >> 8) - 1;
+    if (df.nee) {
+        const float4 a = w.n0[slot], b = w.n1[slot], c = w.n2[slot];
+        df.n1 = xyz(a);
+        df.nDim = __float_as_uint(a.w);
+        df.n2 = xyz(b);
+        df.nMaxInter = __float_as_int(b.w);
+        df.nC = xyz(c);
+        const uint32_t m = __float_as_uint(c.w);
+        df.nMedium = (int)(m & 0xFFFFu) - 1;
+        df.nOnSurface = (m >> 16) & 1u;
+    }
+    if (df.hit) {
+        const float4 a = w.h0[slot], b = w.h1[slot], e = w.h2[slot];
+        df.hO = xyz(a);
+        df.hMint = a.w;
+        df.hD = xyz(b);
+        df.hDim = __float_as_uint(b.w);
+        df.hC = xyz(e);
+        const uint32_t m = __float_as_uint(e.w);
+        df.hMedium = (int)(m & 0xFFFFu) - 1;
+        df.hInter = (int)(m >> 16);
+    }
+}
+
 // wave sums of the per-thread counters, one atomic each per wave
 __device__ __forceinline__ void volStats(const VolDev &v, uint32_t segs, uint32_t shadows, uint32_t lookups) {
     unsigned long long s0 = segs, s1 = shadows, s2 = lookups;
@@ -1077,16 +1255,31 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
     volStageStats(v, 3, flights, lookups);
 }
 
-// interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices
-template <bool GUIDED>
-__global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
+// interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices.  KIND 2: both
+// in one launch; KIND 0 / 1: the medium / surface blocks only, as launches of their own (PG_VOL_SPLIT_VERTEX,
+// default), so each gets its own register budget: with the walks deferred to k_vnee the medium kernel fits
+// 3 waves per SIMD without scratch (PG_VMEDIUM_WAVES), the surface kernel's BSDFs need more
+#ifndef PG_VMEDIUM_WAVES
+#define PG_VMEDIUM_WAVES 3
+#endif
+#ifndef PG_VSURFACE_WAVES
+#define PG_VSURFACE_WAVES PG_VOL_WAVES
+#endif
+template <bool NEE_STAGE, int KIND>
+struct VVertexWaves {  // the inline walks (PG_VOL_NEE_STAGE=0, A/B) keep round 4's budget
+    static constexpr int value = !NEE_STAGE ? PG_VVERTEX_WAVES
+                                            : (KIND == 0 ? PG_VMEDIUM_WAVES : (KIND == 1 ? PG_VSURFACE_WAVES : PG_VVERTEX_WAVES));
+};
+template <bool GUIDED, bool NEE_STAGE, int KIND>
+__global__ __launch_bounds__(TRACE_BLOCK, (VVertexWaves<NEE_STAGE, KIND>::value)) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
                                                                        VolWave w, Queue qm, Queue qs, Queue qd,
                                                                        uint32_t mblocks, uint32_t dblocks, Queue nf,
-                                                                       Queue ns, Queue nd) {
+                                                                       Queue ns, Queue nd, Queue qn) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     const TStack stk = threadStack(stack, v.stack_ovf);
     // blocks [0, mblocks): medium vertices; [mblocks, mblocks + dblocks): delta surfaces; the rest: surfaces
-    const bool medium = blockIdx.x < mblocks, delta = !medium && blockIdx.x < mblocks + dblocks;
+    const bool medium = KIND == 0 || (KIND == 2 && blockIdx.x < mblocks);
+    const bool delta = !medium && blockIdx.x < mblocks + dblocks;
     const uint32_t b = medium ? blockIdx.x : (delta ? blockIdx.x - mblocks : blockIdx.x - mblocks - dblocks);
     const uint32_t nb = medium ? mblocks : (delta ? dblocks : gridDim.x - mblocks - dblocks);
     const Queue &q = medium ? qm : (delta ? qd : qs);
@@ -1095,7 +1288,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
     uint32_t segs = 0, shadows = 0, lookups = 0, vertices = 0, vlookups = 0;
     for (uint32_t base = (b / PG_QSHARDS) * TRACE_BLOCK; base < n; base += rows * TRACE_BLOCK) {
         const uint32_t i = base + threadIdx.x;
-        bool toF = false, toS = false, cheap = false;
+        bool toF = false, toS = false, cheap = false, toN = false;
         uint32_t slot = 0;
         uint16_t key = 0;
         if (i < n) {
@@ -1104,11 +1297,25 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
             VRng rng;
             loadPath(w, slot, P, rng);
             const uint32_t l0 = rng.lookups;
-            const bool alive = medium ? volMedium<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, xyz(w.mp[slot]))
-                                      : volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+            VDefer df;
+            clearDefer(df);
+            bool alive;
+            if (KIND == 0 || (KIND == 2 && medium))
+                alive = volMedium<GUIDED, NEE_STAGE>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, xyz(w.mp[slot]), df, w);
+            else
+                alive = volSurface<GUIDED, NEE_STAGE>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, df, w);
             vertices++;
+            const bool ended = !(alive && volDepthOk(g, P));
+            if (df.hit || df.nee) {
+                if (NEE_STAGE) {  // the record is in the slot's VolWave entries; k_vnee walks it after this launch
+                    w.nflags[slot] = deferFlags(df, ended);
+                    toN = true;
+                } else {
+                    resolveDeferred(sc, v, df, rng.key, rng.sample, slot, P.L, stk, segs, rng.lookups);
+                }
+            }
             vlookups += rng.lookups - l0;
-            if (alive && volDepthOk(g, P)) {
+            if (!ended) {
                 storePath(w, slot, P, rng);
                 toF = P.medium >= 0;
                 toS = !toF;
@@ -1120,9 +1327,40 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VVERTEX_WAVES) void k_vvertex(GPara
         }
         flightAppend(toF, slot, key, nf, sh);
         surfAppend(toS, cheap, slot, ns, nd, sh);
+        if (NEE_STAGE) waveAppend(toN, slot, qn.items + (size_t)sh * qn.stride, qn.counts + sh);
     }
     volStats(v, segs, shadows, lookups);
     volStageStats(v, 5, vertices, vlookups);
+}
+
+// the interactions' deferred transmittance walks (VDefer, stored per slot by k_vvertex): the emitter hit's
+// walk, then the NEE's shadow walk, each on its sub-stream, their contributions into the path's L (or, for
+// a path that ended at that interaction, its output radiance) and the NEE into its vertex's snapshot
+#ifndef PG_VNEE_WAVES
+#define PG_VNEE_WAVES 3
+#endif
+template <bool GUIDED>
+__global__ __launch_bounds__(TRACE_BLOCK, PG_VNEE_WAVES) void k_vnee(GParams g, SceneDev sc, VolDev v, VolWave w, Queue qn) {
+    __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
+    const TStack stk = threadStack(stack, v.stack_ovf);
+    const uint32_t sh = blockIdx.x & (PG_QSHARDS - 1), rows = gridDim.x / PG_QSHARDS;
+    const uint32_t n = qn.counts[sh];
+    uint32_t segs = 0, walks = 0, lookups = 0;
+    for (uint32_t i = (blockIdx.x / PG_QSHARDS) * TRACE_BLOCK + threadIdx.x; i < n; i += rows * TRACE_BLOCK) {
+        const uint32_t slot = qn.items[(size_t)sh * qn.stride + i];
+        bool ended;
+        VDefer df;
+        loadDefer(w, slot, df, ended);
+        const uint4 r = w.r[slot];  // key and sample (constant over the path's life)
+        float4 *dst = ended ? v.rad + slot : w.L + slot;
+        const float4 l4 = *dst;
+        f3 L = xyz(l4);
+        resolveDeferred(sc, v, df, r.x, r.y, slot, L, stk, segs, lookups);
+        *dst = f4(L, l4.w);
+        walks++;
+    }
+    volStats(v, segs, 0, lookups);
+    volStageStats(v, 7, walks, lookups);
 }
 
 // the chunk's last paths: each thread runs one to its end (paths of `qf` start with their flight, those
@@ -1146,8 +1384,14 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vtail(GParams g, 
         VPath P;
         VRng rng;
         loadPath(w, slot, P, rng);
-        bool alive = flight || volSurface<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
-        while (alive) alive = volStep<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+        bool alive = flight;
+        if (!flight) {
+            VDefer df;
+            clearDefer(df);
+            alive = volSurface<GUIDED, false>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, df, w);
+            if (df.hit || df.nee) resolveDeferred(sc, v, df, rng.key, rng.sample, slot, P.L, stk, segs, rng.lookups);
+        }
+        while (alive) alive = volStepResolved<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
         volEnd(v, slot, P, rng, lookups);
     }
     volStats(v, segs, shadows, lookups);
@@ -1185,20 +1429,42 @@ void pg_launch_vol_flight(hipStream_t s, const GParams &g, const SceneDev &sc, c
 }
 void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                           const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
-                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf) {
+                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf, const Queue *nee) {
     // the three block ranges within TRACE_MAX_BLOCKS (the traversal stacks' overflow ring)
     const uint32_t cap = TRACE_MAX_BLOCKS / PG_QSHARDS / 4;
     const uint32_t mr = max_med ? vrows(max_med, cap) : 0;
     const uint32_t sr = max_surf ? vrows(max_surf, cap) : 0;
     const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
     if (mr + sr + dr == 0) return;
-    const dim3 grid(PG_QSHARDS * (mr + dr + sr));
+    const Queue qn = nee ? *nee : Queue{};
+    const char *se = std::getenv("PG_VOL_SPLIT_VERTEX");  // read per launch: tests switch it within a process
+    const bool split = !(se && *se && std::atoi(se) == 0);
+#define PG_VV(GU, NS, KIND, ROWS, MB)                                                                                \
+    hipLaunchKernelGGL((k_vvertex<GU, NS, KIND>), dim3(PG_QSHARDS * (ROWS)), dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, \
+                       med, surf, dsurf, MB, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf, qn)
+#define PG_VV_ALL(GU, NS)                                                                                            \
+    if (!split) {                                                                                                    \
+        PG_VV(GU, NS, 2, mr + dr + sr, PG_QSHARDS * mr);                                                             \
+    } else {                                                                                                         \
+        if (mr) PG_VV(GU, NS, 0, mr, PG_QSHARDS * mr);                                                               \
+        if (dr + sr) PG_VV(GU, NS, 1, dr + sr, 0u);                                                                  \
+    }
+    if (g.guiding) {
+        if (nee) { PG_VV_ALL(true, true) } else { PG_VV_ALL(true, false) }
+    } else {
+        if (nee) { PG_VV_ALL(false, true) } else { PG_VV_ALL(false, false) }
+    }
+#undef PG_VV_ALL
+#undef PG_VV
+}
+void pg_launch_vol_nee(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w, Queue nee,
+                       uint32_t max_nee) {
+    if (!max_nee) return;
+    const dim3 grid(PG_QSHARDS * vrows(max_nee, TRACE_MAX_BLOCKS / PG_QSHARDS));
     if (g.guiding)
-        hipLaunchKernelGGL(k_vvertex<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, dsurf,
-                           PG_QSHARDS * mr, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf);
+        hipLaunchKernelGGL(k_vnee<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, w, nee);
     else
-        hipLaunchKernelGGL(k_vvertex<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, med, surf, dsurf,
-                           PG_QSHARDS * mr, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf);
+        hipLaunchKernelGGL(k_vnee<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, w, nee);
 }
 void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                         const VolWave &w, Queue flight, uint32_t max_flight, Queue surf, uint32_t max_surf, Queue dsurf,
@@ -1254,7 +1520,7 @@ __global__ __launch_bounds__(VOL_BLOCK, PG_VOL_WAVES) void k_volpath(GParams g, 
             }
         }
         if (!__any(alive)) break;
-        if (alive && !volStep<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows)) {
+        if (alive && !volStepResolved<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows)) {
 #if PG_VOL_CHECK
             if (VCHK(item < nitems, 3, item))
 #endif

@@ -27,6 +27,33 @@ inline float miWeightV(float a, float b) {
     return a / (a + b);
 }
 
+// Transmittance sub-streams (round 5).  Every transmittance estimate an interaction
+// makes -- the NEE shadow walk (Scene::evalTransmittance) and the re-walk of a phase/BSDF-sampled ray that
+// found a lit emitter through media (rayIntersectAndLookForEmitter) -- draws from a counter sub-stream of
+// its own instead of the path's sequential stream: dimensions 0x80000000 | dim << 16 | kind << 15 | j,
+// where dim is the main-stream dimension at which the interaction drew its light sample (kind 0, NEE) or
+// started its emitter walk (kind 1), and j counts the walk's draws (j < 2^15; dim < 2^15 -- a path with
+// more main-stream draws than that reuses sub-stream dimensions 2^15 apart).  The main stream then does
+// not depend on how many numbers a walk used, so the GPU runs the walks as a stage of its own after the
+// interactions (pg_volpath.hip k_vnee).  Per interaction the contributions enter L in a fixed order: the
+// emitter hit (its product T Le w, then times the walk's transmittance), then the NEE (its product
+// T value (f mis), then times the shadow walk's transmittance); the NEE joins the vertex's training
+// snapshot, the emitter hit does not (it is radiance along the sampled direction).
+inline SeqRng subStream(const SeqRng &rng, uint32_t dim, uint32_t kind) {
+    SeqRng s;
+    s.r = rng.r;
+    s.dim = 0x80000000u | (dim << 16) | (kind << 15);
+    return s;
+}
+// a pending NEE of one interaction: its contribution before the shadow walk's transmittance
+struct PendingNee {
+    bool valid = false;
+    V3 C, p1, p2;
+    bool p1OnSurface = false;
+    int medium = -1, maxInter = 0;
+    uint32_t dim = 0;
+};
+
 inline bool isMediumTransition(const pg_shape &sh) { return sh.interior_medium >= 0 || sh.exterior_medium >= 0; }
 // Intersection::getTargetMedium(d): exterior when d leaves through the normal's side
 inline int targetMedium(const pg_shape &sh, V3 d, V3 n) { return dot(d, n) > 0 ? sh.exterior_medium : sh.interior_medium; }
@@ -75,7 +102,8 @@ inline float sceneTransmittance(const Scene &S, V3 p1, bool p1OnSurface, V3 p2, 
 }
 
 struct EmitterQuery {
-    V3 value;         // attenuated emitted radiance (0: none)
+    V3 value;         // emitted radiance of the emitter the walk ended on (0: none), NOT attenuated
+    float T = 1.0f;   // the walk's transmittance (its own sub-stream, kind 1)
     V3 n, d;          // setQuery: emitter shading normal, last segment direction
     float dist = 0;   // setQuery: length of the LAST segment (the reference's dRec.dist)
     int emitter = -1;
@@ -85,10 +113,12 @@ struct EmitterQuery {
 // null surfaces (updating the medium) to find an emitter behind them
 // exact: q.dist = the whole walk's length (pg_config.volpath_exact_mis; unbiased MIS) instead of the
 // reference's last segment
-inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInteractions, Ray ray, Its &its,
+inline void lookForEmitter(const Scene &S, const SeqRng &main, int medium, int maxInteractions, Ray ray, Its &its,
                            EmitterQuery &q, bool lazy, bool grid, VolCounters &cnt, bool exact = false) {
     q.value = V3(0.f);
+    q.T = 1.0f;
     q.emitter = -1;
+    SeqRng rng = subStream(main, main.dim, 1);
     Its its2;
     Its *cur = &its;
     float T = 1.0f, walked = 0.0f;
@@ -106,12 +136,11 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
         const float segT = surface ? cur->t : kInf;
         if (medium >= 0) {
             if (lazy) segs.push_back({ray.o, segT, medium});
-            else T *= S.media[medium].transmittance(grid, ray.o, ray.d, 0.0f, segT, rng);
+            else if (T != 0) T *= S.media[medium].transmittance(grid, ray.o, ray.d, 0.0f, segT, rng);  // lazy's draws
         }
         if (!surface) break;
         const pg_shape &sh = S.shapes[cur->shape];
         if (interactions == maxInteractions || !(S.mats[sh.material].type & ENull) || sh.emitter >= 0) break;
-        if (!lazy && T == 0) return;
         if (isMediumTransition(sh)) medium = targetMedium(sh, ray.d, cur->geoN);
         walked += cur->t;
         ray.o = ray.o + ray.d * cur->t;
@@ -129,7 +158,8 @@ inline void lookForEmitter(const Scene &S, SeqRng &rng, int medium, int maxInter
             if (T == 0) break;
         }
     }
-    q.value = Le * T;
+    q.value = Le;
+    q.T = T;
     q.n = cur->sh.n;
     q.d = ray.d;
     q.dist = exact ? walked + cur->t : cur->t;
@@ -199,6 +229,17 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
     bool emission = true;  // RadianceQueryRecord::ERadiance; ERadianceNoEmission after a scattering event
     int depth = 1;
     auto maxInter = [&](int dep) { return maxDepth - dep - 1; };
+    // an interaction's NEE, once its emitter hit is in L: the shadow walk's transmittance on the NEE's
+    // sub-stream, the contribution into L and into the training snapshot of the interaction's vertex k
+    auto resolveNee = [&](const PendingNee &n, int k) {
+        if (!n.valid) return;
+        SeqRng sub = subStream(rng, n.dim, 0);
+        const float tr = sceneTransmittance(S, n.p1, n.p1OnSurface, n.p2, true, n.medium, n.maxInter, sub, grid);
+        if (tr == 0) return;
+        const V3 add = n.C * tr;
+        L += add;
+        if (k >= 0) vtx[k].Lat += add;
+    };
 
     while (depth <= maxDepth || maxDepth < 0) {
         float mt = 0;
@@ -229,7 +270,9 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
             // and compounds over the many vertices of a dense forward-scattering walk (a = 0.5 at
             // g = 0.8: 2x the unguided RMSE on C5 from a few paths with weights near 2^k)
             const float alphaM = alpha + (1 - alpha) * std::fabs(M.g);
+            PendingNee nee;
             if (cfg.use_nee) {
+                const uint32_t ndim = rng.dim;  // the NEE's transmittance sub-stream (kind 0)
                 float s0, s1;
                 rng.next2(s0, s1);
                 DirectRec dr;
@@ -238,13 +281,11 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 V3 value = sampleEmitterNoVis(S, dr, s0, s1);
                 if (dr.pdf != 0) {
                     cnt.shadow++;
-                    value = value * sceneTransmittance(S, mp, false, dr.p, true, medium, maxInter(depth), rng, grid);
-                    if (!isZero(value)) {
-                        const float phaseVal = hgEval(M.g, wi, dr.d);
-                        if (phaseVal != 0) {
-                            const float mixPdf = dt ? alphaM * phaseVal + (1 - alphaM) * SDTree::pdfDir(*dt, dr.d) : phaseVal;
-                            L += T * value * (phaseVal * miWeightV(dr.pdf, mixPdf));
-                        }
+                    const float phaseVal = hgEval(M.g, wi, dr.d);
+                    if (phaseVal != 0 && !isZero(value)) {
+                        const float mixPdf = dt ? alphaM * phaseVal + (1 - alphaM) * SDTree::pdfDir(*dt, dr.d) : phaseVal;
+                        nee = PendingNee{true, (T * value) * (phaseVal * miWeightV(dr.pdf, mixPdf)), mp, dr.p, false,
+                                         medium, maxInter(depth), ndim};
                     }
                 }
             }
@@ -265,10 +306,17 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 wo = SDTree::sampleDir(*dt, g0, g1, dPdf);
                 phasePdf = hgEval(M.g, wi, wo);
                 woPdf = alphaM * phasePdf + (1 - alphaM) * dPdf;
-                if (!(woPdf > 0)) break;
+                if (!(woPdf > 0)) {
+                    resolveNee(nee, -1);
+                    break;
+                }
                 pw = phasePdf / woPdf;
             }
-            if (recs && nv < maxV) vtx[nv++] = VVtx{mp, wo, T * pw, L, woPdf};
+            int k = -1;
+            if (recs && nv < maxV) {
+                k = nv;
+                vtx[nv++] = VVtx{mp, wo, T * pw, L, woPdf};
+            }
             T *= pw;
             ray = Ray{mp, wo, 0.0f, kInf};
             EmitterQuery q;
@@ -277,8 +325,9 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
             if (!isZero(q.value) && std::min(q.value.x, std::min(q.value.y, q.value.z)) > 0.f) {
                 const float emitterPdf = cfg.use_nee ? pdfEmitterDirect(S, q.emitter, V3(0.f), q.d, q.n, q.dist) : 0.0f;
                 const float w = cfg.use_nee ? miWeightV(woPdf, emitterPdf) : 1.0f;
-                L += T * q.value * w;
+                if (q.T != 0) L += ((T * q.value) * w) * q.T;
             }
+            resolveNee(nee, k);
             emission = false;
         } else {
             // ---- surface interaction (progressive_volpath.cpp:197-352)
@@ -291,7 +340,9 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
             const V3 refN = (Mt.type & (ETransmission | EBackSide)) == 0 ? its.sh.n : V3(0.f);
             const bool guidable = guiding && (Mt.type & ESmooth) && !(Mt.type & EDelta);
             const DTreeW *dt = guidable ? &tree->dtrees[tree->lookup(its.p)] : nullptr;
+            PendingNee nee;
             if (cfg.use_nee && (Mt.type & ESmooth)) {
+                const uint32_t ndim = rng.dim;  // the NEE's transmittance sub-stream (kind 0)
                 float s0, s1;
                 rng.next2(s0, s1);
                 DirectRec dr;
@@ -301,14 +352,14 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 if (dr.pdf != 0) {
                     const int med = isMediumTransition(sh) ? targetMedium(sh, dr.d, its.geoN) : medium;
                     cnt.shadow++;
-                    value = value * sceneTransmittance(S, its.p, true, dr.p, true, med, maxInter(depth), rng, grid);
                     if (!isZero(value)) {
                         const V3 woL = its.toLocal(dr.d);
                         const V3 bsdfVal = bsdfEval(Mt, its.wi, woL);
                         if (!isZero(bsdfVal) && (!cfg.strict_normals || dot(its.geoN, dr.d) * woL.z > 0)) {
                             float bp = bsdfPdf(Mt, its.wi, woL);
                             if (dt) bp = alpha * bp + (1 - alpha) * SDTree::pdfDir(*dt, dr.d);
-                            L += T * value * bsdfVal * miWeightV(dr.pdf, bp);
+                            nee = PendingNee{true, ((T * value) * bsdfVal) * miWeightV(dr.pdf, bp), its.p, dr.p, true, med,
+                                             maxInter(depth), ndim};
                         }
                     }
                 }
@@ -324,7 +375,10 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 woPdf = bs.pdf;
             } else if (rng.next1() < alpha) {
                 weight = bsdfSample(Mt, its.wi, b0, b1, b2, bs);
-                if (isZero(weight)) break;
+                if (isZero(weight)) {
+                    resolveNee(nee, -1);
+                    break;
+                }
                 woPdf = alpha * bs.pdf + (1 - alpha) * SDTree::pdfDir(*dt, its.toWorld(bs.wo));
                 weight = weight * (bs.pdf / woPdf);
             } else {
@@ -335,7 +389,10 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                 const V3 f = bsdfEval(Mt, its.wi, woL);
                 const float bp = bsdfPdf(Mt, its.wi, woL);
                 woPdf = alpha * bp + (1 - alpha) * dPdf;
-                if (!(woPdf > 0) || isZero(f)) break;
+                if (!(woPdf > 0) || isZero(f)) {
+                    resolveNee(nee, -1);
+                    break;
+                }
                 weight = f / woPdf;
                 bs.wo = woL;
                 bs.pdf = bp;
@@ -344,17 +401,27 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                                       : EGlossyTransmission;
                 bs.eta = refl ? 1.0f : (its.wi.z > 0 ? Mt.eta : Mt.invEta);
             }
-            if (isZero(weight)) break;
+            if (isZero(weight)) {
+                resolveNee(nee, -1);
+                break;
+            }
             const V3 wo = its.toWorld(bs.wo);
-            if (cfg.strict_normals && dot(its.geoN, wo) * bs.wo.z <= 0) break;
-            if (recs && !(bs.sampledType & EDelta) && bs.sampledType != ENull && nv < maxV)
+            if (cfg.strict_normals && dot(its.geoN, wo) * bs.wo.z <= 0) {
+                resolveNee(nee, -1);
+                break;
+            }
+            int k = -1;
+            if (recs && !(bs.sampledType & EDelta) && bs.sampledType != ENull && nv < maxV) {
+                k = nv;
                 vtx[nv++] = VVtx{its.p, wo, T * weight, L, woPdf};
+            }
             const V3 itsP = its.p, itsGeoN = its.geoN;
             ray = Ray{itsP, wo, kEpsilon, kInf};
             T *= weight;
             eta *= bs.eta;
             if (isMediumTransition(sh)) medium = targetMedium(sh, wo, itsGeoN);
             if (bs.sampledType == ENull) {  // index-matched boundary: continue straight through
+                resolveNee(nee, k);  // (a null BSDF has no smooth lobe: never an NEE here)
                 emission = !scattered;
                 if (!S.intersect(ray, its)) its.t = kInf;
                 cnt.segments++;
@@ -369,8 +436,9 @@ inline V3 VolLi(const Scene &S, const pg_config &cfg, SeqRng &rng, Ray ray, VolC
                                              ? pdfEmitterDirect(S, q.emitter, refN, q.d, q.n, q.dist)
                                              : 0.0f;
                 const float w = cfg.use_nee ? miWeightV(woPdf, emitterPdf) : 1.0f;
-                L += T * q.value * w;
+                if (q.T != 0) L += ((T * q.value) * w) * q.T;
             }
+            resolveNee(nee, k);
             emission = false;
         }
         if (depth++ >= cfg.rr_depth) {

@@ -32,7 +32,7 @@ def test_library_exports_every_symbol(pg):
     out = subprocess.run(["nm", "-D", "--defined-only", pg.capi.LIB_PATH], capture_output=True, text=True).stdout
     for name in declared_functions():
         assert re.search(rf"\bT {name}\b", out), name
-    assert lib.pg_abi_version() == pg.capi.PG_ABI_VERSION == 11
+    assert lib.pg_abi_version() == pg.capi.PG_ABI_VERSION == 12
 
 
 def test_struct_layouts_match_header(pg):

@@ -53,6 +53,52 @@ def test_single_rank_communicator_is_identity(pg):
     t2, f2 = _train(pg, sc, True, mode="allgather")
     assert np.array_equal(t0, t2)
     assert np.array_equal(f0[0], f2[0])
+    # the all-gather in many slices (pg_comm_allgather_records: rounds of PG_GATHER_SLICE records per rank
+    # through one reused buffer, the last round padded): the same tree
+    os.environ["PG_GATHER_SLICE"] = "777"
+    try:
+        t3, f3 = _train(pg, sc, True, mode="allgather")
+    finally:
+        del os.environ["PG_GATHER_SLICE"]
+    assert np.array_equal(t0, t3)
+    assert np.array_equal(f0[0], f3[0])
+
+
+def test_record_allgather_equals_single_rank(pg):
+    """The record all-gather exchange (pg_comm_allgather_records' arithmetic) emulated with
+    two shard contexts on one GPU: every rank's records (pg_get_records) splatted into every rank's
+    building tree in rank order (pg_splat_records) give the single-rank tree bit for bit, as
+    test_tree_stats_allreduce_equals_single_rank does for the statistics all-reduce.  RCCL refuses two
+    ranks on one device, so this is the multi-rank arithmetic of the library's all-gather path."""
+    from mitsuba_path_guiding_amd.integrator import Device
+    sc = pg.scenes.cornell(64, 48)
+    cfg = dict(guiding=1, s_tree_threshold=300.0)
+    full = Device(pg.capi.default_config(**cfg))
+    full.upload(sc)
+    parts = []
+    for r in range(2):
+        d = Device(pg.capi.default_config(rank=r, world_size=2, **cfg))
+        d.upload(sc)
+        parts.append(d)
+    off = 0
+    for it in range(4):
+        full.render_pass(2 ** it, off, True)
+        nfull = full.record_count()
+        full.splat_local()
+        full.refit(it)
+        for d in parts:
+            d.render_pass(2 ** it, off, True)
+        recs = [d.get_records() for d in parts]
+        assert sum(len(x) for x in recs) == 32 * nfull and all(len(x) for x in recs)
+        for d in parts:
+            for x in recs:  # rank order
+                d.splat_records(x)
+            d.refit(it)
+        off += 2 ** it
+    t = full.get_sdtree()
+    assert all(np.array_equal(d.get_sdtree(), t) for d in parts)
+    for d in parts + [full]:
+        d.close()
 
 
 def test_comm_calls_need_a_communicator(pg):

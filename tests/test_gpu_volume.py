@@ -243,8 +243,11 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
     slot: films, sums of squares, training records (through the trees) and path counters must be the
     megakernel's bit for bit -- whether every iteration runs as launches (tail threshold 0), the
     default tail threshold, or the tail kernel takes the whole chunk after the camera rays; with one,
-    two (default) or three lanes of chunks in flight (films in chunk order), and with the flight
-    queues sorted by cell (PG_VOL_SORT)."""
+    two or three (default) lanes of chunks in flight (films in chunk order), with the flight queues
+    sorted by cell (PG_VOL_SORT), and whether the interactions' transmittance walks run as their own stage
+    (k_vnee, default) or inline (PG_VOL_NEE_STAGE=0), and the medium and surface interactions as two
+    launches (default) or one (PG_VOL_SPLIT_VERTEX=0): the walks draw from their own sub-streams and add to
+    L in a fixed order (oracle/orc_volpath.h subStream)."""
     from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer, ProgressiveVolumetricPathTracer
     sc = pg.scenes.smoke(96, 96, res=48)
     props = {"trainingIterations": 3, "samplesPerProgression": 8}
@@ -257,11 +260,13 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
     if case == "guided_exact_chunked":
         props.update({"exactMis": True, "maxPathsInFlight": 4096 + 512})
     out = []
-    runs = (("0", None, None, None), ("1", "0", None, None), ("1", None, None, None), ("1", str(1 << 30), None, None),
-            ("1", None, "1", None), ("1", "0", "3", "1"))
-    for wf, tail, lanes, sort in runs:
+    runs = (("0", None, None, None, None, None), ("1", "0", None, None, None, None), ("1", None, None, None, None, None),
+            ("1", str(1 << 30), None, None, None, None), ("1", None, "1", None, None, None), ("1", "0", "3", "1", None, None),
+            ("1", "0", None, None, "0", None), ("1", "0", "2", None, None, "0"))
+    for wf, tail, lanes, sort, nee, split in runs:
         monkeypatch.setenv("PG_VOL_WAVEFRONT", wf)
-        for var, val in (("PG_VOL_TAIL_PATHS", tail), ("PG_VOL_LANES", lanes), ("PG_VOL_SORT", sort)):
+        for var, val in (("PG_VOL_TAIL_PATHS", tail), ("PG_VOL_LANES", lanes), ("PG_VOL_SORT", sort),
+                         ("PG_VOL_NEE_STAGE", nee), ("PG_VOL_SPLIT_VERTEX", split)):
             if val is None:
                 monkeypatch.delenv(var, raising=False)
             else:

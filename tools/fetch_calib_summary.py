@@ -62,12 +62,16 @@ def main(run, dst):
             e["fetch_per_line"] = round(fb / max(cs["lines_128"], 1), 2)
         if "TCC_EA0_RDREQ_sum" in v:
             e["ea_rdreq_per_line"] = round(v["TCC_EA0_RDREQ_sum"] / max(cs["lines_128"], 1), 3)
+        if "TCC_EA0_RDREQ_LEVEL_sum" in v and v.get("TCC_EA0_RDREQ_sum"):
+            # Little's law over the L2's memory-side read queue: mean cycles a read request is outstanding
+            e["ea_read_latency_cycles"] = round(v["TCC_EA0_RDREQ_LEVEL_sum"] / v["TCC_EA0_RDREQ_sum"], 1)
         if "TCC_HIT_sum" in v and "TCC_MISS_sum" in v:
             e["l2_hit"] = round(v["TCC_HIT_sum"] / max(v["TCC_HIT_sum"] + v["TCC_MISS_sum"], 1), 4)
         rows.append(e)
         print(f"{cs['case']:28s} true {cs['true_bytes']/1e6:9.1f} MB  {cs['gbs']:8.1f} GB/s  "
               f"fetch/true {e.get('fetch_per_true_byte', float('nan')):6.3f}  fetch/line {e.get('fetch_per_line', float('nan')):7.1f} B  "
-              f"EA req/line {e.get('ea_rdreq_per_line', float('nan')):6.3f}  L2 hit {e.get('l2_hit', float('nan')):.3f}")
+              f"EA req/line {e.get('ea_rdreq_per_line', float('nan')):6.3f}  L2 hit {e.get('l2_hit', float('nan')):.3f}  "
+              f"EA lat {e.get('ea_read_latency_cycles', float('nan')):7.1f}")
     json.dump({"source": run, "cases": rows}, open(dst, "w"), indent=1)
 
 

@@ -19,7 +19,7 @@ import subprocess
 import sys
 from collections import defaultdict
 
-PATH_KERNELS = ("k_trace", "k_shade", "k_shadow", "k_shade_all", "k_rays", "k_vflight", "k_vvertex")
+PATH_KERNELS = ("k_trace", "k_shade", "k_shadow", "k_shade_all", "k_rays", "k_vflight", "k_vvertex", "k_vnee")
 
 
 def base_name(n):
