@@ -177,6 +177,7 @@ struct VolLane {
     DevBuf keys, sorted, hist;  // flight order keys of both flight queues, a sorted copy, histograms (PG_VOL_SORT)
     PinnedBuf host;
     uint32_t cap = 0;
+    int stateF4 = 0;  // float4 arrays per slot in `state` (7, or 14 with the k_vnee stage's records)
     // the chunk in flight
     bool active = false, waved = false;  // waved: its paths are done, its film waits for its turn
     uint32_t chunk = 0, pb = 0, np = 0, nl = 0, sample_base = 0;
@@ -1164,7 +1165,7 @@ bool volNeeStage() {
     return e && *e ? std::atoi(e) != 0 : false;
 }
 // VolLane path state: VolWave's 13 float4 per slot; its queues (pg_volpath.hip)
-constexpr int kVolStateF4 = 14, kVolQueues = 8;
+constexpr int kVolStateF4 = 14, kVolStateF4Inline = 7, kVolQueues = 8;
 // k_vnee of iteration i on the lane's second stream, concurrent with iteration i + 1's k_vflight (which reads
 // no state the walks write); k_vvertex of i + 1 waits for it.  PG_VOL_NEE_OVERLAP=0: on the lane's stream
 bool volNeeOverlap() {
@@ -1230,16 +1231,24 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         if (!l.stream) {
             HIPC(c, hipStreamCreateWithFlags(&l.stream, hipStreamNonBlocking));
             HIPC(c, hipEventCreateWithFlags(&l.ready, hipEventDisableTiming));
+        }
+        // the second stream only when the overlapped k_vnee stage runs: HIP maps a process's streams onto
+        // GPU_MAX_HW_QUEUES (4) hardware queues, and with one more stream per lane two lanes shared a queue
+        // and serialized (C5 380 against 400 Mpaths/s, profiles/r05h_vol_streams/)
+        if (neeOverlap && !l.nstream) {
             HIPC(c, hipStreamCreateWithFlags(&l.nstream, hipStreamNonBlocking));
             HIPC(c, hipEventCreateWithFlags(&l.vdone, hipEventDisableTiming));
             HIPC(c, hipEventCreateWithFlags(&l.ndone, hipEventDisableTiming));
         }
         l.npending = false;
-        if (l.cap < want) {
-            HIPC(c, l.state.alloc((size_t)want * 16 * kVolStateF4));
-            HIPC(c, l.items.alloc((size_t)pg_queue_stride(want) * PG_QSHARDS * 4 * kVolQueues));
-            HIPC(c, l.rad.alloc((size_t)want * 16));
-            l.cap = want;
+        const int f4 = neeStage ? kVolStateF4 : kVolStateF4Inline;  // the stage's records only when it runs
+        if (l.cap < want || l.stateF4 != f4) {
+            const uint32_t lc = std::max(want, l.cap);
+            HIPC(c, l.state.alloc((size_t)lc * 16 * f4));
+            l.stateF4 = f4;
+            HIPC(c, l.items.alloc((size_t)pg_queue_stride(lc) * PG_QSHARDS * 4 * kVolQueues));
+            HIPC(c, l.rad.alloc((size_t)lc * 16));
+            l.cap = lc;
         }
         HIPC(c, l.counts.alloc(cbytes));
         HIPC(c, l.host.reserve(cbytes));
@@ -1264,8 +1273,16 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         float4 *st = l.state.as<float4>();
         const size_t cap = l.cap;
         w = VolWave{st, st + cap, reinterpret_cast<uint4 *>(st + 2 * cap), st + 3 * cap, st + 4 * cap,
-                    reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap, st + 7 * cap, st + 8 * cap, st + 9 * cap,
-                    st + 10 * cap, st + 11 * cap, st + 12 * cap, reinterpret_cast<uint32_t *>(st + 13 * cap)};
+                    reinterpret_cast<uint4 *>(st + 5 * cap), st + 6 * cap};
+        if (l.stateF4 == kVolStateF4) {  // the k_vnee stage's deferred-walk records
+            w.n0 = st + 7 * cap;
+            w.n1 = st + 8 * cap;
+            w.n2 = st + 9 * cap;
+            w.h0 = st + 10 * cap;
+            w.h1 = st + 11 * cap;
+            w.h2 = st + 12 * cap;
+            w.nflags = reinterpret_cast<uint32_t *>(st + 13 * cap);
+        }
         // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices, 5/6: delta surface,
         // 7: deferred transmittance walks (k_vnee)
         const size_t qstride = (size_t)pg_queue_stride(l.cap) * PG_QSHARDS;

@@ -30,10 +30,36 @@ namespace {
 // Path-state accesses (every SoA record is read once and written once per bounce).  Non-temporal
 // loads/stores here measured +1 % on C3 but made results timing-dependent with three lanes in flight
 // (2 outcomes in 12 runs of tools/det_kitchen.py, 1 in 20 without), so they are plain.
+// PG_NT_STATE=1 (A/B builds): the non-temporal variant again (round 5, VERDICT r04 item 2: keep the streamed
+// state out of the XCD's L2 so the BVH and TriAccel working set stays).
+#ifndef PG_NT_STATE
+#define PG_NT_STATE 0
+#endif
+#if PG_NT_STATE
+typedef float pgF4v __attribute__((ext_vector_type(4)));
+typedef unsigned int pgU4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ldS(const float4 *p) {
+    const pgF4v v = __builtin_nontemporal_load(reinterpret_cast<const pgF4v *>(p));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 ldS(const uint4 *p) {
+    const pgU4v v = __builtin_nontemporal_load(reinterpret_cast<const pgU4v *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void stS(float4 *p, float4 a) {
+    const pgF4v v = {a.x, a.y, a.z, a.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<pgF4v *>(p));
+}
+__device__ __forceinline__ void stS(uint4 *p, uint4 a) {
+    const pgU4v v = {a.x, a.y, a.z, a.w};
+    __builtin_nontemporal_store(v, reinterpret_cast<pgU4v *>(p));
+}
+#else
 __device__ __forceinline__ float4 ldS(const float4 *p) { return *p; }
 __device__ __forceinline__ uint4 ldS(const uint4 *p) { return *p; }
 __device__ __forceinline__ void stS(float4 *p, float4 a) { *p = a; }
 __device__ __forceinline__ void stS(uint4 *p, uint4 a) { *p = a; }
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,

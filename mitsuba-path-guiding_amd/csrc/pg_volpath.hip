@@ -1256,9 +1256,10 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
 }
 
 // interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices.  KIND 2: both
-// in one launch; KIND 0 / 1: the medium / surface blocks only, as launches of their own (PG_VOL_SPLIT_VERTEX,
-// default), so each gets its own register budget: with the walks deferred to k_vnee the medium kernel fits
-// 3 waves per SIMD without scratch (PG_VMEDIUM_WAVES), the surface kernel's BSDFs need more
+// in one launch (default with the walks inline); KIND 0 / 1: the medium / surface blocks only, as launches of
+// their own (with the k_vnee stage, or PG_VOL_SPLIT_VERTEX=1), so each gets its own register budget: with the
+// walks deferred to k_vnee the medium kernel fits 3 waves per SIMD without scratch (PG_VMEDIUM_WAVES), the
+// surface kernel's BSDFs need more
 #ifndef PG_VMEDIUM_WAVES
 #define PG_VMEDIUM_WAVES 3
 #endif
@@ -1437,8 +1438,11 @@ void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, c
     const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
     if (mr + sr + dr == 0) return;
     const Queue qn = nee ? *nee : Queue{};
-    const char *se = std::getenv("PG_VOL_SPLIT_VERTEX");  // read per launch: tests switch it within a process
-    const bool split = !(se && *se && std::atoi(se) == 0);
+    // two launches when the walks are a stage of their own (the medium launch then fits 3 waves/SIMD); one
+    // with the walks inline (C5 382.0 / 382.6 Mpaths/s against 374.8 / 374.8 split, profiles/r05d_ab/).
+    // PG_VOL_SPLIT_VERTEX overrides, read per launch: tests switch it within a process
+    const char *se = std::getenv("PG_VOL_SPLIT_VERTEX");
+    const bool split = se && *se ? std::atoi(se) != 0 : nee != nullptr;
 #define PG_VV(GU, NS, KIND, ROWS, MB)                                                                                \
     hipLaunchKernelGGL((k_vvertex<GU, NS, KIND>), dim3(PG_QSHARDS * (ROWS)), dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, \
                        med, surf, dsurf, MB, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf, qn)
