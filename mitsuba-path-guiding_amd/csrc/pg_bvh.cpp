@@ -681,7 +681,9 @@ static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_
         nodes.resize(nodes.size() + 4 * PG_QNODE_F4, 0.0f);
         return q;
     };
+    out.top_nodes = 0;  // set below: the 4-wide nodes of the breadth-first top levels
     if (bn[0].leaf) {  // the root is a leaf: one node with one leaf slot
+        out.top_nodes = 1;
         const uint32_t q = alloc();
         float *o = &nodes[(size_t)q * 4 * PG_QNODE_F4];
         int32_t r[4] = {ref(0, 0), PG_QNODE_EMPTY, PG_QNODE_EMPTY, PG_QNODE_EMPTY};
@@ -694,10 +696,24 @@ static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_
         out.nodes.swap(nodes);
         return true;
     }
-    st.push_back({0, alloc(), 1});
-    while (!st.empty()) {
-        const QTask t = st.back();
-        st.pop_back();
+    // the top PG_BVH4_TOP_LEVELS levels' nodes are processed breadth first, so their children -- the
+    // nodes of depths <= PG_BVH4_TOP_LEVELS -- take the first indices (k_rays' LDS tile); the rest depth
+    // first.  Node contents and refs do not depend on the order: walks return the same hits.
+    std::vector<QTask> bfs{{0, alloc(), 1}};
+    std::vector<uint32_t> depthOf{0};
+    size_t head = 0;
+    auto depth = [&](uint32_t q) { return q < depthOf.size() ? depthOf[q] : 0xFFFFFFFFu; };
+    while (true) {
+        QTask t;
+        if (head < bfs.size()) {
+            t = bfs[head++];
+        } else if (!st.empty()) {
+            t = st.back();
+            st.pop_back();
+        } else {
+            break;
+        }
+        const uint32_t td = depth(t.qnode);
         std::vector<int32_t> ch;
         if (!greedy) collect(t.bnode, ch);
         else ch = {bn[t.bnode].child[0], bn[t.bnode].child[1]};
@@ -731,14 +747,20 @@ static bool buildQuadBvh(const std::vector<BNode> &bn, const std::vector<uint32_
             } else {
                 const uint32_t q = alloc();
                 r[s] = (int32_t)q;
-                st.push_back({ch[s], q, need});
+                if (td != 0xFFFFFFFFu && td + 1 < (uint32_t)PG_BVH4_TOP_LEVELS) {  // breadth-first top levels
+                    depthOf.resize(q + 1, 0xFFFFFFFFu);
+                    depthOf[q] = td + 1;
+                    bfs.push_back({ch[s], q, need});
+                } else {
+                    st.push_back({ch[s], q, need});
+                }
             }
         }
         float *o = &nodes[(size_t)t.qnode * 4 * PG_QNODE_F4];
         putQuadNode(o, box, r, (int)ch.size());
+        if (head == bfs.size() && out.top_nodes == 0) out.top_nodes = (uint32_t)(nodes.size() / (4 * PG_QNODE_F4));
     }
     out.nodes.swap(nodes);
-    out.top_nodes = 0;
     return maxNeed <= PG_QSTACK_DEPTH;
 }
 

@@ -958,7 +958,7 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     pg_status s;
     if ((s = upload(c, c->rtab, rtab))) return s;
     for (auto &mo : rtabOf) c->host_mats[mo.first].rtrans = c->rtab.as<float>() + mo.second;
-    c->bvh_top_nodes = std::min<uint32_t>(bvh.top_nodes, PG_BVH_TOP_NODES);
+    c->bvh_top_nodes = std::min<uint32_t>(bvh.top_nodes, PG_BVH4 ? PG_BVH4_TOP_NODES : PG_BVH_TOP_NODES);
     if ((s = upload(c, c->nodes, bvh.nodes)) || (s = upload(c, c->tris, bvh.tris)) ||
         (s = upload(c, c->wnodes, bvh.wnodes)) || (s = upload(c, c->tshade, shade)) ||
         (s = upload(c, c->tclass, tclass)) ||

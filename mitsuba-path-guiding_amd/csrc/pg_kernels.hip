@@ -17,6 +17,17 @@
 #ifndef SHADE_LDS_MATS
 #define SHADE_LDS_MATS 0   // > 0: k_shade stages up to this many materials in LDS (64 = 8 KiB)
 #endif
+#ifndef PG_RAYS_LDS_TOP
+#define PG_RAYS_LDS_TOP 0  // 1: k_rays' closest-hit blocks stage the 4-wide BVH's top levels in LDS (1.3 KiB)
+#endif
+// the LDS tile of the closest-hit BVH's top levels: node size and capacity of this build's BVH
+#if PG_BVH4
+#define PG_TOP_NODE_F4 PG_QNODE_F4
+#define PG_TOP_TILE_F4 (PG_BVH4_TOP_NODES * PG_QNODE_F4)
+#else
+#define PG_TOP_NODE_F4 PG_BVH_NODE_F4
+#define PG_TOP_TILE_F4 (PG_BVH_TOP_NODES * PG_BVH_NODE_F4)
+#endif
 #ifndef PG_TRACE_LDS_TOP
 #define PG_TRACE_LDS_TOP 0  // 1: k_trace stages the BVH's top PG_BVH_TOP_LEVELS levels in LDS (2 KiB)
 #endif
@@ -179,10 +190,10 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, P
                                                        float4 *first) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
     // the BVH's top levels (breadth first, pg_layout.h PG_BVH_TOP_NODES), staged in LDS once per block
-    __shared__ float4 top[(PG_TRACE_LDS_TOP ? PG_BVH_TOP_NODES : 1) * PG_BVH_NODE_F4];
+    __shared__ float4 top[(PG_TRACE_LDS_TOP ? PG_TOP_TILE_F4 : 1)];
     const int ntop = PG_TRACE_LDS_TOP ? (int)sc.top_nodes : 0;
     if (PG_TRACE_LDS_TOP) {
-        for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_BVH_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
+        for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_TOP_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
         __syncthreads();
     }
     traceRows<ENV, PG_TRACE_LDS_TOP != 0>(g, sc, p, q, cqs, first, blockIdx.x, gridDim.x, threadStack(stack, p.stack_ovf),
@@ -242,11 +253,20 @@ __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_
     __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
 #if PG_RAYS_TRACE_FIRST  // the costlier closest-hit blocks dispatched first (profiles/r03zg_rays_order_ab)
     const uint32_t trace_blocks = gridDim.x - shadow_blocks;
-    if (blockIdx.x >= trace_blocks)
+    if (blockIdx.x >= trace_blocks) {
         shadowRows(sc, p, shq, blockIdx.x - trace_blocks, shadow_blocks, threadWideStack(stack, p.stack_ovf));
-    else
-        traceRows<ENV, false>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks, threadStack(stack, p.stack_ovf),
-                              nullptr, 0);
+    } else {
+        // the 4-wide BVH's breadth-first top levels in LDS (PG_RAYS_LDS_TOP, A/B; round 5 re-measure of the
+        // round-2 tile on the 64-B nodes)
+        __shared__ float4 top[PG_RAYS_LDS_TOP ? PG_TOP_TILE_F4 : 1];
+        const int ntop = PG_RAYS_LDS_TOP ? (int)sc.top_nodes : 0;
+        if (PG_RAYS_LDS_TOP) {
+            for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_TOP_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
+            __syncthreads();
+        }
+        traceRows<ENV, PG_RAYS_LDS_TOP != 0>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks,
+                                             threadStack(stack, p.stack_ovf), top, ntop);
+    }
 #else
     if (blockIdx.x < shadow_blocks)
         shadowRows(sc, p, shq, blockIdx.x, shadow_blocks, threadWideStack(stack, p.stack_ovf));

@@ -166,6 +166,13 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 #define PG_QNODE_F4 8
 #endif
 #define PG_QNODE_EMPTY 0x7ffffffe
+// The 4-wide nodes of the top PG_BVH4_TOP_LEVELS + 1 levels come first, breadth first (round 5; the rest
+// depth first): k_rays / k_trace stage nodes [0, SceneDev.top_nodes) in LDS with PG_RAYS_LDS_TOP (A/B).
+// 1 + 4 + 16 = 21 nodes, 1.3 KiB of quantised nodes.
+#ifndef PG_BVH4_TOP_LEVELS
+#define PG_BVH4_TOP_LEVELS 2
+#endif
+#define PG_BVH4_TOP_NODES 21
 // closest-hit stack entries a 4-wide traversal may need (the builder checks its trees against it;
 // the global overflow ring already holds PG_QSTACK_DEPTH - LDS_STACK words per thread)
 #define PG_QSTACK_DEPTH 96

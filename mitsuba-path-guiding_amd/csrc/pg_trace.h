@@ -339,10 +339,11 @@ __device__ __forceinline__ SlabRay slabRay(f3 o, f3 d) {
 // nodes, its hit children visited nearest first (a 5-exchange sorting network on the entry
 // distances; the others pushed far to near), with the binary walk's while-while loop, postponed
 // leaves, tie rule and widened culling distance, so it returns the same hit.
-template <bool ANY>
+// LTOP: nodes [0, ntop) are read from `lnodes` (the breadth-first top levels, staged in LDS by the caller)
+template <bool ANY, bool LTOP = false>
 __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, const float4 *__restrict__ tris, f3 o, f3 d,
                                           float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
-                                          const TStack &stk) {
+                                          const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
     const int DONE = 0x7fffffff;
     const float INF = __builtin_huge_valf();
     const SlabRay sr = slabRay(o, d);
@@ -361,7 +362,19 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
 #if PG_QNODE_QUANT
             // planes origin + q 2^e: t = q (2^e idir) + (origin - o) idir, the latter padded outward by
             // slabRay's addends and by 2^-22 |origin idir| (its own rounding)
-            const float4 n0 = np[0], rf = np[1], q0 = np[2], q1 = np[3];
+            float4 n0, rf, q0, q1;
+            if (LTOP && node < ntop) {  // LDS loads for the staged top levels, global loads below them
+                const float4 *lp = lnodes + (size_t)PG_QNODE_F4 * node;
+                n0 = lp[0];
+                rf = lp[1];
+                q0 = lp[2];
+                q1 = lp[3];
+            } else {
+                n0 = np[0];
+                rf = np[1];
+                q0 = np[2];
+                q1 = np[3];
+            }
             const uint32_t e = __float_as_uint(n0.w);
             const float sx = __uint_as_float((e & 0xFFu) << 23) * idir.x;
             const float sy = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y;
@@ -386,8 +399,9 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
         k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
     }
 #else
-            const float4 lx = np[0], hx = np[1], ly = np[2], hy = np[3], lz = np[4], hz = np[5];
-            const float4 rf = np[6];
+            const float4 *fp = (LTOP && node < ntop) ? lnodes + (size_t)PG_QNODE_F4 * node : np;
+            const float4 lx = fp[0], hx = fp[1], ly = fp[2], hy = fp[3], lz = fp[4], hz = fp[5];
+            const float4 rf = fp[6];
 #define PG_Q4_SLOT(i, c)                                                                              \
     {                                                                                                 \
         const float x0 = fmaf(lx.c, idir.x, aLo.x), x1 = fmaf(hx.c, idir.x, aHi.x);                   \
@@ -531,8 +545,7 @@ __device__ __forceinline__ bool traverse(const float4 *__restrict__ nodes, const
                                          float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
                                          const TStack &stk, const float4 *lnodes = nullptr, int ntop = 0) {
 #if PG_BVH4
-    static_assert(!LTOP, "LDS-staged top levels are a binary-BVH option");
-    return traverse4<ANY>(nodes, tris, o, d, tmin, tmax, hitTri, hu, hv, stk);
+    return traverse4<ANY, LTOP>(nodes, tris, o, d, tmin, tmax, hitTri, hu, hv, stk, lnodes, ntop);
 #else
     return traverseBin<ANY, LTOP>(nodes, tris, o, d, tmin, tmax, hitTri, hu, hv, stk, lnodes, ntop);
 #endif
