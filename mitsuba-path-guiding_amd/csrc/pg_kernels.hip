@@ -738,7 +738,10 @@ __device__ __forceinline__ void tailShade(const GParams &g, const SceneDev &sc, 
     }
 }
 template <bool ENV>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_tail(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue q,
+#ifndef PG_TAIL_WAVES
+#define PG_TAIL_WAVES 0  // 0: the compiler's budget (A/B: 3)
+#endif
+__global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_TAIL_WAVES > 0 ? PG_TAIL_WAVES : 1))) void k_tail(GParams g, SceneDev sc, SDDev sd, PathDev p, Queue q,
                                                       unsigned long long *stats) {
     __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
     const TStack stk = threadStack(stack, p.stack_ovf);

@@ -938,28 +938,40 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
 }
 // an interaction's deferred walks, in the oracle's order: the emitter hit, then the NEE (into L and into
 // the snapshot of the interaction's training vertex); each on its own sub-stream of the path's key
-__device__ __forceinline__ void resolveDeferred(const SceneDev &sc, const VolDev &v, const VDefer &df, uint32_t key,
-                                                uint32_t sample, uint32_t item, f3 &L, const TStack &stk,
-                                                uint32_t &segs, uint32_t &lookups) {
+// the walks' transmittances, each on its sub-stream (no radiance touched yet)
+__device__ __forceinline__ void walkDeferred(const SceneDev &sc, const VolDev &v, const VDefer &df, uint32_t key,
+                                             uint32_t sample, const TStack &stk, uint32_t &segs, uint32_t &lookups,
+                                             float &Th, float &Tn) {
+    Th = Tn = 0.0f;
     if (df.hit) {
         VRng sub = subStream(key, sample, df.hDim, 1);
-        const float T = emitterWalkT(sc, v, df.hMedium, df.hInter, df.hO, df.hD, df.hMint, sub, stk, segs);
+        Th = emitterWalkT(sc, v, df.hMedium, df.hInter, df.hO, df.hD, df.hMint, sub, stk, segs);
         lookups += sub.lookups;
-        if (T != 0) L = L + df.hC * T;
     }
     if (df.nee) {
         VRng sub = subStream(key, sample, df.nDim, 0);
-        const float tr = sceneTransmittance(sc, v, df.n1, df.nOnSurface, df.n2, df.nMedium, df.nMaxInter, sub, stk, segs);
+        Tn = sceneTransmittance(sc, v, df.n1, df.nOnSurface, df.n2, df.nMedium, df.nMaxInter, sub, stk, segs);
         lookups += sub.lookups;
-        if (tr != 0) {
-            const f3 add = df.nC * tr;
-            L = L + add;
-            if (df.k >= 0) {
-                float4 *vb = v.vtx + ((size_t)df.k * v.vtx_P + item) * PG_VTX_F4;
-                vb[2] = f4(xyz(vb[2]) + add, 0.0f);
-            }
+    }
+}
+// their contributions, in the fixed order: the emitter hit, then the NEE (also into the vertex's snapshot)
+__device__ __forceinline__ void addDeferred(const VolDev &v, const VDefer &df, float Th, float Tn, uint32_t item, f3 &L) {
+    if (df.hit && Th != 0) L = L + df.hC * Th;
+    if (df.nee && Tn != 0) {
+        const f3 add = df.nC * Tn;
+        L = L + add;
+        if (df.k >= 0) {
+            float4 *vb = v.vtx + ((size_t)df.k * v.vtx_P + item) * PG_VTX_F4;
+            vb[2] = f4(xyz(vb[2]) + add, 0.0f);
         }
     }
+}
+__device__ __forceinline__ void resolveDeferred(const SceneDev &sc, const VolDev &v, const VDefer &df, uint32_t key,
+                                                uint32_t sample, uint32_t item, f3 &L, const TStack &stk,
+                                                uint32_t &segs, uint32_t &lookups) {
+    float Th, Tn;
+    walkDeferred(sc, v, df, key, sample, stk, segs, lookups, Th, Tn);
+    addDeferred(v, df, Th, Tn, item, L);
 }
 __device__ __forceinline__ void clearDefer(VDefer &df) {
     df.nee = df.hit = false;
@@ -1256,20 +1268,34 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
 }
 
 // interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices.  KIND 2: both
-// in one launch (default with the walks inline); KIND 0 / 1: the medium / surface blocks only, as launches of
-// their own (with the k_vnee stage, or PG_VOL_SPLIT_VERTEX=1), so each gets its own register budget: with the
-// walks deferred to k_vnee the medium kernel fits 3 waves per SIMD without scratch (PG_VMEDIUM_WAVES), the
-// surface kernel's BSDFs need more
+// in one launch (PG_VOL_SPLIT_VERTEX=0); KIND 0 / 1 (default): the medium / surface blocks only, as launches of
+// their own, so each gets its own register budget: the medium kernel runs at 3 waves per SIMD (with the
+// walks deferred to k_vnee without scratch, PG_VMEDIUM_WAVES; with them inline 44 B/lane of scratch,
+// PG_VMEDIUM_INLINE_WAVES), the surface kernel's BSDFs need more
 #ifndef PG_VMEDIUM_WAVES
 #define PG_VMEDIUM_WAVES 3
 #endif
 #ifndef PG_VSURFACE_WAVES
 #define PG_VSURFACE_WAVES PG_VOL_WAVES
 #endif
+// the medium launch with its walks inline: 3 waves/SIMD (192 VGPRs uncapped; 168 with 44 B/lane of scratch,
+// the path state stored before the walks): C5 405.2 / 404.6 against 393.0 / 392.6 Mpaths/s at 2 waves and
+// 392.3 / 393.2 as one launch (profiles/r05o_vol_vertex_split/)
+#ifndef PG_VMEDIUM_INLINE_WAVES
+#define PG_VMEDIUM_INLINE_WAVES 3
+#endif
+// ... and the surface launch at 3 waves too (228 VGPRs uncapped; 168 with 156 B/lane of scratch): C5
+// 439.2 / 439.6 against 405.8 / 405.5 at 2 waves; 4 waves 434.0 / 433.8, the medium launch at 4 with the
+// surface at 3 432.9 / 431.5 (profiles/r05p_vol_waves/, r05q_vol_waves/).  With three lanes in flight the
+// interactions' occupancy pays more than their spills cost
+#ifndef PG_VSURFACE_INLINE_WAVES
+#define PG_VSURFACE_INLINE_WAVES 3
+#endif
 template <bool NEE_STAGE, int KIND>
-struct VVertexWaves {  // the inline walks (PG_VOL_NEE_STAGE=0, A/B) keep round 4's budget
-    static constexpr int value = !NEE_STAGE ? PG_VVERTEX_WAVES
-                                            : (KIND == 0 ? PG_VMEDIUM_WAVES : (KIND == 1 ? PG_VSURFACE_WAVES : PG_VVERTEX_WAVES));
+struct VVertexWaves {
+    static constexpr int value = KIND == 0 ? (NEE_STAGE ? PG_VMEDIUM_WAVES : PG_VMEDIUM_INLINE_WAVES)
+                                           : (KIND == 1 ? (NEE_STAGE ? PG_VSURFACE_WAVES : PG_VSURFACE_INLINE_WAVES)
+                                                        : PG_VVERTEX_WAVES);
 };
 template <bool GUIDED, bool NEE_STAGE, int KIND>
 __global__ __launch_bounds__(TRACE_BLOCK, (VVertexWaves<NEE_STAGE, KIND>::value)) void k_vvertex(GParams g, SceneDev sc, VolDev v, SDDev sd,
@@ -1307,15 +1333,9 @@ __global__ __launch_bounds__(TRACE_BLOCK, (VVertexWaves<NEE_STAGE, KIND>::value)
                 alive = volSurface<GUIDED, NEE_STAGE>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, df, w);
             vertices++;
             const bool ended = !(alive && volDepthOk(g, P));
-            if (df.hit || df.nee) {
-                if (NEE_STAGE) {  // the record is in the slot's VolWave entries; k_vnee walks it after this launch
-                    w.nflags[slot] = deferFlags(df, ended);
-                    toN = true;
-                } else {
-                    resolveDeferred(sc, v, df, rng.key, rng.sample, slot, P.L, stk, segs, rng.lookups);
-                }
-            }
+            const uint32_t key0 = rng.key, sample0 = rng.sample;
             vlookups += rng.lookups - l0;
+            // the path's state goes out first, so it holds no registers across the walks (inline below)
             if (!ended) {
                 storePath(w, slot, P, rng);
                 toF = P.medium >= 0;
@@ -1324,6 +1344,23 @@ __global__ __launch_bounds__(TRACE_BLOCK, (VVertexWaves<NEE_STAGE, KIND>::value)
                 if (toS) cheap = cheapSurface(sc, v, P.its.valid, P.its.tri);
             } else {
                 volEnd(v, slot, P, rng, lookups);
+            }
+            if (df.hit || df.nee) {
+                if (NEE_STAGE) {  // the record is in the slot's VolWave entries; k_vnee walks it after this launch
+                    w.nflags[slot] = deferFlags(df, ended);
+                    toN = true;
+                } else {  // inline: the walks, then their adds into the stored radiance (the same order and sums)
+                    float Th, Tn;
+                    uint32_t wl = 0;
+                    walkDeferred(sc, v, df, key0, sample0, stk, segs, wl, Th, Tn);
+                    lookups += wl;
+                    vlookups += wl;
+                    float4 *dst = ended ? v.rad + slot : w.L + slot;
+                    const float4 l4 = *dst;
+                    f3 L = xyz(l4);
+                    addDeferred(v, df, Th, Tn, slot, L);
+                    *dst = f4(L, l4.w);
+                }
             }
         }
         flightAppend(toF, slot, key, nf, sh);
@@ -1366,8 +1403,11 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VNEE_WAVES) void k_vnee(GParams g, 
 
 // the chunk's last paths: each thread runs one to its end (paths of `qf` start with their flight, those
 // of `qs` with their surface interaction)
+#ifndef PG_VTAIL_WAVES
+#define PG_VTAIL_WAVES 3  // C5 442.3 / 441.9 against 439.2 / 439.6 at 2 (profiles/r05q_vol_waves/)
+#endif
 template <bool GUIDED>
-__global__ __launch_bounds__(TRACE_BLOCK, PG_VOL_WAVES) void k_vtail(GParams g, SceneDev sc, VolDev v, SDDev sd,
+__global__ __launch_bounds__(TRACE_BLOCK, PG_VTAIL_WAVES) void k_vtail(GParams g, SceneDev sc, VolDev v, SDDev sd,
                                                                      VolWave w, Queue qf, Queue qs, Queue qd,
                                                                      uint32_t fblocks, uint32_t dblocks) {
     __shared__ uint32_t stack[LDS_STACK * TRACE_BLOCK];
@@ -1438,11 +1478,12 @@ void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, c
     const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
     if (mr + sr + dr == 0) return;
     const Queue qn = nee ? *nee : Queue{};
-    // two launches when the walks are a stage of their own (the medium launch then fits 3 waves/SIMD); one
-    // with the walks inline (C5 382.0 / 382.6 Mpaths/s against 374.8 / 374.8 split, profiles/r05d_ab/).
-    // PG_VOL_SPLIT_VERTEX overrides, read per launch: tests switch it within a process
+    // medium and surface interactions as two launches (each its own register budget: the medium launch at
+    // 3 waves/SIMD, PG_VMEDIUM_INLINE_WAVES / PG_VMEDIUM_WAVES), or one (PG_VOL_SPLIT_VERTEX=0; read per
+    // launch: tests switch it within a process).  With the walks inline and the path state stored before
+    // them: C5 405.2 / 404.6 split against 392.3 / 393.2 one launch (profiles/r05o_vol_vertex_split/)
     const char *se = std::getenv("PG_VOL_SPLIT_VERTEX");
-    const bool split = se && *se ? std::atoi(se) != 0 : nee != nullptr;
+    const bool split = se && *se ? std::atoi(se) != 0 : true;
 #define PG_VV(GU, NS, KIND, ROWS, MB)                                                                                \
     hipLaunchKernelGGL((k_vvertex<GU, NS, KIND>), dim3(PG_QSHARDS * (ROWS)), dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, \
                        med, surf, dsurf, MB, PG_QSHARDS * dr, next_flight, next_surf, next_dsurf, qn)
