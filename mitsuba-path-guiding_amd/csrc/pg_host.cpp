@@ -1184,11 +1184,14 @@ struct VChunk {
     uint32_t pb, np, nl, sample_base;
 };
 // flight queues sorted by the 16^3 cell of the flight's start before k_vflight, for shards of at least this
-// many flights (PG_VOL_SORT overrides; 0 = off): C5 351.5 / 350.0 against 346.3 / 345.7 Mpaths/s unsorted;
-// an octant + 8^3-cell key measured the same (profiles/r04s_vol_sort/, r04t_vol_ab/)
+// many flights (PG_VOL_SORT; 0 = off, the default since round 5).  Round 4: C5 351.5 / 350.0 against
+// 346.3 / 345.7 Mpaths/s unsorted (profiles/r04s_vol_sort/, r04t_vol_ab/).  With round 5's 3-wave interaction
+// launches the sort no longer pays: 442.9 / 442.5 sorted (4096) against 445.0 / 445.8 unsorted, k_vflight
+// 45.3 against 48.9 ms per calibration pass but k_vvertex 136.4 against 133.8 (its state reads no longer
+// scattered) plus the sort kernels (profiles/r05t_vol_tune/)
 uint32_t volSortMin() {
     const char *e = std::getenv("PG_VOL_SORT");
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 4096u;
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
 }
 // volumetric wavefront lanes in flight: pg_config.path_lanes (default 3, as for the path integrator; C5 at
 // the round-4 kernels: 393.7 / 397.0 / 389.7 Mpaths/s with 2 / 3 / 4 lanes, profiles/r04aj_vol_lanes/);

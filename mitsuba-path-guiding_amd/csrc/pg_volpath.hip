@@ -1276,7 +1276,7 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
 #define PG_VMEDIUM_WAVES 3
 #endif
 #ifndef PG_VSURFACE_WAVES
-#define PG_VSURFACE_WAVES PG_VOL_WAVES
+#define PG_VSURFACE_WAVES 3
 #endif
 // the medium launch with its walks inline: 3 waves/SIMD (192 VGPRs uncapped; 168 with 44 B/lane of scratch,
 // the path state stored before the walks): C5 405.2 / 404.6 against 393.0 / 392.6 Mpaths/s at 2 waves and
