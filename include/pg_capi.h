@@ -292,7 +292,7 @@ typedef struct pg_stats {
     uint64_t vol_flights;
     uint64_t vol_flight_lookups;
     double vol_vertex_ms;
-    uint64_t vol_vertex_launches;
+    uint64_t vol_vertex_launches; /* kernels: each interaction stage launches the medium and the surface kernel */
     uint64_t vol_vertices;
     uint64_t vol_vertex_lookups;
     /* ABI 12: the interactions' deferred transmittance walks (k_vnee: NEE shadow walks and emitter walks

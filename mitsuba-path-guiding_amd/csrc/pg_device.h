@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include "pg_layout.h"
+#include "pg_fastmath.h"  // fastlog / fastexp: the reference's math::fastlog / fastexp call sites only
 
 #define PGD __device__ __forceinline__
 
@@ -150,8 +151,8 @@ PGD f3 refractV(f3 wi, f3 m, float eta, float cosThetaT) {
     return m * (dot(wi, m) * eta + cosThetaT) - wi * eta;
 }
 
-PGD float erfinvf_(float x) {  // Giles 2010 single-precision fit (math::erfinv)
-    float w = -logf((1.0f - x) * (1.0f + x)), p;
+PGD float erfinvf_(float x) {  // Giles 2010 single-precision fit (math.cpp:25-53)
+    float w = -fastlog((1.0f - x) * (1.0f + x)), p;
     if (w < 5.0f) {
         w = w - 2.5f;
         p = 2.81022636e-08f;
@@ -177,6 +178,15 @@ PGD float erfinvf_(float x) {  // Giles 2010 single-precision fit (math::erfinv)
     }
     return p * x;
 }
+PGD float erfAS(float x) {  // math.cpp:55-72 (A&S 7.1.26, not the device library's erff)
+    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f, a4 = -1.453152027f,
+                a5 = 1.061405429f, p = 0.3275911f;
+    const float sign = copysignf(1.0f, x);
+    x = fabsf(x);
+    const float t = 1.0f / (1.0f + p * x);
+    const float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * fastexp(-x * x);
+    return sign * y;
+}
 
 // ---- microfacet distribution (src/bsdfs/microfacet.h:191-600)
 struct Mf {
@@ -190,7 +200,7 @@ struct Mf {
         float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / c2;
         float r;
         if (type == 0) {
-            r = expf(-be) / (kPi * au * av * c2 * c2);
+            r = fastexp(-be) / (kPi * au * av * c2 * c2);
         } else {
             float root = (1.0f + be) * c2;
             r = 1.0f / (kPi * au * av * root * root);
@@ -239,7 +249,7 @@ struct Mf {
             alphaSqr = 1.0f / (cs * cs + ss * ss);
         }
         if (type == 0) {
-            float t2 = alphaSqr * -logf(1.0f - sx);
+            float t2 = alphaSqr * -fastlog(1.0f - sx);
             cosThetaM = 1.0f / sqrtf(1.0f + t2);
             pdf = (1.0f - sx) / (kPi * au * av * cosThetaM * cosThetaM * cosThetaM);
         } else {
@@ -255,15 +265,15 @@ struct Mf {
     PGD void sampleVisible11(float thetaI, float sx, float sy, float &slx, float &sly) const {
         if (type == 0) {
             if (thetaI < 1e-4f) {
-                float r = sqrtf(-logf(1.0f - sx)), s, c;
+                float r = sqrtf(-fastlog(1.0f - sx)), s, c;
                 sincosf(2 * kPi * sy, &s, &c);
                 slx = r * c;
                 sly = r * s;
                 return;
             }
-            const float SQRT_PI_INV = 0.56418958354775628695f;
+            const float SQRT_PI_INV = 0.56418955f;  // microfacet.h:574, 1 / std::sqrt(M_PI) in float (M_PI is float)
             float tanThetaI = tanf(thetaI), cotThetaI = 1 / tanThetaI;
-            float a = -1, c = erff(cotThetaI);
+            float a = -1, c = erfAS(cotThetaI);
             float sample_x = fmaxf(sx, 1e-6f);
             float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
             float b = c - (1 + c) * powf(1 - sample_x, fit);
@@ -1013,6 +1023,15 @@ PGD unsigned long long fracStat(float w, float pb, float pg, float q0, int k) {
     if (v < -kFracCap) v = -kFracCap;
     return (unsigned long long)(long long)v;
 }
+// back to the translation unit's own contraction (Makefile FPC: -DPG_FPC_ON / -DPG_FPC_FAST), not a fixed
+// setting: until round 5's last commits a bare contract(on) here re-enabled contraction for every kernel
+// after this header in the off build
+#if defined(PG_FPC_FAST)
+#pragma clang fp contract(fast)
+#elif defined(PG_FPC_ON)
 #pragma clang fp contract(on)
+#else
+#pragma clang fp contract(off)
+#endif
 
 }  // namespace pgd

@@ -1418,8 +1418,8 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
         // the previous iteration's walks write L: done before this iteration's interactions read it
         if (pg_status js = joinNee(l)) return js;
         if (neeStage) HIPC(c, hipMemsetAsync(q[7].counts, 0, PG_QSHARDS * 4, l.stream));
-        pg_launch_vol_vertex(l.stream, g, sc, lv, sd, w, q[4], mm, q[2 + cur], ms, q[5 + cur], ms, q[nxt], q[2 + nxt],
-                             q[5 + nxt], neeStage ? &q[7] : nullptr);
+        const int vk = pg_launch_vol_vertex(l.stream, g, sc, lv, sd, w, q[4], mm, q[2 + cur], ms, q[5 + cur], ms,
+                                            q[nxt], q[2 + nxt], q[5 + nxt], neeStage ? &q[7] : nullptr);
         if (evt) HIPC(c, hipEventRecord(c->vw_ev[2], l.stream));
         // the deferred walks: at most one entry per path live in this iteration (<= ms per shard)
         if (neeOverlap) {
@@ -1442,7 +1442,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
             }
             HIPC(c, hipEventElapsedTime(&b, c->vw_ev[1], c->vw_ev[2]));
             c->stats.vol_vertex_ms += b;
-            c->stats.vol_vertex_launches++;
+            c->stats.vol_vertex_launches += vk;  // kernels, not stages: the medium and surface launches
             if (neeStage) {
                 HIPC(c, hipEventElapsedTime(&e, c->vw_ev[2], c->vw_ev[3]));
                 c->stats.vol_nee_ms += e;

@@ -170,9 +170,9 @@ void pg_launch_vol_camera(hipStream_t s, const GParams &g, const SceneDev &sc, c
 // surf / dsurf: surface vertices on other / delta-class surfaces (and escaped rays), pg_volpath.hip PG_VOL_SPLIT_SURF
 void pg_launch_vol_flight(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                           const VolWave &w, Queue flight, uint32_t max_flight, Queue med, Queue surf, Queue dsurf);
-void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
-                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf, const Queue *nee);
+int pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                         const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
+                         uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf, const Queue *nee);
 // the interactions' deferred transmittance walks (k_vnee); max_nee bounds every shard of `nee`
 void pg_launch_vol_nee(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w, Queue nee,
                        uint32_t max_nee);

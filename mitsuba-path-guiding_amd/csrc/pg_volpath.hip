@@ -223,7 +223,7 @@ __device__ __forceinline__ bool sampleDistance(const MedView &M, f3 o, f3 d, flo
     if (!medClip(M, o, d, 0.0f, maxt, t0, t1)) return false;
     float t = t0;
     for (;;) {
-        t -= logf(1 - rng.next1()) * M.invMax;
+        t -= trackLog(1 - rng.next1()) * M.invMax;
         if (!(t < t1)) return false;
         const f3 p = o + d * t;
         const float density = lookupDensity(M, p) * M.scale;
@@ -273,7 +273,7 @@ __device__ __forceinline__ bool trackGrid(const MedView &M, f3 o, f3 d, float t0
         const float mu = M.maj[((size_t)c[2] * M.my + c[1]) * M.mx + c[0]];
         if (mu > 0) {
             for (;;) {
-                const float ts = t - logf(1 - rng.next1()) / mu;
+                const float ts = t - trackLog(1 - rng.next1()) / mu;
                 if (!(ts < tExit)) break;
                 t = ts;
                 const f3 p = o + d * t;
@@ -327,7 +327,7 @@ __device__ __forceinline__ float evalTransmittance(const MedView &M, f3 o, f3 d,
     for (int i = 0; i < 2; ++i) {
         float t = t0;
         for (;;) {
-            t -= logf(1 - rng.next1()) * M.invMax;
+            t -= trackLog(1 - rng.next1()) * M.invMax;
             if (!(t < t1)) {
                 result += 1;
                 break;
@@ -1468,15 +1468,15 @@ void pg_launch_vol_flight(hipStream_t s, const GParams &g, const SceneDev &sc, c
     else
         hipLaunchKernelGGL(k_vflight<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, med, surf, dsurf);
 }
-void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
-                          const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
-                          uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf, const Queue *nee) {
+int pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
+                         const VolWave &w, Queue med, uint32_t max_med, Queue surf, uint32_t max_surf, Queue dsurf,
+                         uint32_t max_dsurf, Queue next_flight, Queue next_surf, Queue next_dsurf, const Queue *nee) {
     // the three block ranges within TRACE_MAX_BLOCKS (the traversal stacks' overflow ring)
     const uint32_t cap = TRACE_MAX_BLOCKS / PG_QSHARDS / 4;
     const uint32_t mr = max_med ? vrows(max_med, cap) : 0;
     const uint32_t sr = max_surf ? vrows(max_surf, cap) : 0;
     const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
-    if (mr + sr + dr == 0) return;
+    if (mr + sr + dr == 0) return 0;
     const Queue qn = nee ? *nee : Queue{};
     // medium and surface interactions as two launches (each its own register budget: the medium launch at
     // 3 waves/SIMD, PG_VMEDIUM_INLINE_WAVES / PG_VMEDIUM_WAVES), or one (PG_VOL_SPLIT_VERTEX=0; read per
@@ -1501,6 +1501,7 @@ void pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, c
     }
 #undef PG_VV_ALL
 #undef PG_VV
+    return split ? (mr ? 1 : 0) + (dr + sr ? 1 : 0) : 1;  // kernels launched (bench.py's per-launch averages)
 }
 void pg_launch_vol_nee(hipStream_t s, const GParams &g, const SceneDev &sc, const VolDev &v, const VolWave &w, Queue nee,
                        uint32_t max_nee) {
@@ -1645,7 +1646,7 @@ __global__ __launch_bounds__(256) void k_medium_query(const GMedium *medium, int
         if (grid) return t0 < t1 && trackGrid(M, o, d, t0, t1, rng, tHit);
         float t = t0;
         for (;;) {
-            t -= logf(1 - rng.next1()) * M.invMax;
+            t -= trackLog(1 - rng.next1()) * M.invMax;
             if (!(t < t1)) return false;
             const float density = lookupDensity(M, o + d * t) * M.scale;
             if (density * M.invMax > rng.next1()) {

@@ -181,9 +181,15 @@ inline V3 refractV(V3 wi, V3 m, float eta, float cosThetaT) {
     return m * (dot(wi, m) * eta + cosThetaT) - wi * eta;
 }
 
-// ---- erf / erfinv (Giles 2010 single-precision fit, as used by math::erfinv)
+// ---- math::fastlog / math::fastexp as the reference builds them on Linux x86_64
+// (include/mitsuba/core/math.h:175-199): the double-precision libm call, rounded to float.  Every call
+// site the reference writes as math::fastlog / fastexp uses these; its plain std::exp / std::log stay float.
+inline float fastlog(float x) { return (float)std::log((double)x); }
+inline float fastexp(float x) { return (float)std::exp((double)x); }
+
+// ---- erf / erfinv (math.cpp:25-72): Giles 2010 single-precision fit; erf is A&S 7.1.26, not libm's
 inline float erfinvf_(float x) {
-    float w = -std::log((1.0f - x) * (1.0f + x)), p;
+    float w = -fastlog((1.0f - x) * (1.0f + x)), p;
     if (w < 5.0f) {
         w = w - 2.5f;
         p = 2.81022636e-08f;
@@ -209,6 +215,15 @@ inline float erfinvf_(float x) {
     }
     return p * x;
 }
+inline float erfAS(float x) {  // math.cpp:55-72
+    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f, a4 = -1.453152027f,
+                a5 = 1.061405429f, p = 0.3275911f;
+    const float sign = signum(x);
+    x = std::fabs(x);
+    const float t = 1.0f / (1.0f + p * x);
+    const float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * fastexp(-x * x);
+    return sign * y;
+}
 
 // ---- microfacet distribution (microfacet.h)
 struct Microfacet {
@@ -224,7 +239,7 @@ struct Microfacet {
         float be = ((m.x * m.x) / (au * au) + (m.y * m.y) / (av * av)) / c2;
         float r;
         if (type == 0) {
-            r = std::exp(-be) / (kPi * au * av * c2 * c2);
+            r = fastexp(-be) / (kPi * au * av * c2 * c2);
         } else {
             float root = (1.0f + be) * c2;
             r = 1.0f / (kPi * au * av * root * root);
@@ -277,7 +292,7 @@ struct Microfacet {
             alphaSqr = 1.0f / (cs * cs + ss * ss);
         }
         if (type == 0) {
-            float t2 = alphaSqr * -std::log(1.0f - sx);
+            float t2 = alphaSqr * -fastlog(1.0f - sx);
             cosThetaM = 1.0f / std::sqrt(1.0f + t2);
             pdf = (1.0f - sx) / (kPi * au * av * cosThetaM * cosThetaM * cosThetaM);
         } else {
@@ -293,14 +308,14 @@ struct Microfacet {
     void sampleVisible11(float thetaI, float sx, float sy, float &slx, float &sly) const {
         if (type == 0) {
             if (thetaI < 1e-4f) {
-                float r = std::sqrt(-std::log(1.0f - sx));
+                float r = std::sqrt(-fastlog(1.0f - sx));
                 slx = r * std::cos(2 * kPi * sy);
                 sly = r * std::sin(2 * kPi * sy);
                 return;
             }
             const float SQRT_PI_INV = 1 / std::sqrt(kPi);
             float tanThetaI = std::tan(thetaI), cotThetaI = 1 / tanThetaI;
-            float a = -1, c = std::erf(cotThetaI);
+            float a = -1, c = erfAS(cotThetaI);
             float sample_x = std::max(sx, 1e-6f);
             float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
             float b = c - (1 + c) * std::pow(1 - sample_x, fit);

@@ -161,7 +161,7 @@ struct Medium {
         if (!clip(o, d, mint, maxt, t0, t1)) return false;
         float t = t0;
         for (;;) {
-            t -= std::log(1 - rng.next1()) * invMax;
+            t -= fastlog(1 - rng.next1()) * invMax;
             if (!(t < t1)) return false;
             V3 p = o + d * t;
             float density = lookup(p) * scale;
@@ -216,7 +216,7 @@ struct Medium {
             const float mu = maj[((size_t)c[2] * mres[1] + c[1]) * mres[0] + c[0]];
             if (mu > 0) {
                 for (;;) {
-                    const float ts = t - std::log(1 - rng.next1()) / mu;
+                    const float ts = t - fastlog(1 - rng.next1()) / mu;
                     if (!(ts < tExit)) break;
                     t = ts;
                     const V3 p = o + d * t;
@@ -277,7 +277,7 @@ struct Medium {
         for (int i = 0; i < nSamples; ++i) {
             float t = t0;
             for (;;) {
-                t -= std::log(1 - rng.next1()) * invMax;
+                t -= fastlog(1 - rng.next1()) * invMax;
                 if (!(t < t1)) {
                     result += 1;
                     break;

@@ -201,8 +201,11 @@ def test_bsdf_parity(pg, O):
         g = dev.bsdf_query(mi, wi, u, wg)
         c = O.bsdf_query(pg.capi, m, wi, u, wg)
         same_type = g[:, 7] == c[:, 7]
-        assert same_type.mean() > 0.998, (mi, same_type.mean())
         ok = same_type & (c[:, 7] != 0)
+        rel_all = np.abs(g - c) / np.maximum(np.abs(c), 1e-6)
+        print(f"bsdf {mi}: same lobe {same_type.mean():.5f}, bit-equal rows {np.all(g == c, axis=1).mean():.5f}, "
+              f"max rel (same lobe) {rel_all[ok].max():.3g}, q999 {np.quantile(rel_all[ok].max(1), 0.999):.3g}")
+        assert same_type.mean() > 0.998, (mi, same_type.mean())
         assert np.quantile(np.abs(g[ok, 0:3] - c[ok, 0:3]).max(1), 0.999) < 2e-3, mi
         for col in (3, 4, 5, 6, 8, 9, 10, 11):
             a, b = g[:, col], c[:, col]

@@ -1,8 +1,10 @@
 """GPU parity of the volumetric path (pg_volpath.hip) against the CPU oracle (oracle/orc_volpath.h).
 
 Unit level, same inputs and the same counter-RNG draws on both sides: HG sample/eval, grid lookups,
-Woodcock free flight and transmittance estimates (identical draw counts for >= 99.9 % of rays; fp32
-results within 1e-4 relative, the device's logf/FMA differing by ulps).  Image level: per-pixel
+Woodcock free flight and transmittance estimates (identical draw counts for >= 99.9 % of rays; free-flight
+distances within 1e-6 relative: the tracking loops' device logf rounds differently from the reference's
+double-precision fastlog on 39 % of arguments, an ulp per step; measured 100 % equal draw counts and
+<= 3.2e-7, and bit-identical results with PG_TRACK_FASTLOG=1, profiles/r05x_fastlog/).  Image level: per-pixel
 z-test and overall-mean z-test on the furnace (expectation exactly 1), the absorbing slab (closed
 form) and the C5 smoke scene class at a reduced grid and resolution.
 """
@@ -34,11 +36,16 @@ def test_phase_and_medium_units(pg, O):
     wog /= np.linalg.norm(wog, axis=1, keepdims=True)
     g = dev.phase_query(0, wi, u, wog)
     c = O.hg_query(pg.capi, 0.8, wi, u, wog)
+    print(f"hg: direction max |diff| {np.abs(g[:, :3] - c[:, :3]).max():.3g}, bit-equal rows "
+          f"{np.all(g == c, axis=1).mean():.5f}, pdf/eval max rel "
+          f"{(np.abs(g[:, 3:] - c[:, 3:]) / np.maximum(np.abs(c[:, 3:]), 1e-6)).max():.3g}")
     assert np.quantile(np.abs(g[:, :3] - c[:, :3]), 0.999) < 1e-4
     assert np.quantile(np.abs(g[:, 3:] - c[:, 3:]) / np.maximum(np.abs(c[:, 3:]), 1e-6), 0.999) < 1e-4
     # grid lookups
     p = rng.uniform(-1.1, 1.1, size=(n, 3)).astype(np.float32)
-    assert np.allclose(dev.medium_lookup(0, p), osc.medium_lookup(0, p), atol=1e-6)
+    lg, lc = dev.medium_lookup(0, p), osc.medium_lookup(0, p)
+    print(f"lookups: bit-equal {np.mean(lg == lc):.5f}, max |diff| {np.abs(lg - lc).max():.3g}")
+    assert np.allclose(lg, lc, atol=1e-6)
     # Woodcock free flight / transmittance with the same draws
     rays = np.zeros((n, 8), np.float32)
     rays[:, 0:3] = rng.uniform(-1.5, 1.5, size=(n, 3))
@@ -51,11 +58,13 @@ def test_phase_and_medium_units(pg, O):
         cc = osc.medium_sample(0, rays, keys, transmittance=tr, grid=grid)
         col = 1 if tr else 2
         same = gg[:, col] == cc[:, col]
+        print(f"tracking tr={tr} grid={grid}: same lookups {same.mean():.5f}, bit-equal results "
+              f"{np.all(gg[:, :3] == cc[:, :3], axis=1).mean():.5f}")
         assert same.mean() > 0.999, (tr, grid, same.mean())
         assert np.array_equal(gg[same, 0], cc[same, 0])
         if not tr:
             hit = same & (cc[:, 0] > 0.5)
-            assert np.quantile(np.abs(gg[hit, 1] - cc[hit, 1]) / np.abs(cc[hit, 1]).clip(1e-3), 0.999) < 1e-4
+            assert np.quantile(np.abs(gg[hit, 1] - cc[hit, 1]) / np.abs(cc[hit, 1]).clip(1e-3), 0.999) < 1e-6
     dev.close()
 
 
@@ -106,7 +115,8 @@ def test_smoke_image_parity(pg, O):
     assert abs(_mean_z(g, c)) < 5
     # same counter streams on both sides: most pixels agree to fp32 noise, not just statistically
     close = np.abs(m1 - m2) <= 1e-3 * np.maximum(np.abs(m2), 1e-3)
-    assert close.mean() > 0.5, close.mean()
+    print(f"c5 smoke same streams: pixels within 1e-3 {close.mean():.4f}")
+    assert close.mean() > 0.99, close.mean()  # measured 1.0000 (profiles/r05x_fastlog/)
 
 
 def test_smoke_image_parity_global_majorant(pg, O):
@@ -210,8 +220,9 @@ def test_guided_volpath_same_tree_parity(pg, O, beta):
     assert (np.abs(z) < 5).mean() > 0.999
     assert abs(_mean_z(g, c[:2])) < 5
     close = np.abs(m1 - m2) <= 1e-3 * np.maximum(np.abs(m2), 1e-3)
-    assert close.mean() > 0.5, close.mean()
-    assert abs(nrec_gpu - nrec_cpu) <= 0.01 * nrec_cpu, (nrec_gpu, nrec_cpu)
+    print(f"c5 guided same tree beta {beta}: pixels within 1e-3 {close.mean():.4f}, records {nrec_gpu} / {nrec_cpu}")
+    assert close.mean() > 0.99, close.mean()  # measured 1.0000 / 1.0000 (profiles/r05x_fastlog/)
+    assert abs(nrec_gpu - nrec_cpu) <= 0.001 * nrec_cpu, (nrec_gpu, nrec_cpu)  # measured equal
     r = np.frombuffer(recs.tobytes(), np.float32).reshape(-1, 8)
     assert np.all(np.isfinite(r[:, [0, 1, 2, 4, 5]])) and np.all(r[:, 5] > 0)
 
