@@ -402,10 +402,22 @@ PGD float roughPlasticProbSpec(const GMat &M, float cosThetaI) {
     return (p * M.specWeight) / (p * M.specWeight + (1 - p) * (1 - M.specWeight));
 }
 
+// Compile-time BSDF model selection: MODEL >= 0 compiles that model only (the surface path's material-class
+// queues); PG_MODELS_DIFFUSE_NULL compiles the diffuse and null models only (a volumetric scene whose every
+// material is one of them: the surface launches drop the microfacet, dielectric and plastic code and its
+// registers, pg_volpath.hip k_vvertex KIND 3); -1 dispatches on M.model at run time
+constexpr int PG_MODELS_DIFFUSE_NULL = -2;
+template <int MODEL>
+PGD int modelSel(const GMat &M) {
+    if constexpr (MODEL >= 0) return MODEL;
+    else if constexpr (MODEL == PG_MODELS_DIFFUSE_NULL) return M.model == PG_BSDF_NULL ? PG_BSDF_NULL : PG_BSDF_DIFFUSE;
+    else return (int)M.model;
+}
+
 // f * cos(theta_o), solid-angle measure (BSDF::eval with ESolidAngle)
 template <int MODEL = -1>
 PGD f3 bsdfEval1(const GMat &M, f3 wi, f3 wo) {
-    switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
+    switch (modelSel<MODEL>(M)) {
         case PG_BSDF_DIFFUSE:  // diffuse.cpp:116-124
             if (wi.z <= 0 || wo.z <= 0) return mk1(0.f);
             return diffOf(M) * (kInvPi * wo.z);
@@ -459,7 +471,7 @@ PGD f3 bsdfEval1(const GMat &M, f3 wi, f3 wo) {
 
 template <int MODEL = -1>
 PGD float bsdfPdf1(const GMat &M, f3 wi, f3 wo) {
-    switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
+    switch (modelSel<MODEL>(M)) {
         case PG_BSDF_DIFFUSE:
             if (wi.z <= 0 || wo.z <= 0) return 0.0f;
             return cosineHemispherePdf(wo);
@@ -516,7 +528,7 @@ PGD float bsdfPdf1(const GMat &M, f3 wi, f3 wo) {
 // BSDF::sample(bRec, pdf, sample) -> weight = f*cos/pdf; u2 = component sample (roughdielectric)
 template <int MODEL = -1>
 PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
-    switch (MODEL >= 0 ? MODEL : (int)M.model) {  // compile-time when MODEL >= 0
+    switch (modelSel<MODEL>(M)) {
         case PG_BSDF_NULL: {  // null.cpp:64-75 (eval/pdf of the continuous measures are 0)
             bs.wo = -wi;
             bs.eta = 1.0f;
@@ -672,7 +684,7 @@ PGD f3 bsdfSample1(const GMat &M, f3 wi, float u0, float u1, float u2, BS &bs) {
 // delta models are never guided).  pg_config.glossy_prior; oracle glossyRate (orc_bsdf.h).
 template <int MODEL = -1>
 PGD float glossyRate(const GMat &M, float cosThetaI) {
-    switch (MODEL >= 0 ? MODEL : (int)M.model) {
+    switch (modelSel<MODEL>(M)) {
         case PG_BSDF_ROUGHCONDUCTOR:
         case PG_BSDF_ROUGHDIELECTRIC: return 1.0f;
         case PG_BSDF_ROUGHPLASTIC:

@@ -198,6 +198,7 @@ struct Ctx {
     bool has_env = false;
     // media (volpath)
     DevBuf media, density, tmed, majorant, tcheap;
+    bool diffuse_null = false;  // every material diffuse or null: VolDev::models (PG_VOL_MODELS=0 turns it off)
     int32_t cam_medium = -1;
     uint32_t num_media = 0;
     DevBuf vol_rad, vol_ovf, vol_work;  // per-item radiance, traversal-stack overflow, counter + stats
@@ -881,6 +882,9 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
         return fail(c, PG_ERR_INVALID, "pg_upload_scene: BVH deeper than the traversal stack");
     std::vector<float> shade((size_t)20 * nt);
     std::vector<uint8_t> tclass(nt), tcheap(nt);
+    c->diffuse_null = true;
+    for (uint32_t i = 0; i < d->num_materials; ++i)
+        if (d->materials[i].type != PG_BSDF_DIFFUSE && d->materials[i].type != PG_BSDF_NULL) c->diffuse_null = false;
     for (uint32_t k = 0; k < nt; ++k) {
         uint32_t t = bvh.order[k];
         packShade(&shade[20 * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
@@ -1528,6 +1532,10 @@ pg_status renderVolpath(Ctx *c, uint32_t spp, uint32_t sample_offset, bool rec) 
     v.media = c->media.as<GMedium>();
     v.tmed = c->tmed.as<uint32_t>();
     v.tcheap = c->tcheap.as<uint8_t>();
+    {  // the surface launches specialised to diffuse / null materials (read per pass: tests A/B it in-process)
+        const char *e = std::getenv("PG_VOL_MODELS");
+        v.models = c->diffuse_null && !(e && *e && std::atoi(e) == 0) ? 1u : 0u;
+    }
     v.cam_medium = c->cam_medium;
     v.num_media = c->num_media;
     v.rad = c->vol_rad.as<float4>();

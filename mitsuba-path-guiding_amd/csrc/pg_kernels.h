@@ -72,6 +72,7 @@ struct VolDev {
     float dist_beta;           // pg_config.distance_guiding
     uint32_t refill_min;       // k_volpath refills a wave's finished lanes once at least this many are idle
     const uint8_t *tcheap;     // per BVH-order triangle: 1 = delta BSDF or emitter (the wavefront's cheap surface queue)
+    uint32_t models;           // 1: every material is diffuse or null (surface launches compiled for those only)
 };
 
 // Volumetric wavefront (pg_volpath.hip k_vcam, k_vflight, k_vvertex, k_vtail): the megakernel's per-lane

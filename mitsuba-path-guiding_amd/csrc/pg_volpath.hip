@@ -793,7 +793,8 @@ __device__ __forceinline__ bool volMedium(const GParams &g, const SceneDev &sc, 
     }
     return volRoulette(g, P, rng);
 }
-template <bool GUIDED, bool SINK>
+// MODELS: pg_device.h modelSel (-1 any material; PG_MODELS_DIFFUSE_NULL when the scene has only those)
+template <bool GUIDED, bool SINK, int MODELS = -1>
 __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                                            VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
                                            uint32_t &shadows, VDefer &df, const VolWave &wk) {
@@ -835,9 +836,9 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
                 shadows++;
                 if (!isZero(value)) {
                     const f3 woL = h.sh.toLocal(dD);
-                    const f3 f = bsdfEval(M, h.wi, woL);
+                    const f3 f = bsdfEval<MODELS>(M, h.wi, woL);
                     if (!isZero(f) && (!g.strict_normals || dot(h.geoN, dD) * woL.z > 0)) {
-                        const float bp = bsdfPdf(M, h.wi, woL);
+                        const float bp = bsdfPdf<MODELS>(M, h.wi, woL);
                         deferNeeWalk<SINK>(df, wk, item, h.p, ep, true, m2, maxInter, ndim);
                         if (guide) {
                             neeV = (P.T * value) * f;
@@ -858,13 +859,13 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
         f3 weight;
         float woPdf;
         if (!guide) {
-            weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+            weight = bsdfSample<MODELS>(M, h.wi, b0, b1, b2, bs);
             woPdf = bs.pdf;
         } else {
             int mode = 0;  // 0: BSDF sample failed, 1: BSDF sample (D-tree pdf query), 2: D-tree sample
             float bu = 0, bw = 0;
             if (rng.next1() < alpha) {
-                weight = bsdfSample(M, h.wi, b0, b1, b2, bs);
+                weight = bsdfSample<MODELS>(M, h.wi, b0, b1, b2, bs);
                 if (!isZero(weight)) {
                     mode = 1;
                     dirToCanonical(h.sh.toWorld(bs.wo), bu, bw);
@@ -883,8 +884,8 @@ __device__ __forceinline__ bool volSurface(const GParams &g, const SceneDev &sc,
                 weight = weight * (bs.pdf / woPdf);
             } else {
                 const f3 woL = h.sh.toLocal(canonicalToDir(cu, cv));
-                const f3 f = bsdfEval(M, h.wi, woL);
-                const float bp = bsdfPdf(M, h.wi, woL);
+                const f3 f = bsdfEval<MODELS>(M, h.wi, woL);
+                const float bp = bsdfPdf<MODELS>(M, h.wi, woL);
                 woPdf = alpha * bp + (1 - alpha) * dPdf;
                 if (!(woPdf > 0) || isZero(f)) return false;
                 weight = f / woPdf;
@@ -978,7 +979,7 @@ __device__ __forceinline__ void clearDefer(VDefer &df) {
     df.k = -1;
 }
 
-template <bool GUIDED>
+template <bool GUIDED, int MODELS = -1>
 __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                                         VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
                                         uint32_t &shadows, VDefer &df) {
@@ -987,17 +988,17 @@ __device__ __forceinline__ bool volStep(const GParams &g, const SceneDev &sc, co
     const VolWave none{};
     if (P.medium >= 0 && volFlight<GUIDED>(v, sd, P, rng, mp))
         return volMedium<GUIDED, false>(g, sc, v, sd, P, rng, stk, item, segs, shadows, mp, df, none);
-    return volSurface<GUIDED, false>(g, sc, v, sd, P, rng, stk, item, segs, shadows, df, none);
+    return volSurface<GUIDED, false, MODELS>(g, sc, v, sd, P, rng, stk, item, segs, shadows, df, none);
 }
 // one step with its walks resolved right away (k_vtail, k_volpath): the same arithmetic as the wavefront's
 // k_vvertex + k_vnee
-template <bool GUIDED>
+template <bool GUIDED, int MODELS = -1>
 __device__ __forceinline__ bool volStepResolved(const GParams &g, const SceneDev &sc, const VolDev &v, const SDDev &sd,
                                                 VPath &P, VRng &rng, const TStack &stk, uint32_t item, uint32_t &segs,
                                                 uint32_t &shadows) {
     VDefer df;
     clearDefer(df);
-    const bool alive = volStep<GUIDED>(g, sc, v, sd, P, rng, stk, item, segs, shadows, df);
+    const bool alive = volStep<GUIDED, MODELS>(g, sc, v, sd, P, rng, stk, item, segs, shadows, df);
     if (df.hit || df.nee) resolveDeferred(sc, v, df, rng.key, rng.sample, item, P.L, stk, segs, rng.lookups);
     return alive;
 }
@@ -1269,6 +1270,8 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
 
 // interactions: blocks [0, mblocks) take the medium vertices, the rest the surface vertices.  KIND 2: both
 // in one launch (PG_VOL_SPLIT_VERTEX=0); KIND 0 / 1 (default): the medium / surface blocks only, as launches of
+// their own; KIND 3: the surface launch of a scene whose materials are all diffuse or null (VolDev::models),
+// compiled without the other BSDF models.  KIND 0 / 1 / 3 are launches of
 // their own, so each gets its own register budget: the medium kernel runs at 3 waves per SIMD (with the
 // walks deferred to k_vnee without scratch, PG_VMEDIUM_WAVES; with them inline 44 B/lane of scratch,
 // PG_VMEDIUM_INLINE_WAVES), the surface kernel's BSDFs need more
@@ -1294,7 +1297,7 @@ void k_vflight(GParams g, SceneDev sc, VolDev v, SDDev sd, VolWave w, Queue qf, 
 template <bool NEE_STAGE, int KIND>
 struct VVertexWaves {
     static constexpr int value = KIND == 0 ? (NEE_STAGE ? PG_VMEDIUM_WAVES : PG_VMEDIUM_INLINE_WAVES)
-                                           : (KIND == 1 ? (NEE_STAGE ? PG_VSURFACE_WAVES : PG_VSURFACE_INLINE_WAVES)
+                                           : (KIND == 1 || KIND == 3 ? (NEE_STAGE ? PG_VSURFACE_WAVES : PG_VSURFACE_INLINE_WAVES)
                                                         : PG_VVERTEX_WAVES);
 };
 template <bool GUIDED, bool NEE_STAGE, int KIND>
@@ -1330,7 +1333,8 @@ __global__ __launch_bounds__(TRACE_BLOCK, (VVertexWaves<NEE_STAGE, KIND>::value)
             if (KIND == 0 || (KIND == 2 && medium))
                 alive = volMedium<GUIDED, NEE_STAGE>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, xyz(w.mp[slot]), df, w);
             else
-                alive = volSurface<GUIDED, NEE_STAGE>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, df, w);
+                alive = volSurface<GUIDED, NEE_STAGE, KIND == 3 ? PG_MODELS_DIFFUSE_NULL : -1>(g, sc, v, sd, P, rng, stk,
+                                                                                          slot, segs, shadows, df, w);
             vertices++;
             const bool ended = !(alive && volDepthOk(g, P));
             const uint32_t key0 = rng.key, sample0 = rng.sample;
@@ -1406,7 +1410,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VNEE_WAVES) void k_vnee(GParams g, 
 #ifndef PG_VTAIL_WAVES
 #define PG_VTAIL_WAVES 3  // C5 442.3 / 441.9 against 439.2 / 439.6 at 2 (profiles/r05q_vol_waves/)
 #endif
-template <bool GUIDED>
+template <bool GUIDED, int MODELS>
 __global__ __launch_bounds__(TRACE_BLOCK, PG_VTAIL_WAVES) void k_vtail(GParams g, SceneDev sc, VolDev v, SDDev sd,
                                                                      VolWave w, Queue qf, Queue qs, Queue qd,
                                                                      uint32_t fblocks, uint32_t dblocks) {
@@ -1429,10 +1433,10 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VTAIL_WAVES) void k_vtail(GParams g
         if (!flight) {
             VDefer df;
             clearDefer(df);
-            alive = volSurface<GUIDED, false>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, df, w);
+            alive = volSurface<GUIDED, false, MODELS>(g, sc, v, sd, P, rng, stk, slot, segs, shadows, df, w);
             if (df.hit || df.nee) resolveDeferred(sc, v, df, rng.key, rng.sample, slot, P.L, stk, segs, rng.lookups);
         }
-        while (alive) alive = volStepResolved<GUIDED>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
+        while (alive) alive = volStepResolved<GUIDED, MODELS>(g, sc, v, sd, P, rng, stk, slot, segs, shadows);
         volEnd(v, slot, P, rng, lookups);
     }
     volStats(v, segs, shadows, lookups);
@@ -1492,7 +1496,8 @@ int pg_launch_vol_vertex(hipStream_t s, const GParams &g, const SceneDev &sc, co
         PG_VV(GU, NS, 2, mr + dr + sr, PG_QSHARDS * mr);                                                             \
     } else {                                                                                                         \
         if (mr) PG_VV(GU, NS, 0, mr, PG_QSHARDS * mr);                                                               \
-        if (dr + sr) PG_VV(GU, NS, 1, dr + sr, 0u);                                                                  \
+        if (dr + sr && v.models) PG_VV(GU, NS, 3, dr + sr, 0u);                                                      \
+        else if (dr + sr) PG_VV(GU, NS, 1, dr + sr, 0u);                                                             \
     }
     if (g.guiding) {
         if (nee) { PG_VV_ALL(true, true) } else { PG_VV_ALL(true, false) }
@@ -1521,12 +1526,15 @@ void pg_launch_vol_tail(hipStream_t s, const GParams &g, const SceneDev &sc, con
     const uint32_t dr = max_dsurf ? vrows(max_dsurf, cap) : 0;
     if (fr + sr + dr == 0) return;
     const dim3 grid(PG_QSHARDS * (fr + dr + sr));
-    if (g.guiding)
-        hipLaunchKernelGGL(k_vtail<true>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, dsurf,
-                           PG_QSHARDS * fr, PG_QSHARDS * dr);
-    else
-        hipLaunchKernelGGL(k_vtail<false>, grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, dsurf,
-                           PG_QSHARDS * fr, PG_QSHARDS * dr);
+#define PG_VT(GU, MO)                                                                                                \
+    hipLaunchKernelGGL((k_vtail<GU, MO>), grid, dim3(TRACE_BLOCK), 0, s, g, sc, v, sd, w, flight, surf, dsurf,      \
+                       PG_QSHARDS * fr, PG_QSHARDS * dr)
+    if (g.guiding) {
+        if (v.models) PG_VT(true, PG_MODELS_DIFFUSE_NULL); else PG_VT(true, -1);
+    } else {
+        if (v.models) PG_VT(false, PG_MODELS_DIFFUSE_NULL); else PG_VT(false, -1);
+    }
+#undef PG_VT
 }
 
 namespace {

@@ -202,17 +202,28 @@ def test_bsdf_parity(pg, O):
         c = O.bsdf_query(pg.capi, m, wi, u, wg)
         same_type = g[:, 7] == c[:, 7]
         ok = same_type & (c[:, 7] != 0)
-        rel_all = np.abs(g - c) / np.maximum(np.abs(c), 1e-6)
+        qv = []
+        for col in (3, 4, 5, 6, 8, 9, 10, 11):
+            sel = (ok if col < 8 else np.ones(n, bool)) & (np.abs(c[:, col]) > 1e-6)
+            if sel.sum():
+                qv.append(np.quantile(np.abs(g[sel, col] - c[sel, col]) / np.abs(c[sel, col]), 0.999))
         print(f"bsdf {mi}: same lobe {same_type.mean():.5f}, bit-equal rows {np.all(g == c, axis=1).mean():.5f}, "
-              f"max rel (same lobe) {rel_all[ok].max():.3g}, q999 {np.quantile(rel_all[ok].max(1), 0.999):.3g}")
-        assert same_type.mean() > 0.998, (mi, same_type.mean())
-        assert np.quantile(np.abs(g[ok, 0:3] - c[ok, 0:3]).max(1), 0.999) < 2e-3, mi
+              f"direction q999 {np.quantile(np.abs(g[ok, 0:3] - c[ok, 0:3]).max(1), 0.999):.3g}, "
+              f"value columns q999 rel {max(qv):.3g}")
+        # round 5 (profiles/r05x_fastlog/r05ab/bsdf.log): every model but roughplastic within 2.7e-5 of the
+        # oracle (directions 1.7e-6) at the 99.9th percentile, 34-100 % of rows bit for bit.  roughplastic's
+        # rough-transmittance tables come from two quadratures of the same integral (csrc/pg_rtrans.cpp over
+        # normals, orc_rtrans.h over roughdielectric's sample square; both within ~1e-4 of the shipped
+        # .dat tables, tests/test_rtrans.py): 8.0e-3 / 8.5e-4 measured
+        assert same_type.mean() > 0.9995, (mi, same_type.mean())
+        tol_dir, tol_val = (2e-3, 1e-2) if m.type == pg.capi.PG_BSDF_ROUGHPLASTIC else (2e-5, 2e-4)
+        assert np.quantile(np.abs(g[ok, 0:3] - c[ok, 0:3]).max(1), 0.999) < tol_dir, mi
         for col in (3, 4, 5, 6, 8, 9, 10, 11):
             a, b = g[:, col], c[:, col]
             sel = (ok if col < 8 else np.ones(n, bool)) & (np.abs(b) > 1e-6)
             rel = np.abs(a[sel] - b[sel]) / np.abs(b[sel])
             if sel.sum():
-                assert np.quantile(rel, 0.999) < 1e-2, (mi, col, np.quantile(rel, 0.999))
+                assert np.quantile(rel, 0.999) < tol_val, (mi, col, np.quantile(rel, 0.999))
     dev.close()
 
 

@@ -227,6 +227,24 @@ def test_guided_volpath_same_tree_parity(pg, O, beta):
     assert np.all(np.isfinite(r[:, [0, 1, 2, 4, 5]])) and np.all(r[:, 5] > 0)
 
 
+def test_diffuse_null_surface_kernels_bit_identical(pg, monkeypatch):
+    """A scene whose materials are all diffuse or null runs the surface launches compiled for those two
+    models only (VolDev::models, k_vvertex KIND 3, k_vtail): the same arithmetic for every material it
+    has, so the guided job's film, tree and records are bit-identical to the generic kernels'."""
+    from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer
+    sc = pg.scenes.smoke(64, 64, res=48)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PG_VOL_MODELS", flag)
+        t = GuidedVolumetricPathTracer({"trainingIterations": 3, "samplesPerProgression": 8})
+        t.preprocess(sc)
+        rgbw, sq = t.render(16)
+        out.append((rgbw, sq, t.dev.get_sdtree()))
+        t.postprocess()
+    for a, b in zip(out[0], out[1]):
+        assert np.array_equal(a, b)
+
+
 def test_volpath_refill_threshold_bit_identical(pg, monkeypatch):
     """k_volpath refills a wave's idle lanes in batches (VolDev.refill_min, PG_VOL_REFILL): every
     work item draws from its own stream and writes its own slots, so films and trees must not depend
