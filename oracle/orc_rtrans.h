@@ -5,13 +5,13 @@
 //       int_0^1 2 x T(x) dx over the cubic-interpolated table; theta grid cos = t^4, t_0 = step/10
 //   src/bsdfs/rtrans.h              eval = Catmull-Rom in cos^(1/4) over the table, clamped
 //   src/bsdfs/roughplastic.cpp:283-299  external table at eta, Fdr = 1 - internal diffuse at 1/eta
-// The sample square is integrated on a midpoint grid of roughdielectric's sampleVisible=false
-// path (Walter et al.: m drawn from D cos with alpha scaled by 1.2 - 0.2 sqrt|cos theta_i|, weight
-// |D G <wi, m> / (pdf cos theta_i)| (1 - F)).  That estimator reproduces the shipped .dat tables
-// to ~1e-4; the visible-normal path differs by ~3e-3 for Beckmann, whose G1 is Walter's rational
-// approximation while visible-normal sampling is normalised with the exact one.  The library
-// integrates the same quantity over normals (csrc/pg_rtrans.cpp); tests/test_rtrans.py compares
-// both with the reference's .dat slices.
+// T(wi) is the transmission albedo of the rough interface, integrated over the microfacet normals in
+// double (rtAlbedo below, the same quadrature as csrc/pg_rtrans.cpp since round 5, so oracle and library
+// hold the same tables).  Round 4's estimator integrated the sample square of roughdielectric's
+// sampleVisible=false path (Walter et al.: alpha scaled by 1.2 - 0.2 sqrt|cos theta_i|); it reproduced the
+// shipped .dat tables to ~1e-4 as this one does (tests/test_rtrans.py compares both sides with them); the
+// visible-normal path differs by ~3e-3 for Beckmann, whose G1 is Walter's rational approximation while
+// visible-normal sampling is normalised with the exact one.
 #pragma once
 #include <cmath>
 #include <thread>
@@ -42,47 +42,86 @@ inline float rtransEval(const float *tab, float cosTheta) {
     return std::min(1.0f, std::max(0.0f, r));
 }
 
-// roughdielectric transmission-only sample weight, importance mode, sampleVisible=false
-// (roughdielectric.cpp:431-518)
-inline double transmissionWeight(const Microfacet &d, float eta, V3 wi, float u0, float u1) {
-    Microfacet sd = d;
-    const float s = 1.2f - 0.2f * std::sqrt(std::fabs(wi.z));
-    sd.au *= s;
-    sd.av *= s;
-    float mpdf;
-    V3 m = sd.sample(wi, u0, u1, mpdf);
-    if (mpdf == 0) return 0.0;
-    float cosThetaT;
-    float F = fresnelDielectricExt(dot(wi, m), cosThetaT, eta);
-    if (cosThetaT == 0) return 0.0;
-    V3 wo = refractV(wi, m, eta, cosThetaT);
-    if (wi.z * wo.z >= 0) return 0.0;
-    return (double)(1 - F) * std::fabs(d.eval(m) * d.G(wi, wo, m) * dot(wi, m) / (mpdf * wi.z));
+// T(wi), the transmission albedo of the rough interface (rdielprec.cpp:40-110 estimates it by sampling
+// roughdielectric's transmission-only weight over the sample square).  Round 5: the same integral over the
+// microfacet normals as the library (csrc/pg_rtrans.cpp), in double with the same operation order and
+// quadrature, so the oracle's and the kernels' roughplastic tables are the same floats and the BSDF unit
+// parity of roughplastic is as tight as the other models'.  The integrand: normals drawn with density
+// D(m) cos(theta_m) (sampleAll's mapping, microfacet.h:354-420) on an N x N midpoint grid, u -> 1 - (1 - u)^2
+// for GGX's tail, reweighted to the visible-normal density G1(wi, m) <wi, m> D(m) / cos(theta_i) and times
+// (1 - F) G1(wo, m) for the refracted wo.  Both sides stay pinned to the shipped .dat slices
+// (tests/test_rtrans.py); round 4's sample-square estimator agreed with this one to < 1e-3.
+inline double rtG1(int dist, double alpha, const double v[3], const double m[3]) {  // microfacet.h:556-600
+    const double vm = v[0] * m[0] + v[1] * m[1] + v[2] * m[2];
+    if (vm * v[2] <= 0) return 0.0;
+    const double sin2 = 1.0 - v[2] * v[2];
+    if (sin2 <= 0) return 1.0;
+    const double tanTheta = std::fabs(std::sqrt(sin2) / v[2]);
+    if (tanTheta == 0) return 1.0;
+    if (dist == 0) {  // Beckmann: Walter's rational approximation
+        const double a = 1.0 / (alpha * tanTheta);
+        if (a >= 1.6) return 1.0;
+        return (3.535 * a + 2.181 * a * a) / (1.0 + 2.276 * a + 2.577 * a * a);
+    }
+    const double root = alpha * tanTheta;
+    return 2.0 / (1.0 + std::sqrt(1.0 + root * root));
+}
+inline double rtFresnel(double cosI, double eta, double &cosT) {  // fresnelDielectricExt in double
+    if (eta == 1) {
+        cosT = -cosI;
+        return 0.0;
+    }
+    const double scale = cosI > 0 ? 1.0 / eta : eta;
+    const double cosT2 = 1 - (1 - cosI * cosI) * (scale * scale);
+    if (cosT2 <= 0) {
+        cosT = 0;
+        return 1.0;
+    }
+    const double ci = std::fabs(cosI), ct = std::sqrt(cosT2);
+    const double Rs = (ci - eta * ct) / (ci + eta * ct), Rp = (eta * ci - ct) / (eta * ci + ct);
+    cosT = cosI > 0 ? -ct : ct;
+    return 0.5 * (Rs * Rs + Rp * Rp);
+}
+inline double rtAlbedo(int dist, double alpha, double eta, double cosThetaI, int N) {
+    const double kPiD = 3.14159265358979323846;
+    const double wi[3] = {std::sqrt(std::max(0.0, 1 - cosThetaI * cosThetaI)), 0.0, cosThetaI};
+    double sum = 0;
+    for (int a = 0; a < N; ++a) {
+        const double u = (a + 0.5) / N, sx = 1.0 - (1.0 - u) * (1.0 - u), jac = 2.0 * (1.0 - u);
+        const double tan2 = dist == 0 ? alpha * alpha * -std::log(1.0 - sx) : alpha * alpha * sx / (1.0 - sx);
+        const double cosM = 1.0 / std::sqrt(1.0 + tan2), sinM = std::sqrt(std::max(0.0, 1 - cosM * cosM));
+        double row = 0;
+        for (int b = 0; b < N; ++b) {
+            const double phi = 2 * kPiD * (b + 0.5) / N;
+            const double m[3] = {sinM * std::cos(phi), sinM * std::sin(phi), cosM};
+            const double wim = wi[0] * m[0] + wi[1] * m[1] + wi[2] * m[2];
+            if (wim <= 0) continue;
+            const double w = rtG1(dist, alpha, wi, m) * wim / (cosThetaI * cosM);
+            if (w == 0) continue;
+            double cosT;
+            const double F = rtFresnel(wim, eta, cosT);
+            if (cosT == 0) continue;
+            const double sc = cosT < 0 ? 1.0 / eta : eta;  // refract (roughdielectric.cpp)
+            const double wo[3] = {m[0] * (wim * sc + cosT) - wi[0] * sc, m[1] * (wim * sc + cosT) - wi[1] * sc,
+                                  m[2] * (wim * sc + cosT) - wi[2] * sc};
+            if (wi[2] * wo[2] >= 0) continue;
+            row += w * (1 - F) * rtG1(dist, alpha, wo, m);
+        }
+        sum += row * jac;
+    }
+    return sum / ((double)N * N);
 }
 
-inline void rtransTable(int dist, float alpha, float eta, std::vector<float> &out) {
+inline void rtransTable(int dist, double alpha, double eta, std::vector<float> &out) {
     out.assign(kRtransSamples, 0.0f);
-    const Microfacet d(dist, alpha, alpha, false);
-    const int N = 200;
     const double step = 1.0 / (kRtransSamples - 1);
     unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> pool;
     for (unsigned t = 0; t < nt; ++t)
         pool.emplace_back([&, t] {
             for (int i = (int)t; i < kRtransSamples; i += (int)nt) {
-                double x = i == 0 ? step / 10 : i * step;
-                float c = (float)std::pow(x, 4.0);
-                V3 wi(std::sqrt(std::max(0.0f, 1 - c * c)), 0.0f, c);
-                // u0 = 1 - (1 - v)^2 (Jacobian 2 (1 - v)) resolves GGX's heavy tail near u0 = 1
-                double acc = 0;
-                for (int a = 0; a < N; ++a) {
-                    const double v = (a + 0.5) / N;
-                    const float u0 = (float)(1.0 - (1.0 - v) * (1.0 - v));
-                    double row = 0;
-                    for (int b = 0; b < N; ++b) row += transmissionWeight(d, eta, wi, u0, (b + 0.5f) / N);
-                    acc += row * 2.0 * (1.0 - v);
-                }
-                out[i] = (float)(acc / ((double)N * N));
+                const double x = i == 0 ? step / 10 : i * step;  // rdielprec.cpp:87-90: cos = t^4
+                out[i] = (float)rtAlbedo(dist, alpha, eta, std::pow(x, 4.0), 128);
             }
         });
     for (auto &th : pool) th.join();
@@ -92,7 +131,7 @@ inline void rtransTable(int dist, float alpha, float eta, std::vector<float> &ou
 inline void roughPlasticTables(int dist, float alpha, float eta, std::vector<float> &ext, float &fdrInt) {
     std::vector<float> in;
     rtransTable(dist, alpha, eta, ext);
-    rtransTable(dist, alpha, 1.0f / eta, in);
+    rtransTable(dist, alpha, 1.0 / (double)eta, in);
     const int M = 1 << 14;
     double acc = 0;
     for (int i = 0; i < M; ++i) {

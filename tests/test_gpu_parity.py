@@ -211,12 +211,11 @@ def test_bsdf_parity(pg, O):
               f"direction q999 {np.quantile(np.abs(g[ok, 0:3] - c[ok, 0:3]).max(1), 0.999):.3g}, "
               f"value columns q999 rel {max(qv):.3g}")
         # round 5 (profiles/r05x_fastlog/r05ab/bsdf.log): every model but roughplastic within 2.7e-5 of the
-        # oracle (directions 1.7e-6) at the 99.9th percentile, 34-100 % of rows bit for bit.  roughplastic's
-        # rough-transmittance tables come from two quadratures of the same integral (csrc/pg_rtrans.cpp over
-        # normals, orc_rtrans.h over roughdielectric's sample square; both within ~1e-4 of the shipped
-        # .dat tables, tests/test_rtrans.py): 8.0e-3 / 8.5e-4 measured
+        # oracle (directions 1.7e-6) at the 99.9th percentile, 34-100 % of rows bit for bit.  roughplastic
+        # (8.0e-3 then: two quadratures of its rough-transmittance tables) now shares the library's tables
+        # bit for bit (tests/test_rtrans.py)
         assert same_type.mean() > 0.9995, (mi, same_type.mean())
-        tol_dir, tol_val = (2e-3, 1e-2) if m.type == pg.capi.PG_BSDF_ROUGHPLASTIC else (2e-5, 2e-4)
+        tol_dir, tol_val = 2e-5, 2e-4
         assert np.quantile(np.abs(g[ok, 0:3] - c[ok, 0:3]).max(1), 0.999) < tol_dir, mi
         for col in (3, 4, 5, 6, 8, 9, 10, 11):
             a, b = g[:, col], c[:, col]

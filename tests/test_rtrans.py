@@ -5,7 +5,9 @@ per material in RoughPlastic::configure (roughplastic.cpp:283-299, rtrans.h setE
 evalDiffuse).  tests/golden/rtrans_slices.npz holds those reductions for four (distribution, eta,
 alpha) cases (made by tests/golden/make_rtrans_fixture.py from the .dat files).  The library
 (pg_rough_transmittance, host-only) and the oracle integrate the same quantity directly at the
-material's (eta, alpha) with different estimators; both must agree with the shipped tables.
+material's (eta, alpha), both with the same double-precision quadrature over the microfacet normals
+(round 5; until then the oracle sampled roughdielectric's sample square, which agreed to < 1e-3), so
+their tables are the same floats; both must agree with the shipped tables.
 """
 import os
 
@@ -45,7 +47,7 @@ def test_library_vs_oracle_and_limits(pg, O):
     for dist, eta, alpha in [(0, 1.3, 0.05), (1, 2.0, 0.5), (0, 1.6, 1.5)]:
         t, f = rough_transmittance(dist, alpha, eta)
         to, fo = O.rough_transmittance(pg.capi, dist, alpha, eta)
-        assert np.abs(t - to).max() < 1e-3 and abs(f - fo) < 1e-3
+        assert np.array_equal(t, to) and f == fo
         # normal incidence of a nearly smooth interface: 1 - Fresnel reflectance
         if alpha <= 0.05:
             assert abs(t[-1] - (1 - ((eta - 1) / (eta + 1)) ** 2)) < 2e-3
