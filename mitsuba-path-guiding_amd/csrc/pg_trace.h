@@ -105,11 +105,22 @@ struct WStack {
 // Triangle test of every walk (pg_layout.h PG_TRIACCEL): a hit at t in [tmin, tmax] with (bu, bv) the
 // barycentric weights of p1 and p2.  TriAccel::rayIntersect (triaccel.h:96-157) with the reference's
 // expression order and no contraction: the oracle's t, u, v bit for bit.
+// PG_TRI_PRELOAD=1: the record's three rows loaded together up front instead of rows 1 and 2 only for the
+// lanes whose earlier tests pass (the later rows are cache hits of the same lines): k_rays 23.72-23.83
+// against 23.82-23.91 ms per calibration pass, C3 609-613 against 613-621 Mpaths/s (profiles/r05af_tri_preload/);
+// off by default
+#ifndef PG_TRI_PRELOAD
+#define PG_TRI_PRELOAD 0
+#endif
 __device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
                                        float &tt, float &bu, float &bv) {
 #if PG_TRIACCEL
 #pragma clang fp contract(off)
     const float4 r0 = tris[3 * tr + 0];
+#if PG_TRI_PRELOAD
+    const float4 r1 = tris[3 * tr + 1];
+    const float2 r2 = *reinterpret_cast<const float2 *>(tris + 3 * tr + 2);
+#endif
     const uint32_t k = __float_as_uint(r0.w);  // projection axis; (u, v) = the next two axes cyclically
     const float ou = k == 0 ? o.y : (k == 1 ? o.z : o.x), ov = k == 0 ? o.z : (k == 1 ? o.x : o.y);
     const float ok = k == 0 ? o.x : (k == 1 ? o.y : o.z);
@@ -117,11 +128,15 @@ __device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t
     const float dk = k == 0 ? d.x : (k == 1 ? d.y : d.z);
     tt = (r0.z - ou * r0.x - ov * r0.y - ok) / (du * r0.x + dv * r0.y + dk);
     if (!(tt >= tmin && tt <= tmax)) return false;
+#if !PG_TRI_PRELOAD
     const float4 r1 = tris[3 * tr + 1];
+#endif
     const float hu = ou + tt * du - r1.x, hv = ov + tt * dv - r1.y;
     const float u = hv * r1.z + hu * r1.w;
     if (!(u >= 0.0f)) return false;
+#if !PG_TRI_PRELOAD
     const float2 r2 = *reinterpret_cast<const float2 *>(tris + 3 * tr + 2);
+#endif
     const float v = hu * r2.x + hv * r2.y;
     if (!(v >= 0.0f && u + v <= 1.0f)) return false;
     bu = u;
