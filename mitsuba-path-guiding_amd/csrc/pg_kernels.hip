@@ -153,7 +153,14 @@ __device__ __forceinline__ void classAppend(int cls, uint32_t slot, const ClassQ
 // ENV: the scene has an environment emitter (escaped paths pick up its radiance)
 // first: the camera rays' bounce with denoiser features on (pg_config.aovs): the hit record of every
 // path also goes to p.aov, which k_film resolves into albedo and normal (nullptr: off)
-template <bool ENV, bool LTOP>
+// WIDE (PG_CLOSEST_WIDE, A/B): the closest hits walk the shadow rays' 8-wide quantised BVH (octant order,
+// boxes culled at tmax; no slab padding) instead of the 4-wide nodes: k_rays 29.4 against 23.9 ms per
+// calibration pass, C3 549-553 against 616-621 Mpaths/s (profiles/r05ag_closest_wide/): octant order
+// visits more boxes than the 4-wide walk's sorted descent saves in node fetches
+#ifndef PG_CLOSEST_WIDE
+#define PG_CLOSEST_WIDE 0
+#endif
+template <bool ENV, bool LTOP, bool WIDE = false>
 __device__ __forceinline__ void traceRows(const GParams &g, const SceneDev &sc, const PathDev &p, const Queue &q,
                                           const ClassQueues &cqs, float4 *first, uint32_t bid, uint32_t nblk,
                                           const TStack &stk, const float4 *top, int ntop) {
@@ -171,7 +178,12 @@ __device__ __forceinline__ void traceRows(const GParams &g, const SceneDev &sc, 
             float tmax = d.w;
             uint32_t tri = 0xFFFFFFFFu;
             float u = 0, v = 0;
-            bool h = traverse<false, LTOP>(sc.nodes, sc.tris, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk, top, ntop);
+            bool h;
+            if constexpr (WIDE)
+                h = traverseWide<false>(sc.wnodes, sc.wtris, xyz(o), xyz(d), o.w, tmax, tri, u, v,
+                                        WStack{stk.lds, stk.ovf, stk.ostride});
+            else
+                h = traverse<false, LTOP>(sc.nodes, sc.tris, xyz(o), xyz(d), o.w, tmax, tri, u, v, stk, top, ntop);
             float4 hr = make_float4(h ? tmax : 0.0f, __uint_as_float(h ? tri : 0xFFFFFFFFu), u, v);
             if (first) first[slot] = hr;
             if (ENV && !h) {
@@ -264,7 +276,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_
             for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_TOP_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
             __syncthreads();
         }
-        traceRows<ENV, PG_RAYS_LDS_TOP != 0>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks,
+        traceRows<ENV, PG_RAYS_LDS_TOP != 0, PG_CLOSEST_WIDE != 0>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks,
                                              threadStack(stack, p.stack_ovf), top, ntop);
     }
 #else
