@@ -767,7 +767,8 @@ struct SDView {
     const uint4 *meta;      // per D-tree: sampling root, building root, count, bits(samplingTotal)
     const float4 *qsum;     // sampling nodes, interleaved: node n = {qsum[2n] energies, qchild[2n] children}
     const uint4 *qchild;    // = (const uint4 *)(qsum + 1)
-    const uint32_t *jump;   // S-tree jump grid: (2^jumpBits)^3 cells -> node at depth <= 3*jumpBits
+    const uint32_t *jump;   // S-tree jump grid: (2^jumpBits)^3 cells -> node at depth <= 3*jumpBits, or
+                            // 0x80000000 | D-tree id where the cell lies inside one leaf (k_sd_jump)
     float3 lo;
     float extent;           // cube edge; lookups divide by it (bit-identical with the host spec)
     int jumpBits;
@@ -786,6 +787,7 @@ PGD uint32_t sdLookup(const SDView &v, f3 p) {
     const float fR = (float)R;
     int ix = min((int)(q[0] * fR), R - 1), iy = min((int)(q[1] * fR), R - 1), iz = min((int)(q[2] * fR), R - 1);
     uint32_t n = v.jump[((size_t)iz * R + iy) * R + ix];
+    if (n & 0x80000000u) return n & 0x7FFFFFFFu;  // the cell lies inside one leaf: its D-tree id
     uint2 nd = v.snodes[n];
     if (nd.x == 0xFFFFFFFFu) return nd.y;
     q[0] = q[0] * fR - (float)ix;

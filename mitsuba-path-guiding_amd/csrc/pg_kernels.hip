@@ -1396,7 +1396,9 @@ __global__ __launch_bounds__(256) void k_sd_jump(const uint2 *__restrict__ snode
         if (nd.x == 0xFFFFFFFFu) break;
         n = ((xyz[d % 3] >> (bits - 1 - d / 3)) & 1u) ? nd.y : nd.x;
     }
-    jump[cell] = n;
+    // a cell inside one leaf holds the leaf's D-tree id, flagged (pg_device.h sdLookup: one load, not two)
+    const uint2 nd = snodes[n];
+    jump[cell] = nd.x == 0xFFFFFFFFu ? (0x80000000u | nd.y) : n;
 }
 void pg_launch_sd_jump(hipStream_t s, const uint32_t *snodes, int bits, uint32_t *jump) {
     const uint32_t n = 1u << (3 * bits);

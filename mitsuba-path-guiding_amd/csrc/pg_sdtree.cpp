@@ -236,9 +236,11 @@ static void fillJump(const std::vector<uint32_t> &sn, uint32_t node, int depth, 
                      uint32_t z0, uint32_t sx, uint32_t sy, uint32_t sz, uint32_t *jump) {
     const uint32_t R = 1u << k;
     if (sn[2 * node] == kLeafMark || depth == 3 * k) {
+        // k_sd_jump's encoding: a leaf's cells hold its D-tree id, flagged
+        const uint32_t v = sn[2 * node] == kLeafMark ? (0x80000000u | sn[2 * node + 1]) : node;
         for (uint32_t z = z0; z < z0 + sz; ++z)
             for (uint32_t y = y0; y < y0 + sy; ++y)
-                for (uint32_t x = x0; x < x0 + sx; ++x) jump[((size_t)z * R + y) * R + x] = node;
+                for (uint32_t x = x0; x < x0 + sx; ++x) jump[((size_t)z * R + y) * R + x] = v;
         return;
     }
     const int axis = depth % 3;

@@ -57,7 +57,7 @@ struct SdTree {
         uint32_t *bchild;  // 4 per building node (absolute)
         uint64_t *bsum;    // 4 per building node
         uint64_t *count;   // per leaf
-        uint32_t *jump;    // (2^kJumpBits)^3 S-tree node ids, index (z * R + y) * R + x (nullptr: skipped)
+        uint32_t *jump;    // (2^kJumpBits)^3 S-tree node ids or 0x80000000 | D-tree id inside one leaf, index (z * R + y) * R + x (nullptr: skipped)
         uint64_t *frac;    // kFracStats per leaf
     };
     void flattenInto(const Layout &d) const;
