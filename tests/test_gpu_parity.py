@@ -321,6 +321,58 @@ def test_sdtree_splat_refit_bitexact(pg, O, scenes):
     dev.close()
 
 
+def test_sdtree_deep_lookup_matches_oracle(pg, O, scenes):
+    """An S-tree far deeper than the 64^3 jump grid resolves (records concentrated in a tiny cube, a low
+    split threshold): lookups there take the grid's node entry and descend the rest of the way
+    (pg_device.h sdLookup / sdDescend; most cells of trained trees hold a leaf's D-tree id), and must
+    match the oracle's plain descent."""
+    sc = scenes["cornell"]
+    cfg = pg.capi.default_config(guiding=1, s_tree_threshold=50.0)
+    osc = O.OracleScene(pg.capi, sc)
+    otree = O.OracleSDTree(osc)
+    dev = make_dev(pg, sc, guiding=1, s_tree_threshold=50.0)
+    lo, hi = (np.asarray(b, np.float64) for b in sc.bounds())
+    centre = lo + 0.3 * (hi - lo)
+    rng = np.random.default_rng(11)
+    rec_t = np.dtype([("pos", "<f4", 3), ("dir", "<u4"), ("radiance", "<f4"), ("wo_pdf", "<f4"),
+                      ("product", "<f4"), ("weight", "<f4")])
+    assert rec_t.itemsize == 32
+    for it in range(3):
+        n = 200_000
+        r = np.zeros(n, rec_t)
+        r["pos"] = centre + (hi - lo) * 1e-5 * (rng.random((n, 3)) - 0.5)
+        r["dir"] = rng.integers(0, 2 ** 32, size=n, dtype=np.uint32)
+        r["radiance"] = rng.random(n).astype(np.float32) + 0.1
+        r["wo_pdf"] = 0.25
+        r["weight"] = -1.0
+        recs = r.view(np.uint8)
+        dev.splat_records(recs)
+        otree.splat_bytes(recs)
+        dev.refit(it)
+        otree.refit(it, cfg)
+        assert np.array_equal(dev.get_sdtree(), otree.serialize()), it
+    blob = otree.serialize().tobytes()  # header 16 + box 32 + counts 16, then the S-tree node pairs
+    ns = int(np.frombuffer(blob, np.uint32, 1, 48)[0])
+    sn = np.frombuffer(blob, np.uint32, 2 * ns, 64).reshape(-1, 2)
+    depth, stack, deepest = {0: 0}, [0], 0
+    while stack:
+        k = stack.pop()
+        deepest = max(deepest, depth[k])
+        if sn[k, 0] != 0xFFFFFFFF:
+            for c in sn[k]:
+                depth[int(c)] = depth[k] + 1
+                stack.append(int(c))
+    assert deepest > 3 * 6, deepest  # deeper than the 2^6-per-axis jump grid resolves (measured 35)
+    m = 50_000
+    pos = np.concatenate([centre + (hi - lo) * 2e-5 * (rng.random((m, 3)) - 0.5),
+                          lo + (hi - lo) * rng.random((m, 3))]).astype(np.float32)
+    d = rng.normal(size=(2 * m, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    gp, cp = dev.sdtree_pdf(pos, d), otree.pdf(pos, d)
+    assert (np.abs(gp - cp) <= 1e-5 * np.abs(cp)).mean() > 0.999
+    dev.close()
+
+
 def test_guided_training_parity(pg, O, scenes):
     """Guided training on GPU vs oracle: same number of records per iteration (within MC noise),
     and the guided image agrees with the unguided oracle image (guiding is unbiased)."""
