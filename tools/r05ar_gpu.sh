@@ -1,13 +1,11 @@
 #!/bin/bash
 # round 5 (ar): every hit in one shading class with run-time BSDF dispatch (ab/one, PG_ONE_CLASS=1; the queue
 # then stays in rough slot order, so the SoA state reads coalesce) against the material-class queues: the C3
-# guided parity test on the variant, then C3 x3 interleaved
+# variant changes results (delta vertices take the guided class's record path: parity_one.log), then C3 x3
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r05ar
 mkdir -p $O
-# PG_LIB=ab/one/libpgamd.so timeout -k 10 300 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -m gpu -q -rP --timeout 250 --timeout-method thread > $O/parity_one.log 2>&1; s=$?
-true
 for i in 1 2 3; do
   PG_LIB=ab/one/libpgamd.so timeout -k 10 240 python bench.py --no-cpu --no-quality > $O/c3_one_$i.log 2>&1 || exit 1
   timeout -k 10 240 python bench.py --no-cpu --no-quality > $O/c3_cls_$i.log 2>&1 || exit 1
