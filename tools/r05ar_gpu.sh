@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5 (ar): every hit in one shading class with run-time BSDF dispatch (ab/one, PG_ONE_CLASS=1; the queue
 # then stays in rough slot order, so the SoA state reads coalesce) against the material-class queues: the C3
-# variant changes results (delta vertices take the guided class's record path: parity_one.log), then C3 x3
+# variant's results differ from the class-queue build (parity_one.log, cause not investigated), then C3 x3
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r05ar
