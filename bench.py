@@ -11,9 +11,11 @@ value = all paths of the job / max-over-ranks wall time.
 
 Also reported:
   roofline   the dominant kernel's algorithmic bytes per launch (SURVEY.md §8d's 420 B per segment,
-             split per kernel) over its HIP-event-measured average launch, on a
-             one-lane context (the timed job overlaps three lanes); `traffic` from the committed
-             rocprofv3 PMC summary named in `traffic_source` (with its code revision);
+             split per kernel) over its average launch on a one-lane calibration context
+             (the timed job overlaps three lanes): the headline `frac` with the duration from the
+             committed rocprofv3 kernel trace of those launches (profiles/pmc_latest.json), this run's
+             HIP-event figure as `frac_hip_events`; `traffic` from the committed rocprofv3 PMC summary
+             named in `traffic_source` (with its code revision);
   pipeline   §8d's pipeline figure: segments/s x 420 B over the timed wall clock;
   quality    (N = 1, C3 at 1280x720) relative errors of the timed job's guided image against the
              65,536-spp unguided ground truth tests/golden/c3_gt.npz, next to the unguided path
@@ -368,16 +370,11 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
             e["avg_launch_ms_rocprof"] = round(cal / 1e6, 4)
             e["frac_rocprof"] = round(v[1] / v[2] / (cal / 1e9) / 1e9 / HBM_PEAK_GBS, 5)
         out[k] = e
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic, "traffic_source": source,
+    return {"bound": "hbm", **headline_frac(achieved, per_launch, ms / max(launches, 1), out[dom]),
+            "traffic": traffic, "traffic_source": source,
             "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
-            # the fraction with the kernel's duration from the committed rocprofv3 summary of the same
-            # launches (profiles/pmc_latest.json "calibration", revision in traffic_source) in place of
-            # this run's HIP events: the two agree when the profiled revision is this one
-            "frac_rocprof": out[dom].get("frac_rocprof"), "avg_launch_ms_rocprof": out[dom].get("avg_launch_ms_rocprof"),
             "kernel": dom, "dominant_by": "algorithmic bytes per pass (time shares under kernels)",
             "algorithmic_bytes_per_launch": int(per_launch),
-            "avg_launch_ms": round(ms / max(launches, 1), 4),
             "bytes_model": {"k_trace": f"{BYTES_TRACE_PER_RAY} B/camera ray",
                             shade_name: f"{BYTES_SHADE_PER_VERTEX} B/shaded vertex (+{BYTES_SHADE_RECORD} B when "
                                         "recording)",
@@ -386,6 +383,30 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
             "measured": f"1-lane context, guided {scene.width}x{scene.height} x {spp} spp with the trained tree, "
                         f"no records; the fused launches the timed job runs, HIP events on the lane's stream",
             "kernels": out}
+
+
+def headline_frac(achieved_hip, per_launch, avg_ms_hip, dom):
+    """The roofline's headline figures.  `achieved` / `frac` / `avg_launch_ms` take the dominant kernel's
+    average launch duration from the committed rocprofv3 kernel trace of the same calibration launches
+    (profiles/pmc_*_latest.json "calibration_avg_ns"), so they reproduce from profiles/ alone; this run's
+    HIP-event duration on the driver's box is reported beside them (`frac_hip_events`), with the ratio of
+    the two boxes' durations named when they differ by more than 2 %.  Without a committed summary the HIP
+    events are the headline."""
+    cal_ms = dom.get("avg_launch_ms_rocprof")
+    hip = {"frac_hip_events": round(achieved_hip / HBM_PEAK_GBS, 5), "avg_launch_ms_hip_events": round(avg_ms_hip, 4)}
+    if not cal_ms:
+        return {"achieved": round(achieved_hip, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved_hip / HBM_PEAK_GBS, 5), "frac_source": "HIP events, this run",
+                "avg_launch_ms": round(avg_ms_hip, 4), **hip}
+    achieved = per_launch / (cal_ms / 1e3) / 1e9
+    out = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+           "frac_source": "rocprofv3 kernel trace of the calibration launches (traffic_source file)",
+           "avg_launch_ms": round(cal_ms, 4), **hip}
+    ratio = avg_ms_hip / cal_ms
+    if abs(ratio - 1) > 0.02:
+        out["box_difference"] = (f"this run's HIP-event launch average is {ratio:.3f}x the profiled one: a different "
+                                 "box (clocks, memory, other tenants) or a kernel revision newer than the profile")
+    return out
 
 
 def volume_roofline(d, pg=None, scene=None, integ=None, local=0, a=None, spp=64):
@@ -472,12 +493,11 @@ def wavefront_roofline(pg, scene, integ, local, a, spp):
     dom = max(kernels, key=lambda k: kernels[k][1])
     ms, nbytes, launches, _ = kernels[dom]
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 5), "kernel": dom,
-            "frac_rocprof": out[dom].get("frac_rocprof"), "avg_launch_ms_rocprof": out[dom].get("avg_launch_ms_rocprof"),
+    return {"bound": "hbm", **headline_frac(achieved, nbytes / max(launches, 1), ms / max(launches, 1), out[dom]),
+            "kernel": dom,
             "traffic": out[dom].get("traffic_bytes_per_launch"), "traffic_source": source,
             "traffic_over_algorithmic": out[dom].get("traffic_over_algorithmic"),
-            "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)), "avg_launch_ms": round(ms / max(launches, 1), 4),
+            "algorithmic_bytes_per_launch": int(nbytes / max(launches, 1)),
             "bytes_model": {"k_vflight": f"{BYTES_VOL_FLIGHT} B state per flight + {BYTES_DENSITY_LOOKUP} B per density lookup",
                             "k_vvertex": f"{BYTES_VOL_VERTEX} B state per interaction + {BYTES_DENSITY_LOOKUP} B per density lookup",
                             "k_vnee": f"{BYTES_VOL_NEE} B per deferred walk slot + {BYTES_DENSITY_LOOKUP} B per density lookup"},

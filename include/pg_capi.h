@@ -363,6 +363,12 @@ pg_status pg_local_pixel_count(void *ctx, uint64_t *count);
 /* rays: n x 8 floats (o.xyz, tmin, d.xyz, tmax).  hits: n x 4 (t, prim as float bits, u, v);
  * prim = 0xFFFFFFFF for a miss.  any_hit: hits[i*4] = 1 if occluded else 0. */
 pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hit, float *hits);
+/* The closest hit's full record as the shading kernels build it (fillIntersectionRecord<true>,
+ * skdtree.h:343-430: barycentric position, face normal flipped to the shading normal's side, interpolated
+ * shading normal, shading frame by computeShadingFrame(n, dpdu = p1 - p0), wi = toLocal(-d)); the unit KAT of
+ * src/tests/test_dgeom.cpp:69-177.  rays: n x 8 as pg_trace_rays; out: n x 16 floats (p.xyz, t, geoN.xyz,
+ * shN.xyz, shFrame.s.xyz, wi.xyz), all zero for a miss. */
+pg_status pg_hit_records(void *ctx, const float *rays, uint64_t n, float *out);
 /* BSDF queries on the device for material `material` of the uploaded scene.
  * wi: n x 3 local; u: n x 3 (2D sample + component sample); out per query 12 floats:
  * wo.xyz, pdf, weight.rgb, sampled_type, eval(wi,wo_given).rgb, pdf(wi,wo_given).

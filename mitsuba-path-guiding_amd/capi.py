@@ -175,6 +175,7 @@ SIGNATURES = [
     ("pg_get_stats", C.c_int32, [VP, C.POINTER(pg_stats)]),
     ("pg_local_pixel_count", C.c_int32, [VP, C.POINTER(C.c_uint64)]),
     ("pg_trace_rays", C.c_int32, [VP, VP, C.c_uint64, C.c_int32, VP]),
+    ("pg_hit_records", C.c_int32, [VP, VP, C.c_uint64, VP]),
     ("pg_bsdf_query", C.c_int32, [VP, C.c_uint32, VP, VP, VP, C.c_uint64, VP]),
     ("pg_phase_query", C.c_int32, [VP, C.c_uint32, VP, VP, C.c_uint64, VP]),
     ("pg_medium_query", C.c_int32, [VP, C.c_uint32, C.c_int32, VP, VP, C.c_uint64, VP]),

@@ -1168,7 +1168,8 @@ bool volNeeStage() {
     const char *e = std::getenv("PG_VOL_NEE_STAGE");
     return e && *e ? std::atoi(e) != 0 : false;
 }
-// VolLane path state: VolWave's 13 float4 per slot; its queues (pg_volpath.hip)
+// VolLane path state: VolWave's 14 float4 per slot (7 path columns, 6 deferred-walk columns and their flags /
+// key / sample column; the first 7 when the walks run inline); its queues (pg_volpath.hip)
 constexpr int kVolStateF4 = 14, kVolStateF4Inline = 7, kVolQueues = 8;
 // k_vnee of iteration i on the lane's second stream, concurrent with iteration i + 1's k_vflight (which reads
 // no state the walks write); k_vvertex of i + 1 waits for it.  PG_VOL_NEE_OVERLAP=0: on the lane's stream
@@ -1288,7 +1289,7 @@ pg_status volWavefrontPass(Ctx *c, const GParams &g, const SceneDev &sc, const V
             w.h0 = st + 10 * cap;
             w.h1 = st + 11 * cap;
             w.h2 = st + 12 * cap;
-            w.nflags = reinterpret_cast<uint32_t *>(st + 13 * cap);
+            w.nflags = reinterpret_cast<uint4 *>(st + 13 * cap);
         }
         // queues 0/1: flight of even / odd iterations, 2/3: surface, 4: medium vertices, 5/6: delta surface,
         // 7: deferred transmittance walks (k_vnee)
@@ -2452,9 +2453,28 @@ pg_status pg_trace_rays(void *ctx, const float *rays, uint64_t n, int32_t any_hi
     HIPC(c, h.alloc(n * 16));
     HIPC(c, ovf.alloc(pg_stack_overflow_words(pg_trace_rays_threads(n)) * 4));
     HIPC(c, hipMemcpyAsync(r.p, rays, n * 32, hipMemcpyHostToDevice, c->stream));
-    pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, any_hit, h.as<float>(), ovf.as<uint32_t>());
+    pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, any_hit ? 1 : 0, h.as<float>(),
+                         ovf.as<uint32_t>());
     HIPC(c, hipGetLastError());
     HIPC(c, hipMemcpyAsync(hits, h.p, n * 16, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    return PG_OK;
+}
+
+pg_status pg_hit_records(void *ctx, const float *rays, uint64_t n, float *out) {
+    Ctx *c = (Ctx *)ctx;
+    if (!c || (!rays && n) || (!out && n)) return fail(c, PG_ERR_INVALID, "pg_hit_records: null argument");
+    if (!c->has_scene) return fail(c, PG_ERR_STATE, "pg_hit_records: no scene");
+    HIPC(c, hipSetDevice(c->cfg.device));
+    if (!n) return PG_OK;
+    DevBuf r, h, ovf;
+    HIPC(c, r.alloc(n * 32));
+    HIPC(c, h.alloc(n * 64));
+    HIPC(c, ovf.alloc(pg_stack_overflow_words(pg_trace_rays_threads(n)) * 4));
+    HIPC(c, hipMemcpyAsync(r.p, rays, n * 32, hipMemcpyHostToDevice, c->stream));
+    pg_launch_trace_rays(c->stream, sceneView(c), r.as<float>(), (uint32_t)n, 2, h.as<float>(), ovf.as<uint32_t>());
+    HIPC(c, hipGetLastError());
+    HIPC(c, hipMemcpyAsync(out, h.p, n * 64, hipMemcpyDeviceToHost, c->stream));
     HIPC(c, hipStreamSynchronize(c->stream));
     return PG_OK;
 }

@@ -89,7 +89,10 @@ struct VolWave {
     // NEE (shadow walk origin, dim), (emitter point, max crossings), (contribution, flags); emitter hit
     // (walk origin, mint), (direction, dim), (contribution, medium | crossings)
     float4 *n0, *n1, *n2, *h0, *h1, *h2;
-    uint32_t *nflags;  // which of them are valid, whether the path ended, its vertex (pg_volpath.hip deferFlags)
+    // (flags: which of them are valid, whether the path ended, its vertex (pg_volpath.hip deferFlags); the
+    // path's rng key; its sample; 0): the walks' streams come from here, so k_vnee shares no memory with the
+    // next iteration's k_vflight, which rewrites r[slot] on the other stream (PG_VOL_NEE_OVERLAP)
+    uint4 *nflags;
 };
 
 // Sharded work queue of path slots: shard s holds items[s * stride, s * stride + counts[s]).

@@ -1150,13 +1150,26 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const f
     uint32_t tri = 0xFFFFFFFFu;
     float u = 0, v = 0;
     float *h = hits + 4 * (size_t)i;
-    if (any) {
+    if (any == 1) {
         bool occ = occluded(sc, o, d, r[3], tmax, wstk);
         h[0] = occ ? 1.0f : 0.0f;
         h[1] = h[2] = h[3] = 0.0f;
         return;
     }
     bool hit = traverse<false>(sc.nodes, sc.tris, o, d, r[3], tmax, tri, u, v, stk);
+    if (any == 2) {  // pg_hit_records: the hit record the shading kernels build (fetchHit), 16 floats per ray
+        float *q = hits + 16 * (size_t)i;
+        if (!hit) {
+            for (int k = 0; k < 16; ++k) q[k] = 0.0f;
+            return;
+        }
+        Hit hr;
+        fetchHit(sc, tri, u, v, d, hr);
+        const float rec[16] = {hr.p.x,    hr.p.y,    hr.p.z,    tmax,       hr.geoN.x, hr.geoN.y, hr.geoN.z, hr.shN.x,
+                               hr.shN.y,  hr.shN.z,  hr.sh.s.x, hr.sh.s.y,  hr.sh.s.z, hr.wi.x,   hr.wi.y,   hr.wi.z};
+        for (int k = 0; k < 16; ++k) q[k] = rec[k];
+        return;
+    }
     uint32_t orig = hit ? __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w) : 0xFFFFFFFFu;
     h[0] = hit ? tmax : 0.0f;
     h[1] = __uint_as_float(orig);

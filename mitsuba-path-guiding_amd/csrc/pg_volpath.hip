@@ -56,12 +56,15 @@ struct VRng {
 };
 
 // Transmittance sub-streams (oracle/orc_volpath.h subStream): the NEE shadow walk (kind 0) and the
-// re-walk of a sampled ray that found a lit emitter through media (kind 1) draw from the counter stream
-// at dimensions 0x80000000 | dim << 16 | kind << 15 | j, dim = the main-stream dimension at which the
-// interaction drew its light sample / started its emitter walk.  The main stream then does not depend
-// on the walks, so the wavefront runs them as a stage of their own (k_vnee).
+// re-walk of a sampled ray that found a lit emitter through media (kind 1) draw from a Philox stream keyed
+// by key ^ 0x9E3779B9 (2 dim + kind + 1), dim = the main-stream dimension at which the interaction drew its
+// light sample / started its emitter walk, at dimensions 0x80000000 + j (the main stream's stay below
+// 2^31).  The key map is a bijection of (dim, kind) for dim < 2^31, so no two walks of a path share
+// numbers however long the path or the walk (round 6; until then dim and kind were bit-packed into the
+// dimension and aliased from dim = 2^15 or j = 2^15 on).  The main stream does not depend on the walks, so
+// the wavefront runs them as a stage of their own (k_vnee).
 __device__ __forceinline__ VRng subStream(uint32_t key, uint32_t sample, uint32_t dim, uint32_t kind) {
-    return VRng{key, sample, 0x80000000u | (dim << 16) | (kind << 15), 0};
+    return VRng{key ^ (0x9E3779B9u * (2u * dim + kind + 1u)), sample, 0x80000000u, 0};
 }
 
 // What an interaction leaves for its transmittance walks (k_vnee in the wavefront, resolveDeferred
@@ -1069,8 +1072,12 @@ __device__ __forceinline__ void storePath(const VolWave &w, uint32_t slot, const
 __device__ __forceinline__ uint32_t deferFlags(const VDefer &df, bool ended) {
     return (df.nee ? 1u : 0u) | (df.hit ? 2u : 0u) | (ended ? 4u : 0u) | ((uint32_t)(df.k + 1) << 8);
 }
-__device__ __forceinline__ void loadDefer(const VolWave &w, uint32_t slot, VDefer &df, bool &ended) {
-    const uint32_t flags = w.nflags[slot];
+__device__ __forceinline__ void loadDefer(const VolWave &w, uint32_t slot, VDefer &df, bool &ended, uint32_t &key,
+                                          uint32_t &sample) {
+    const uint4 rec = w.nflags[slot];
+    const uint32_t flags = rec.x;
+    key = rec.y;
+    sample = rec.z;
     df.nee = flags & 1u;
     df.hit = (flags >> 1) & 1u;
     ended = (flags >> 2) & 1u;
@@ -1351,7 +1358,7 @@ __global__ __launch_bounds__(TRACE_BLOCK, (VVertexWaves<NEE_STAGE, KIND>::value)
             }
             if (df.hit || df.nee) {
                 if (NEE_STAGE) {  // the record is in the slot's VolWave entries; k_vnee walks it after this launch
-                    w.nflags[slot] = deferFlags(df, ended);
+                    w.nflags[slot] = make_uint4(deferFlags(df, ended), key0, sample0, 0u);
                     toN = true;
                 } else {  // inline: the walks, then their adds into the stored radiance (the same order and sums)
                     float Th, Tn;
@@ -1392,12 +1399,12 @@ __global__ __launch_bounds__(TRACE_BLOCK, PG_VNEE_WAVES) void k_vnee(GParams g, 
         const uint32_t slot = qn.items[(size_t)sh * qn.stride + i];
         bool ended;
         VDefer df;
-        loadDefer(w, slot, df, ended);
-        const uint4 r = w.r[slot];  // key and sample (constant over the path's life)
+        uint32_t key, sample;
+        loadDefer(w, slot, df, ended, key, sample);
         float4 *dst = ended ? v.rad + slot : w.L + slot;
         const float4 l4 = *dst;
         f3 L = xyz(l4);
-        resolveDeferred(sc, v, df, r.x, r.y, slot, L, stk, segs, lookups);
+        resolveDeferred(sc, v, df, key, sample, slot, L, stk, segs, lookups);
         *dst = f4(L, l4.w);
         walks++;
     }

@@ -253,6 +253,13 @@ class Device:
         self._chk(self.lib.pg_trace_rays(self.h, _p(rays), len(rays), int(any_hit), _p(hits)))
         return hits
 
+    def hit_records(self, rays):
+        """pg_hit_records: n x 16 (p, t, geoN, shN, shading frame s, wi local) of each ray's closest hit."""
+        rays = np.ascontiguousarray(rays, np.float32)
+        out = np.zeros((len(rays), 16), np.float32)
+        self._chk(self.lib.pg_hit_records(self.h, _p(rays), len(rays), _p(out)))
+        return out
+
     def bsdf_query(self, material, wi, u, wo_given=None):
         wi = np.ascontiguousarray(wi, np.float32)
         u = np.ascontiguousarray(u, np.float32)

@@ -102,7 +102,7 @@ public:
         m_denoiserFile = s->readString();
         m_denoise = s->readBool();
     }
-    void serialize(Stream *s, InstanceManager *m) const {
+    void serialize(Stream *s, InstanceManager *m) const override {
         ProgressiveMonteCarloIntegrator::serialize(s, m);
         s->write(&m_cfg, sizeof(m_cfg));
         s->writeInt(m_trainingIterations);
@@ -116,7 +116,7 @@ public:
     }
 
     bool preprocess(const Scene *scene, RenderQueue *queue, const RenderJob *job,
-                    int sceneResID, int sensorResID, int samplerResID) {
+                    int sceneResID, int sensorResID, int samplerResID) override {
         ProgressiveMonteCarloIntegrator::preprocess(scene, queue, job, sceneResID, sensorResID, samplerResID);
         check(pg_create(&m_cfg, &m_ctx));
         m_flat = flatten(scene);  // TriMesh arrays, BSDFs, emitters (area + environment), media, camera
@@ -136,7 +136,7 @@ public:
     }
 
     bool render(Scene *scene, RenderQueue *queue, const RenderJob *job,
-                int sceneResID, int sensorResID, int samplerResID) {
+                int sceneResID, int sensorResID, int samplerResID) override {
         ref<Timer> timer = new Timer();
         uint32_t offset = 0;
         const size_t npix = (size_t) m_flat.desc.camera.width * m_flat.desc.camera.height;
@@ -268,9 +268,9 @@ public:
         return true;
     }
 
-    void cancel() { if (m_ctx) pg_cancel(m_ctx); ProgressiveMonteCarloIntegrator::cancel(); }
+    void cancel() override { if (m_ctx) pg_cancel(m_ctx); ProgressiveMonteCarloIntegrator::cancel(); }
 
-    void postprocess(const Scene *, RenderQueue *, const RenderJob *, int, int, int) {
+    void postprocess(const Scene *, RenderQueue *, const RenderJob *, int, int, int) override {
         pg_stats st;
         if (m_ctx && pg_get_stats(m_ctx, &st) == PG_OK)
             Log(EInfo, "GPU: %llu paths, %.2f segments/path", (unsigned long long) st.paths,
@@ -280,7 +280,7 @@ public:
     }
 
     // renderBlock() and E() callers get Mitsuba's own (unguided) CPU integrator, same parameters
-    Spectrum Li(const RayDifferential &r, RadianceQueryRecord &rRec) const { return m_cpu->Li(r, rRec); }
+    Spectrum Li(const RayDifferential &r, RadianceQueryRecord &rRec) const override { return m_cpu->Li(r, rRec); }
 
 protected:
     // every pg_status is checked: Log(EError, ...) throws (formatter.h:33) and ends the job

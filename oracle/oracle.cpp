@@ -587,6 +587,24 @@ void oracle_intersect(void *sp, const float *rays, uint64_t n, float *out) {
     }
 }
 
+// The closest hit's record (Scene::fill, fillIntersectionRecord<true> skdtree.h:343-430), the layout of the
+// library's pg_hit_records: p.xyz, t, geoN.xyz, shN.xyz, shading frame s.xyz, wi.xyz; zeros for a miss
+void oracle_hit_records(void *sp, const float *rays, uint64_t n, float *out) {
+    const Scene &S = *(const Scene *)sp;
+    for (uint64_t i = 0; i < n; ++i) {
+        const float *r = rays + 8 * i;
+        Ray ray{V3(r[0], r[1], r[2]), V3(r[4], r[5], r[6]), r[3], r[7]};
+        float *o = out + 16 * i;
+        std::memset(o, 0, 16 * sizeof(float));
+        Its its;
+        if (!S.intersect(ray, its)) continue;
+        const float vals[16] = {its.p.x,    its.p.y,    its.p.z,    its.t,      its.geoN.x, its.geoN.y,
+                                its.geoN.z, its.sh.n.x, its.sh.n.y, its.sh.n.z, its.sh.s.x, its.sh.s.y,
+                                its.sh.s.z, its.wi.x,   its.wi.y,   its.wi.z};
+        std::memcpy(o, vals, sizeof vals);
+    }
+}
+
 // Per query: out[12] = wo.xyz, pdf, weight.rgb, sampledType, eval(wi, wo_given).rgb, pdf(wi, wo_given)
 // roughplastic slices (orc_rtrans.h): table[100], fdr_int
 void oracle_rough_transmittance(uint32_t dist, float alpha, float eta, float *table, float *fdr) {

@@ -53,6 +53,7 @@ def lib(capi):
             "oracle_material_type": (C.c_uint32, [C.POINTER(capi.pg_material)]),
             "oracle_rough_transmittance": (None, [C.c_uint32, C.c_float, C.c_float, VP, VP]),
             "oracle_intersect": (None, [VP, VP, C.c_uint64, VP]),
+            "oracle_hit_records": (None, [VP, VP, C.c_uint64, VP]),
             "oracle_set_volpath_eager": (None, [C.c_int32]),
             "oracle_medium_query": (None, [VP, C.c_int32, C.c_int32, VP, VP, C.c_uint64, VP]),
             "oracle_hg_query": (None, [C.c_float, VP, VP, C.c_uint64, VP]),
@@ -94,6 +95,13 @@ class OracleScene:
         rays = np.ascontiguousarray(rays, np.float32)
         out = np.zeros((len(rays), 16), np.float32)
         self.L.oracle_intersect(self.h, _p(rays), len(rays), _p(out))
+        return out
+
+    def hit_records(self, rays):
+        """n x 16 (p, t, geoN, shN, shading frame s, wi local): the layout of the library's pg_hit_records."""
+        rays = np.ascontiguousarray(rays, np.float32)
+        out = np.zeros((len(rays), 16), np.float32)
+        self.L.oracle_hit_records(self.h, _p(rays), len(rays), _p(out))
         return out
 
     def medium_lookup(self, m, pts):

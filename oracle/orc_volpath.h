@@ -30,10 +30,12 @@ inline float miWeightV(float a, float b) {
 // Transmittance sub-streams (round 5).  Every transmittance estimate an interaction
 // makes -- the NEE shadow walk (Scene::evalTransmittance) and the re-walk of a phase/BSDF-sampled ray that
 // found a lit emitter through media (rayIntersectAndLookForEmitter) -- draws from a counter sub-stream of
-// its own instead of the path's sequential stream: dimensions 0x80000000 | dim << 16 | kind << 15 | j,
-// where dim is the main-stream dimension at which the interaction drew its light sample (kind 0, NEE) or
-// started its emitter walk (kind 1), and j counts the walk's draws (j < 2^15; dim < 2^15 -- a path with
-// more main-stream draws than that reuses sub-stream dimensions 2^15 apart).  The main stream then does
+// its own instead of the path's sequential stream: the Philox key key ^ 0x9E3779B9 (2 dim + kind + 1) at
+// dimensions 0x80000000 + j, where dim is the main-stream dimension at which the interaction drew its light
+// sample (kind 0, NEE) or started its emitter walk (kind 1), and j counts the walk's draws.  Odd-constant
+// multiplication is a bijection mod 2^32, so two walks of one path never share a stream (round 6: until
+// then dim and kind were bit-packed into the dimension, which aliased from dim = 2^15 or j = 2^15 on), and
+// main-stream dimensions stay below 2^31, so no walk draws a main-stream number.  The main stream then does
 // not depend on how many numbers a walk used, so the GPU runs the walks as a stage of its own after the
 // interactions (pg_volpath.hip k_vnee).  Per interaction the contributions enter L in a fixed order: the
 // emitter hit (its product T Le w, then times the walk's transmittance), then the NEE (its product
@@ -42,7 +44,8 @@ inline float miWeightV(float a, float b) {
 inline SeqRng subStream(const SeqRng &rng, uint32_t dim, uint32_t kind) {
     SeqRng s;
     s.r = rng.r;
-    s.dim = 0x80000000u | (dim << 16) | (kind << 15);
+    s.r.key = rng.r.key ^ (0x9E3779B9u * (2u * dim + kind + 1u));
+    s.dim = 0x80000000u;
     return s;
 }
 // a pending NEE of one interaction: its contribution before the shadow walk's transmittance

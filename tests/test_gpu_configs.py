@@ -171,8 +171,11 @@ def test_c5_guided_volpath_256_grid(pg, O):
     z, _ = pixel_parity(g, c[:2], np.arange(64 * 64))
     assert (np.abs(z) < 5).mean() > 0.999
     close = np.abs(mg - mc).max(-1) <= 1e-3 * np.maximum(mc.max(-1), 1e-3)
-    assert close.mean() > 0.5, close.mean()
-    assert abs(nrec_gpu - nrec_cpu) <= 0.01 * nrec_cpu, (nrec_gpu, nrec_cpu)
+    print(f"c5 guided 256^3 same tree: |z|<5 {(np.abs(z) < 5).mean():.5f}, pixels within 1e-3 {close.mean():.5f}, "
+          f"records {nrec_gpu} / {nrec_cpu}")
+    # same tree and streams on both sides: measured 1.00000 (and equal record counts, gpurun_out/r06b)
+    assert close.mean() >= 0.999, close.mean()
+    assert abs(nrec_gpu - nrec_cpu) <= 0.001 * nrec_cpu, (nrec_gpu, nrec_cpu)
 
 
 @pytest.mark.parametrize("paths", [1024, 4096])

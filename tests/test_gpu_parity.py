@@ -133,30 +133,42 @@ def test_trace_matches_bruteforce(pg, O, tmp_path_factory, name):
 
 
 def test_dgeom_kat_gpu(pg, O):
-    """src/tests/test_dgeom.cpp:36-121 through the GPU traversal (t, barycentrics)."""
+    """src/tests/test_dgeom.cpp:35-177 through the GPU traversal and the shading kernels' hit record
+    (pg_hit_records: fetchHit's position, geometric and shading normals, shading frame and local wi), and
+    that record equal to the oracle's bit for bit."""
     import json, os
+    from test_oracle_kat import check_dgeom_case, dgeom_scene
     kat = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "dgeom_kat.json")))
     for case in kat["cases"]:
-        s = pg.scenes.Scene()
-        m = s.add_material(pg.scenes.material("diffuse"))
-        N = None if case["normals"] is None else np.array(case["normals"], np.float32)
-        if N is not None:
-            N /= np.linalg.norm(N, axis=1, keepdims=True)
-        V = np.array(case["vertices"], np.float32)
-        F = np.array([[0, 1, 2]], np.uint32)
-        if N is None:
-            N = np.tile(np.array([[0, 0, 1]], np.float32), (3, 1))
-        s.add_mesh(V, F, N, material=m)
-        s.set_camera((0.2, 0.2, -2), (0.2, 0.2, 0), (0, 1, 0), 40, 8, 8)
-        s.finalize()
+        s = dgeom_scene(pg, case)
         dev = make_dev(pg, s)
         r = np.array([[*case["ray_o"], 1e-4, *case["ray_d"], np.inf]], np.float32)
         h = dev.trace_rays(r)[0]
-        p = np.array(case["ray_o"]) + h[0] * np.array(case["ray_d"])
-        assert np.allclose(p, case["p"], atol=1e-5)
-        bary = case.get("bary", [1 - sum(case.get("uv", [0, 0])), *case.get("uv", [0, 0])])
-        assert np.allclose([h[2], h[3]], bary[1:], atol=1e-5)
+        rec = dev.hit_records(r)[0]
         dev.close()
+        assert h[1].view(np.uint32) == 0
+        check_dgeom_case(case, rec, h[2:4])
+        orec = O.OracleScene(pg.capi, s).hit_records(r)[0]
+        np.testing.assert_array_equal(rec, orec)
+
+
+def test_hit_records_match_oracle(pg, O, scenes):
+    """The hit record of random rays (smooth-shaded spheres of the ajar door included): every field the
+    shading kernels use, GPU against the oracle."""
+    sc = scenes["ajar"]
+    rays = random_rays(sc, 100_000, 9)
+    dev = make_dev(pg, sc)
+    g = dev.hit_records(rays)
+    dev.close()
+    c = O.OracleScene(pg.capi, sc).hit_records(rays)
+    hit = (c[:, 3] > 0) & (g[:, 3] > 0)
+    assert hit.mean() > 0.5
+    same_t = hit & (g[:, 3] == c[:, 3])
+    assert same_t.sum() / hit.sum() > 0.999
+    bit = np.all(g[same_t] == c[same_t], axis=1)
+    print(f"hit records: {same_t.sum()} rays with equal t, bit-equal records {bit.mean():.6f}, max |diff| "
+          f"{np.abs(g[same_t] - c[same_t]).max():.3g}")
+    assert np.quantile(np.abs(g[same_t] - c[same_t]).max(1), 0.999) < 1e-5
 
 
 def _probe_scene(pg):

@@ -273,10 +273,13 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
     megakernel's bit for bit -- whether every iteration runs as launches (tail threshold 0), the
     default tail threshold, or the tail kernel takes the whole chunk after the camera rays; with one,
     two or three (default) lanes of chunks in flight (films in chunk order), with the flight queues
-    sorted by cell (PG_VOL_SORT), and whether the interactions' transmittance walks run as their own stage
-    (k_vnee, default) or inline (PG_VOL_NEE_STAGE=0), and the medium and surface interactions as two
-    launches (default) or one (PG_VOL_SPLIT_VERTEX=0): the walks draw from their own sub-streams and add to
-    L in a fixed order (oracle/orc_volpath.h subStream)."""
+    sorted by cell (PG_VOL_SORT), and whether the interactions' transmittance walks run inline at the end of
+    each interaction (the default, pg_host.cpp volNeeStage) or as a stage of their own (PG_VOL_NEE_STAGE=1:
+    k_vvertex<NEE_STAGE> writes the deferred-walk records, k_vnee walks them, either on a second stream
+    overlapping the next iteration's free flights (PG_VOL_NEE_OVERLAP, default with the stage) or on the
+    lane's stream (PG_VOL_NEE_OVERLAP=0)), and the medium and surface interactions as two launches (default)
+    or one (PG_VOL_SPLIT_VERTEX=0): the walks draw from their own sub-streams and add to L in a fixed order
+    (oracle/orc_volpath.h subStream)."""
     from mitsuba_path_guiding_amd.integrator import GuidedVolumetricPathTracer, ProgressiveVolumetricPathTracer
     sc = pg.scenes.smoke(96, 96, res=48)
     props = {"trainingIterations": 3, "samplesPerProgression": 8}
@@ -289,13 +292,17 @@ def test_volpath_wavefront_equals_megakernel(pg, monkeypatch, case):
     if case == "guided_exact_chunked":
         props.update({"exactMis": True, "maxPathsInFlight": 4096 + 512})
     out = []
-    runs = (("0", None, None, None, None, None), ("1", "0", None, None, None, None), ("1", None, None, None, None, None),
-            ("1", str(1 << 30), None, None, None, None), ("1", None, "1", None, None, None), ("1", "0", "3", "1", None, None),
-            ("1", "0", None, None, "0", None), ("1", "0", "2", None, None, "0"))
-    for wf, tail, lanes, sort, nee, split in runs:
+    # (wavefront, tail threshold, lanes, flight sort, NEE stage, split vertex launches, NEE stage overlap)
+    runs = (("0", None, None, None, None, None, None), ("1", "0", None, None, None, None, None),
+            ("1", None, None, None, None, None, None), ("1", str(1 << 30), None, None, None, None, None),
+            ("1", None, "1", None, None, None, None), ("1", "0", "3", "1", None, None, None),
+            ("1", "0", "2", None, None, "0", None),
+            ("1", "0", None, None, "1", None, "1"), ("1", None, None, None, "1", None, "0"),
+            ("1", "0", "2", None, "1", "0", "0"))
+    for wf, tail, lanes, sort, nee, split, overlap in runs:
         monkeypatch.setenv("PG_VOL_WAVEFRONT", wf)
         for var, val in (("PG_VOL_TAIL_PATHS", tail), ("PG_VOL_LANES", lanes), ("PG_VOL_SORT", sort),
-                         ("PG_VOL_NEE_STAGE", nee), ("PG_VOL_SPLIT_VERTEX", split)):
+                         ("PG_VOL_NEE_STAGE", nee), ("PG_VOL_SPLIT_VERTEX", split), ("PG_VOL_NEE_OVERLAP", overlap)):
             if val is None:
                 monkeypatch.delenv(var, raising=False)
             else:

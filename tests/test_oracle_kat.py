@@ -23,32 +23,57 @@ def _single_triangle_scene(pg, V, N):
     return s.finalize()
 
 
+def dgeom_scene(pg, case):
+    V = np.array(case["vertices"], np.float32)
+    if case["normals"] is None:
+        N = np.tile(np.array([[0, 0, 1]], np.float32), (3, 1))  # TriMesh face normal
+    else:
+        N = np.array(case["normals"], np.float32)
+    return _single_triangle_scene(pg, V, N)
+
+
+def check_dgeom_case(case, rec, bary):
+    """One KAT case against a hit record (n x 16 layout of pg_hit_records / oracle_hit_records: p, t, geoN,
+    shN, shading frame s, wi) and the hit's barycentrics (b1, b2)."""
+    eps = case["eps"]
+    p, geoN, shN, shS, wi = rec[0:3], rec[4:7], rec[7:10], rec[10:13], rec[13:16]
+    assert np.allclose(p, case["p"], atol=eps), (case["name"], p)
+    assert np.allclose(geoN, case["geoN"], atol=eps), (case["name"], geoN)
+    b = np.array([1 - bary[0] - bary[1], bary[0], bary[1]], np.float64)
+    if "bary" in case:
+        assert np.allclose(b, case["bary"], atol=eps), (case["name"], b)
+    # its.uv: interpolated texcoords, or (b1, b2) without them (skdtree.h:398-405)
+    T = case["texcoords"]
+    uv = b[1:] if T is None else (np.array(T, np.float64) * b[:, None]).sum(0)
+    assert np.allclose(uv, case["uv"], atol=eps), (case["name"], uv)
+    if "shN_weights" in case:  # normalize(n0*.7 + n1*.1 + n2*.2)
+        n = (np.array(case["normals"], np.float64) * np.array(case["shN_weights"])[:, None]).sum(0)
+        n /= np.linalg.norm(n)
+    else:
+        n = np.array(case["shN"], np.float64)
+    assert np.allclose(shN, n, atol=eps), (case["name"], shN, n)
+    # shading tangent: computeShadingFrame(n, dpdu) = normalize(dpdu - n dot(n, dpdu)) (:106-107,160-161)
+    if "dpdu" in case:
+        dpdu = np.array(case["dpdu"], np.float64)
+        s = dpdu - n * n.dot(dpdu)
+        s /= np.linalg.norm(s)
+        assert np.allclose(shS, s, atol=eps), (case["name"], shS, s)
+        t = np.cross(n, s)
+        d = -np.array(case["ray_d"], np.float64)
+        assert np.allclose(wi, [d.dot(s), d.dot(t), d.dot(n)], atol=eps), (case["name"], wi)
+
+
 def test_dgeom_kat(pg, O):
     kat = json.load(open(os.path.join(GOLDEN, "dgeom_kat.json")))
+    assert [c["kat"] for c in kat["cases"]] == ["test_dgeom.cpp:35-67", "test_dgeom.cpp:69-120",
+                                                "test_dgeom.cpp:122-177"]
     for case in kat["cases"]:
-        V = np.array(case["vertices"], np.float32)
-        if case["normals"] is None:
-            N = np.tile(np.array([[0, 0, 1]], np.float32), (3, 1))  # TriMesh face normal
-        else:
-            N = np.array(case["normals"], np.float32)
-        sc = _single_triangle_scene(pg, V, N)
-        osc = O.OracleScene(pg.capi, sc)
+        osc = O.OracleScene(pg.capi, dgeom_scene(pg, case))
         r = np.array([[*case["ray_o"], 1e-4, *case["ray_d"], np.inf]], np.float32)
         h = osc.intersect(r)[0]
-        eps = case["eps"]
         assert h[15].view(np.uint32) == 0
-        assert np.allclose(h[0:3], case["p"], atol=eps)
-        assert np.allclose(h[4:7], case["geoN"], atol=eps)
-        assert np.allclose(h[10:13], case["dpdu"], atol=eps)
-        if case["normals"] is None:
-            assert np.allclose(h[7:10], case["shN"], atol=eps)
-            assert np.allclose(h[13:15], case["uv"], atol=eps)
-        else:
-            b = np.array(case["bary"], np.float32)
-            n = (np.array(case["normals"], np.float32) * b[:, None]).sum(0)
-            n /= np.linalg.norm(n)
-            assert np.allclose(h[7:10], n, atol=eps)  # normalize(n0*.7 + n1*.1 + n2*.2)
-            assert np.allclose(h[13:15], b[1:], atol=eps)
+        assert np.allclose(h[10:13], case.get("dpdu", [1, 0, 0]), atol=case["eps"])  # side1 = p1 - p0
+        check_dgeom_case(case, osc.hit_records(r)[0], h[13:15])
 
 
 def _brute_force(V, F, o, d):
