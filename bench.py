@@ -111,13 +111,44 @@ def launch_ranks(n, argv):
     return subprocess.call(cmd, env=env)
 
 
+def deadline_seconds():
+    """PG_BENCH_DEADLINE: seconds a multi-rank start-up stage may take before the rank exits naming the stuck
+    rank (distributed.Watchdog); the first job (kernel loading, the first pg_comm collectives) gets 3x."""
+    return float(os.environ.get("PG_BENCH_DEADLINE", "300"))
+
+
+def first_collective(wd, world, on_dev):
+    """One small all-reduce of the rank ids, timed and reported per rank (the first traffic of the group)."""
+    import torch
+    import torch.distributed as dist
+    stall = os.environ.get("PG_BENCH_STALL_RANK")  # test hook: this rank stalls before its first collective
+    if stall is not None and int(stall) == dist.get_rank():
+        wd.stage("stall (test hook)")
+        time.sleep(3600)
+    wd.stage("first collective", collective=True)
+    t0 = time.perf_counter()
+    tdev = torch.device("cuda", torch.cuda.current_device()) if on_dev else torch.device("cpu")
+    t = torch.tensor([float(dist.get_rank())], dtype=torch.float64, device=tdev)
+    dist.all_reduce(t)
+    total = float(t.item())
+    wd._say(f"first collective complete in {time.perf_counter() - t0:.3f} s (rank sum {total:.0f}, "
+            f"expected {world * (world - 1) / 2:.0f})")
+    assert total == world * (world - 1) / 2, total
+    return total
+
+
 def plumbing_check(a, rank, world):
     """--plumbing-check: the launcher's rank / world wiring without a GPU (gloo process group)."""
     from mitsuba_path_guiding_amd import distributed as D
     import torch
     import torch.distributed as dist
+    wd = D.Watchdog(rank, world, device="cpu", seconds=deadline_seconds())
+    wd.stage("process group init", collective=True)
     D.init("gloo")
+    wd.attach_store()
     assert dist.get_world_size() == world == a.gpus, (dist.get_world_size(), world, a.gpus)
+    first_collective(wd, world, False)
+    wd.done()
     got = [None] * world
     dist.all_gather_object(got, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", -1)),
                                  "world": dist.get_world_size(), "pid": os.getpid()})
@@ -164,12 +195,21 @@ def main():
     if world > 1 and backend == "nccl" and torch.cuda.device_count() < world:
         sys.exit(f"bench.py: {world} ranks need {world} visible GPUs, found {torch.cuda.device_count()} "
                  "(PG_DIST_BACKEND=gloo rehearses ranks that share a GPU)")
+    device = local % max(1, torch.cuda.device_count())
+    # per-rank start-up report and deadlines (stderr; rank 0's stdout keeps the one JSON line)
+    wd = D.Watchdog(rank, world, device=device, seconds=deadline_seconds()) if world > 1 else None
     if world > 1:
+        wd.stage(f"process group init ({backend})", collective=True)
         D.init(backend)
+        wd.attach_store()
         assert torch.distributed.get_world_size() == world == a.gpus
 
     on_dev = torch.cuda.is_available() and backend == "nccl"
-    device = local % max(1, torch.cuda.device_count())
+    if world > 1:
+        wd._say(f"world {world}, local rank {local}, device {device}"
+                + (f" ({torch.cuda.get_device_name(device)})" if torch.cuda.is_available() else ""))
+        first_collective(wd, world, on_dev)
+        wd.stage("scene flatten + upload (pg_create, pg_upload_scene)")
     scene = pg.scenes.SCENES[a.scene](a.width, a.height)
     # postprogression exchange (N > 1): by default the library's own RCCL communicator (pg_comm_*, what
     # the C++ adapter runs): all-reduce of the SD-tree building statistics.  RCCL
@@ -193,6 +233,7 @@ def main():
     integ.preprocess(scene)
     dev = integ.dev
     if capi_comm:
+        wd.stage("pg_comm_init (the library's RCCL communicator)", collective=True)
         D.init_capi_comm(dev)
 
     def barrier():
@@ -211,9 +252,15 @@ def main():
             rgbw, sq = D.reduce_film(rgbw, sq, on_dev)
         return rgbw
 
-    for _ in range(a.warmup):
+    for w in range(a.warmup):
+        if wd is not None and w == 0:  # kernel loading and the first pg_comm collectives
+            wd.stage("first job (warm-up)", seconds=3 * deadline_seconds())
         job()
+    if wd is not None:
+        wd.stage("barrier before the timed region", collective=True)
     barrier()
+    if wd is not None:
+        wd.done()
     s0 = dev.stats()
     t0 = time.perf_counter()
     for _ in range(a.steps):

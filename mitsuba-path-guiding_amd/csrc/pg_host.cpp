@@ -215,6 +215,7 @@ struct Ctx {
     // shard
     std::vector<uint32_t> local_pixels;
     DevBuf d_local_pixels;
+    DevBuf d_band_pixels;  // the surface path's order of the same pixels (cameraBands)
     // path state
     Lane lanes[PG_MAX_LANES];
     int nlanes = PG_DEFAULT_LANES;
@@ -815,6 +816,15 @@ pg_status pg_cancel(void *ctx) {
     return PG_OK;
 }
 
+// the camera's XCD-banded shard map (pg_kernels.h pg_banded_shard_count) over PG_CAMERA_BANDS bands of the local
+// pixels (0: the interleaved map): band g goes to XCD group g % 8, so with more than 8 bands each XCD takes
+// every 8th band (the surface path's pixel order d_band_pixels groups them).  Paths are pure functions of
+// (pixel, sample), so films and trees do not depend on it
+uint32_t cameraBands() {
+    const char *e = std::getenv("PG_CAMERA_BANDS");
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : 0u;
+}
+
 pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     Ctx *c = (Ctx *)ctx;
     if (!c || !d) return fail(c, PG_ERR_INVALID, "pg_upload_scene: null argument");
@@ -1081,6 +1091,20 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
                     for (uint32_t x = bx; x < std::min(bx + B, x1); ++x) c->local_pixels.push_back(y * cam.width + x);
     }
     if ((s = upload(c, c->d_local_pixels, c->local_pixels))) return s;
+    {  // the surface path's pixel order: bands {r, r + 8, r + 16, ...} of the local pixels as the r-th eighth
+        const uint32_t nb = cameraBands(), np = (uint32_t)c->local_pixels.size();
+        std::vector<uint32_t> bp;
+        bp.reserve(np);
+        if (nb > 8 && np >= kBandMinPixels) {
+            for (uint32_t r = 0; r < 8; ++r)
+                for (uint32_t gb = r; gb < nb; gb += 8)
+                    for (uint32_t i = (uint32_t)((uint64_t)gb * np / nb); i < (uint32_t)((uint64_t)(gb + 1) * np / nb); ++i)
+                        bp.push_back(c->local_pixels[i]);
+        } else {
+            bp = c->local_pixels;
+        }
+        if ((s = upload(c, c->d_band_pixels, bp))) return s;
+    }
     size_t fb = (size_t)cam.width * cam.height * 16;
     HIPC(c, c->film.alloc(fb));
     HIPC(c, c->film_sq.alloc(fb));
@@ -1183,6 +1207,7 @@ uint32_t volTailPaths() {
     const char *e = std::getenv("PG_VOL_TAIL_PATHS");
     return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : (uint32_t)1 << 17;
 }
+
 
 // chunks of a volumetric pass: np pixels from pb, nl sample layers from sample_base
 struct VChunk {
@@ -1748,6 +1773,7 @@ static pg_status renderPass(Ctx *c, uint32_t spp, uint32_t sample_offset, int32_
     // are what a render runs; with kernel_timing they are timed as launched (pg_stats rays_ms /
     // shade_ms), so a one-lane calibration context measures the shipped kernels
     const bool fuseRays = !std::getenv("PG_NO_RAYS_FUSION");
+    const bool bands = cameraBands() > 0;
     const bool fuseShade = !c->has_env && !std::getenv("PG_NO_SHADE_FUSION");
     // chunks: whole sample layers over the local pixels when they fit, else pixel ranges
     const uint32_t layersPer = std::max<uint32_t>(1, want / npix);
@@ -1844,15 +1870,15 @@ static pg_status renderPass(Ctx *c, uint32_t spp, uint32_t sample_offset, int32_
         }
         l.b = 0;
         l.sorted = false;  // camera rays: their queue order is already coherent
-        l.bound = pg_camera_shard_count(l.n, 0);
+        l.bound = pg_camera_bound(pg_camera_banded(bands, l.np), l.np, l.nl);
         l.active = true;
         l.traced = false;
         l.chunk = nextChunk++;
         HIPC(c, hipStreamWaitEvent(l.stream, c->pass_start, 0));
         HIPC(c, hipMemsetAsync(l.counters.p, 0, (size_t)kBounceWords * (maxBounces + 1) * 4, l.stream));
         HIPC(c, hipMemsetAsync(l.tail_stats.p, 0, 24, l.stream));
-        pg_launch_camera(l.stream, g, pathView(&l), c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl,
-                         sample_offset + l.layer0, lqueue(l, l.q0.as<uint32_t>(), l.counters.as<uint32_t>()));
+        pg_launch_camera(l.stream, g, pathView(&l), c->d_band_pixels.as<uint32_t>(), l.pb, l.np, l.nl,
+                         sample_offset + l.layer0, lqueue(l, l.q0.as<uint32_t>(), l.counters.as<uint32_t>()), bands);
         return launchTrace(l, nullptr);
     };
     // film + record commit (in chunk order across lanes), statistics copy; then the next chunk
@@ -1863,7 +1889,7 @@ static pg_status renderPass(Ctx *c, uint32_t spp, uint32_t sample_offset, int32_
         HIPC(c, hipMemcpyAsync(l.h_stats, l.counters.p, (size_t)kBounceWords * l.b * 4, hipMemcpyDeviceToHost, l.stream));
         HIPC(c, hipMemcpyAsync(l.h_tail, l.tail_stats.p, 24, hipMemcpyDeviceToHost, l.stream));
         HIPC(c, hipStreamWaitEvent(l.stream, c->film_order, 0));
-        pg_launch_film(l.stream, g, sc, pv, c->d_local_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
+        pg_launch_film(l.stream, g, sc, pv, c->d_band_pixels.as<uint32_t>(), l.pb, l.np, l.nl, c->film.as<float4>(),
                        c->film_sq.as<float4>(), c->aov_albedo.as<float4>(), c->aov_normal.as<float4>());
         if (rec) {
             // every slot can emit at most max_vertices records; grow the buffer (lanes idle) when the

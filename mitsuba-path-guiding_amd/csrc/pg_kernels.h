@@ -111,14 +111,50 @@ struct Queue {
 // major) then the Morton code of the origin's cell in an 8^3 grid over the SD-tree cube (9 bits)
 #define PG_RAY_SORT_BINS 4096
 // camera layout: slot -> shard (slot >> 6) & 63, entry ((slot >> 12) << 6) | (slot & 63)
-__host__ __device__ inline uint32_t pg_queue_stride(uint32_t capacity) { return 64u * ((capacity + 4095u) / 4096u); }
+// shard capacity for `capacity` paths: 64 x ceil(capacity / 4096) for the interleaved camera map, plus what the
+// banded map (below) can add.  A band holds ceil(npix / 8) x nlayers <= n / 8 + 7 nlayers / 8 items and a shard
+// at most 64 x ceil(band / 512) <= n / 64 + 7 nlayers / 64 + 64 of them; bands are used only for >= 4096 pixels,
+// so nlayers <= capacity / 4096: the extra is <= 7 capacity / 2^18 + 64 entries
+__host__ __device__ inline uint32_t pg_queue_stride(uint32_t capacity) {
+    return 64u * ((capacity + 4095u) / 4096u + (uint32_t)(((uint64_t)capacity * 7u + (1u << 24) - 1u) >> 24) + 2u);
+}
 __host__ __device__ inline uint32_t pg_camera_shard_count(uint32_t n, uint32_t s) {
     int rem = (int)(n & 4095u) - 64 * (int)s;
     return 64u * (n >> 12) + (uint32_t)(rem < 0 ? 0 : rem > 64 ? 64 : rem);
 }
+// XCD-banded camera map (round 6, PG_CAMERA_BANDS): blocks b and b + 8 run on one XCD (MI355X_MICROARCH.md
+// §Workgroup dispatch) and every sharded launch gives block b shard b % 64, so shards s and s + 8 share an XCD's
+// L2 for the paths' whole lives.  The banded map deals the chunk's pixels in 8 contiguous bands (local pixel
+// order: whole 32 x 32 tiles), band r to the 8 shards r, r + 8, ..., r + 56, so one XCD traces and shades the
+// paths of one image region: their BVH nodes, triangles, materials and SD-tree cells are that region's.  Within
+// a band, item k (layer-major) goes to shard r + 8 ((k >> 6) & 7) at ((k >> 9) << 6) | (k & 63).  Chunks of
+// fewer than 4096 pixels keep the interleaved map (slot s -> shard (s >> 6) & 63).
+constexpr uint32_t kBandMinPixels = 4096;
+__host__ __device__ inline uint32_t pg_band_start(uint32_t r, uint32_t npix) {
+    return (uint32_t)(((uint64_t)r * npix + 7u) / 8u);
+}
+__host__ __device__ inline uint32_t pg_banded_shard_count(uint32_t npix, uint32_t nlayers, uint32_t s) {
+    const uint32_t r = s & 7u, j = s >> 3;
+    const uint32_t m = (pg_band_start(r + 1, npix) - pg_band_start(r, npix)) * nlayers;
+    const int rem = (int)(m & 511u) - 64 * (int)j;
+    return 64u * (m >> 9) + (uint32_t)(rem < 0 ? 0 : rem > 64 ? 64 : rem);
+}
+__host__ __device__ inline bool pg_camera_banded(bool bands, uint32_t npix) { return bands && npix >= kBandMinPixels; }
+__host__ __device__ inline uint32_t pg_camera_count(bool banded, uint32_t npix, uint32_t nlayers, uint32_t s) {
+    return banded ? pg_banded_shard_count(npix, nlayers, s) : pg_camera_shard_count(npix * nlayers, s);
+}
+// the largest camera shard of a chunk (the bound every later queue of the chunk stays under)
+inline uint32_t pg_camera_bound(bool banded, uint32_t npix, uint32_t nlayers) {
+    uint32_t b = 0;
+    for (uint32_t s = 0; s < 64; ++s) {
+        const uint32_t c = pg_camera_count(banded, npix, nlayers, s);
+        b = c > b ? c : b;
+    }
+    return b;
+}
 
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
-                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q);
+                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q, bool banded);
 // closest hit for the live queue, partitioned by the hit's material class: class c < PG_NUM_CLASSES
 // goes to class_queues[c] (shard s -> shard s); escaped paths are only counted, in
 // class_queues[PG_NUM_CLASSES].counts.  max_shard: upper bound of the largest shard count (sizes

@@ -36,10 +36,10 @@
 // camera rays: PerspectiveCamera::sampleRay (perspective.cpp:271-298) for (pixel, sample) slots
 __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint32_t *__restrict__ local_pixels,
                                                 uint32_t pix_begin, uint32_t npix, uint32_t nlayers,
-                                                uint32_t sample_base, Queue q) {
+                                                uint32_t sample_base, Queue q, bool banded) {
     uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = npix * nlayers;
-    if (slot < PG_QSHARDS) q.counts[slot] = pg_camera_shard_count(n, slot);
+    if (slot < PG_QSHARDS) q.counts[slot] = pg_camera_count(banded, npix, nlayers, slot);
     if (slot >= n) return;
     uint32_t layer = slot / npix, lp = slot - layer * npix;
     uint32_t pix = local_pixels[pix_begin + lp];
@@ -63,7 +63,14 @@ __global__ __launch_bounds__(256) void k_camera(GParams g, PathDev p, const uint
     // never shaded and k_film reads its L.
     stS(&p.rad[slot], make_float4(0.f, 0.f, 0.f, 0.f));
     stS(&p.pinfo[slot], make_uint4(pix, sample, 1u | (PF_EMITTED_QUERY << 16), 0u));
-    q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
+    if (banded) {  // pg_kernels.h pg_banded_shard_count: band r of the local pixels -> shards r, r + 8, ...
+        const uint32_t r = (uint32_t)(((uint64_t)lp * 8u) / npix);
+        const uint32_t b0 = pg_band_start(r, npix), m = pg_band_start(r + 1, npix) - b0;
+        const uint32_t k = layer * m + (lp - b0);
+        q.items[(r + 8u * ((k >> 6) & 7u)) * q.stride + (((k >> 9) << 6) | (k & 63u))] = slot;
+    } else {
+        q.items[((slot >> 6) & 63u) * q.stride + (((slot >> 12) << 6) | (slot & 63u))] = slot;
+    }
 }
 
 // BSDF::getAlbedo of the config BSDFs (diffuse.cpp:112, conductor.cpp:225, roughconductor.cpp:264,
@@ -1243,11 +1250,11 @@ size_t pg_stack_overflow_words(uint64_t max_threads) {
 uint64_t pg_trace_rays_threads(uint64_t n) { return (uint64_t)blocks(n, TRACE_BLOCK) * TRACE_BLOCK; }
 
 void pg_launch_camera(hipStream_t s, const GParams &g, const PathDev &p, const uint32_t *local_pixels,
-                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q) {
+                      uint32_t pix_begin, uint32_t npix, uint32_t nlayers, uint32_t sample_base, Queue q, bool banded) {
     uint64_t n = (uint64_t)npix * nlayers;
     if (!n) return;
     hipLaunchKernelGGL(k_camera, dim3(blocks(n, 256)), dim3(256), 0, s, g, p, local_pixels, pix_begin, npix, nlayers,
-                       sample_base, q);
+                       sample_base, q, pg_camera_banded(banded, npix));
 }
 // grid of a sharded launch: PG_QSHARDS x rows (rows capped for persistent grid-stride kernels)
 static inline dim3 shardGrid(uint32_t max_shard, uint32_t block, uint32_t max_rows) {

@@ -195,6 +195,13 @@ __device__ __forceinline__ uint32_t permuteXor8(uint32_t m, uint32_t x) {
     return m;
 }
 
+// PG_NODE_PK (round 6, default): a slot's near- and far-plane distances of one axis as one packed fma
+// (v_pk_fma_f32 computes two fp32 lanes per instruction at the VALU's full rate), the same fmas bit for bit
+#ifndef PG_NODE_PK
+#define PG_NODE_PK 1
+#endif
+typedef float pgf2 __attribute__((ext_vector_type(2)));
+
 // Traversal of the 8-wide BVH (after Ylitie, Karras & Laine 2017): the current node group
 // G = (child_base, hit bits 24..31 in octant order | imask bits 0..7) and triangle group
 // T = (tri_base, hit bits 0..23); one node is opened per step, its remaining siblings stay on the
@@ -246,11 +253,19 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
             uint32_t hitSlots = 0;
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
+#if PG_NODE_PK  // (near, far) of an axis as one packed fma (pg_trace.h traverse4)
+                const pgf2 tx = __builtin_elementwise_fma(pgf2{qbyte(nX0, nX1, s), qbyte(fX0, fX1, s)}, pgf2{ax, ax}, pgf2{bx, bx});
+                const pgf2 ty = __builtin_elementwise_fma(pgf2{qbyte(nY0, nY1, s), qbyte(fY0, fY1, s)}, pgf2{ay, ay}, pgf2{by, by});
+                const pgf2 tz = __builtin_elementwise_fma(pgf2{qbyte(nZ0, nZ1, s), qbyte(fZ0, fZ1, s)}, pgf2{az, az}, pgf2{bz, bz});
+                const float cmin = max3f(tx.x, ty.x, fmaxf(tz.x, tmin));
+                const float cmax = min3f(tx.y, ty.y, fminf(tz.y, tmax));
+#else
                 const float tnx = fmaf(qbyte(nX0, nX1, s), ax, bx), tfx = fmaf(qbyte(fX0, fX1, s), ax, bx);
                 const float tny = fmaf(qbyte(nY0, nY1, s), ay, by), tfy = fmaf(qbyte(fY0, fY1, s), ay, by);
                 const float tnz = fmaf(qbyte(nZ0, nZ1, s), az, bz), tfz = fmaf(qbyte(fZ0, fZ1, s), az, bz);
                 const float cmin = max3f(tnx, tny, fmaxf(tnz, tmin));
                 const float cmax = min3f(tfx, tfy, fminf(tfz, tmax));
+#endif
                 hitSlots |= (cmin <= cmax ? 1u : 0u) << s;
             }
             const uint32_t nodeHits = permuteXor8(hitSlots & imask, octinv) << 24;
@@ -355,6 +370,15 @@ __device__ __forceinline__ SlabRay slabRay(f3 o, f3 d) {
 // distances; the others pushed far to near), with the binary walk's while-while loop, postponed
 // leaves, tie rule and widened culling distance, so it returns the same hit.
 // LTOP: nodes [0, ntop) are read from `lnodes` (the breadth-first top levels, staged in LDS by the caller)
+// PG_NODE_NEARFAR (round 6, default): each axis's near and far planes chosen once per node by the ray's
+// direction sign (the lo plane is the near one for idir >= 0), so a slot's entry and exit distances are one
+// max3 / min3 each instead of a min and a max per axis.  The same distances and comparisons as the min/max
+// form bit for bit: for a non-empty slot lo <= hi and the padded addends keep their order, so min(lo-plane t,
+// hi-plane t) IS the near plane's t (empty slots are rejected by their ref either way).  The walk is VALU-bound
+// (~4 cycles x 1.0 M VALU wave-instructions per SIMD per k_rays launch against its ~4.8 M cycles)
+#ifndef PG_NODE_NEARFAR
+#define PG_NODE_NEARFAR 1
+#endif
 template <bool ANY, bool LTOP = false>
 __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, const float4 *__restrict__ tris, f3 o, f3 d,
                                           float tmin, float &tmax, uint32_t &hitTri, float &hu, float &hv,
@@ -364,6 +388,11 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
     const SlabRay sr = slabRay(o, d);
     const f3 idir = sr.idir, aLo = sr.addLo, aHi = sr.addHi;
     const float tslack = sr.tslack;
+#if PG_QNODE_QUANT && PG_NODE_NEARFAR
+    const bool negx = idir.x < 0.0f, negy = idir.y < 0.0f, negz = idir.z < 0.0f;
+    const f3 aN = mk(negx ? aHi.x : aLo.x, negy ? aHi.y : aLo.y, negz ? aHi.z : aLo.z);
+    const f3 aF = mk(negx ? aLo.x : aHi.x, negy ? aLo.y : aHi.y, negz ? aLo.z : aHi.z);
+#endif
     int sp = 0;
     int node = 0;
     int leaf = 0;
@@ -394,6 +423,50 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
             const float sx = __uint_as_float((e & 0xFFu) << 23) * idir.x;
             const float sy = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y;
             const float sz = __uint_as_float(((e >> 16) & 0xFFu) << 23) * idir.z;
+#if PG_NODE_NEARFAR
+            // |padding| per axis; near addend - it, far addend + it (the sign-carrying form below, unrolled)
+            const float ax = 2.38418579e-7f * fabsf(n0.x * idir.x);
+            const float ay = 2.38418579e-7f * fabsf(n0.y * idir.y);
+            const float az = 2.38418579e-7f * fabsf(n0.z * idir.z);
+#if !PG_NODE_PK
+            const float bnx = fmaf(n0.x, idir.x, aN.x) - ax, bfx = fmaf(n0.x, idir.x, aF.x) + ax;
+            const float bny = fmaf(n0.y, idir.y, aN.y) - ay, bfy = fmaf(n0.y, idir.y, aF.y) + ay;
+            const float bnz = fmaf(n0.z, idir.z, aN.z) - az, bfz = fmaf(n0.z, idir.z, aF.z) + az;
+#endif
+            const uint32_t wnx = __float_as_uint(negx ? q0.y : q0.x), wfx = __float_as_uint(negx ? q0.x : q0.y);
+            const uint32_t wny = __float_as_uint(negy ? q0.w : q0.z), wfy = __float_as_uint(negy ? q0.z : q0.w);
+            const uint32_t wnz = __float_as_uint(negz ? q1.y : q1.x), wfz = __float_as_uint(negz ? q1.x : q1.y);
+#if PG_NODE_PK
+            // (near, far) of an axis as one packed fma (v_pk_fma_f32: two lanes of fp32 per instruction)
+            const pgf2 sx2 = {sx, sx}, sy2 = {sy, sy}, sz2 = {sz, sz};
+            const pgf2 bx2 = __builtin_elementwise_fma(pgf2{n0.x, n0.x}, pgf2{idir.x, idir.x}, pgf2{aN.x, aF.x}) + pgf2{-ax, ax};
+            const pgf2 by2 = __builtin_elementwise_fma(pgf2{n0.y, n0.y}, pgf2{idir.y, idir.y}, pgf2{aN.y, aF.y}) + pgf2{-ay, ay};
+            const pgf2 bz2 = __builtin_elementwise_fma(pgf2{n0.z, n0.z}, pgf2{idir.z, idir.z}, pgf2{aN.z, aF.z}) + pgf2{-az, az};
+#define PG_QB(w, i) ((float)(((w) >> (8 * (i))) & 0xFFu))
+#define PG_Q4_SLOT(i, c)                                                                              \
+    {                                                                                                 \
+        const pgf2 tx = __builtin_elementwise_fma(pgf2{PG_QB(wnx, i), PG_QB(wfx, i)}, sx2, bx2);        \
+        const pgf2 ty = __builtin_elementwise_fma(pgf2{PG_QB(wny, i), PG_QB(wfy, i)}, sy2, by2);        \
+        const pgf2 tz = __builtin_elementwise_fma(pgf2{PG_QB(wnz, i), PG_QB(wfz, i)}, sz2, bz2);        \
+        const float cmin = fmaxf(fmaxf(tx.x, ty.x), fmaxf(tz.x, tmin));                               \
+        const float cmax = fminf(fminf(tx.y, ty.y), fminf(tz.y, tcull));                              \
+        r[i] = __float_as_int(rf.c);                                                                  \
+        k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
+    }
+#else
+#define PG_QB(w, i) ((float)(((w) >> (8 * (i))) & 0xFFu))
+#define PG_Q4_SLOT(i, c)                                                                              \
+    {                                                                                                 \
+        const float tnx = fmaf(PG_QB(wnx, i), sx, bnx), tfx = fmaf(PG_QB(wfx, i), sx, bfx);           \
+        const float tny = fmaf(PG_QB(wny, i), sy, bny), tfy = fmaf(PG_QB(wfy, i), sy, bfy);           \
+        const float tnz = fmaf(PG_QB(wnz, i), sz, bnz), tfz = fmaf(PG_QB(wfz, i), sz, bfz);           \
+        const float cmin = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));                                  \
+        const float cmax = fminf(fminf(tfx, tfy), fminf(tfz, tcull));                                 \
+        r[i] = __float_as_int(rf.c);                                                                  \
+        k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
+    }
+#endif
+#else
             const float px = copysignf(2.38418579e-7f * fabsf(n0.x * idir.x), idir.x);
             const float py = copysignf(2.38418579e-7f * fabsf(n0.y * idir.y), idir.y);
             const float pz = copysignf(2.38418579e-7f * fabsf(n0.z * idir.z), idir.z);
@@ -413,6 +486,7 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
         r[i] = __float_as_int(rf.c);                                                                  \
         k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
     }
+#endif
 #else
             const float4 *fp = (LTOP && node < ntop) ? lnodes + (size_t)PG_QNODE_F4 * node : np;
             const float4 lx = fp[0], hx = fp[1], ly = fp[2], hy = fp[3], lz = fp[4], hz = fp[5];

@@ -189,3 +189,111 @@ def sum_over_ranks(value, on_device):
     t = torch.tensor([float(value)], dtype=torch.float64, device=tdev)
     dist.all_reduce(t, op=dist.ReduceOp.SUM)
     return float(t.item())
+
+
+class Watchdog:
+    """Host-side deadlines for the multi-rank start-up (what the reference's RemoteWorker handshake and
+    StreamBackend error messages, sched_remote.h:50-236, give an operator: which worker is stuck where).
+
+    Each rank reports every stage it enters on stderr ("[bench rank r/W dev d] stage ..."), with the time
+    the previous one took, and -- once the process group is up -- in the group's key-value store.  A stage
+    that outlives its deadline ends the rank with exit status 3, after naming, from the store, every rank
+    whose last reported stage is not done (the stuck ranks); torch.distributed.run then stops the others.
+    No exec and no GPU call: a plain thread and os._exit."""
+
+    def __init__(self, rank, world, device=None, seconds=300.0, stream=None):
+        import sys
+        import threading
+        import time
+        self.rank, self.world, self.device = rank, world, device
+        self.seconds = float(seconds)
+        self.stream = stream or sys.stderr
+        self.store = None
+        self._lock = threading.Lock()
+        self._stage, self._t0, self._limit, self._n, self._coll = None, time.monotonic(), None, 0, False
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._watch, daemon=True)
+        self._thread.start()
+
+    def _say(self, msg):
+        self.stream.write(f"[bench rank {self.rank}/{self.world} dev {self.device}] {msg}\n")
+        self.stream.flush()
+
+    def attach_store(self):
+        """The process group's store (after init_process_group): stages become visible to every rank."""
+        try:
+            import torch.distributed as dist
+            self.store = dist.distributed_c10d._get_default_store()
+        except Exception:  # noqa: BLE001 -- diagnostics only
+            self.store = None
+        self._publish()
+
+    def _publish(self):
+        if self.store is not None and self._stage is not None:
+            try:
+                self.store.set(f"pg_bench_stage_{self.rank}", f"{self._n}:{int(self._coll)}:{self._stage}")
+            except Exception:  # noqa: BLE001
+                pass
+
+    def stage(self, name, seconds=None, collective=False):
+        """Enter stage `name` (`collective`: the rank waits there for the others, so a deadline in it blames
+        the ranks that are not in a collective)."""
+        import time
+        with self._lock:
+            now = time.monotonic()
+            if self._stage is not None:
+                self._say(f"{self._stage}: done in {now - self._t0:.2f} s")
+            self._stage, self._t0, self._coll = name, now, collective
+            self._n += 1
+            self._limit = self.seconds if seconds is None else float(seconds)
+        self._say(f"stage {name} (deadline {self._limit:.0f} s)")
+        self._publish()
+
+    def done(self):
+        self.stage("done", seconds=float("inf"), collective=True)
+        self._stop.set()
+
+    def others(self):
+        """{rank: (stage number, in a collective, last reported stage)} of the ranks (empty without a store)."""
+        out = {}
+        if self.store is None:
+            return out
+        import datetime
+        try:
+            self.store.set_timeout(datetime.timedelta(seconds=2))
+        except Exception:  # noqa: BLE001
+            pass
+        for r in range(self.world):
+            try:
+                n, coll, name = self.store.get(f"pg_bench_stage_{r}").decode().split(":", 2)
+                out[r] = (int(n), coll == "1", name)
+            except Exception:  # noqa: BLE001 -- a rank that never reported
+                out[r] = (0, False, "(no report: never joined the store)")
+        return out
+
+    def report(self):
+        """'stuck: ...; waiting: ...': ranks outside any collective are the stuck ones (the others wait for them);
+        if every unfinished rank is inside a collective, those in the earliest stage."""
+        ranks = {r: v for r, v in self.others().items() if v[2] != "done"}
+        if not ranks:
+            return "unknown (no store)"
+        out_of_coll = {r for r, v in ranks.items() if not v[1]}
+        if out_of_coll:
+            stuck_set = out_of_coll
+        else:
+            first = min(v[0] for v in ranks.values())
+            stuck_set = {r for r, v in ranks.items() if v[0] == first}
+        stuck = ", ".join(f"rank {r} in {v[2]!r}" for r, v in sorted(ranks.items()) if r in stuck_set)
+        wait = ", ".join(f"rank {r} in {v[2]!r}" for r, v in sorted(ranks.items()) if r not in stuck_set)
+        return f"stuck: {stuck}" + (f"; waiting: {wait}" if wait else "")
+
+    def _watch(self):
+        import os
+        import time
+        while not self._stop.wait(0.25):
+            with self._lock:
+                stage, t0, limit = self._stage, self._t0, self._limit
+            if stage is None or limit is None or time.monotonic() - t0 <= limit:
+                continue
+            self._say(f"DEADLINE: in stage {stage!r} for more than {limit:.0f} s; {self.report()}")
+            os._exit(3)

@@ -55,3 +55,26 @@ def test_cpu_share_is_stated():
             del os.environ["OMP_NUM_THREADS"]
         else:
             os.environ["OMP_NUM_THREADS"] = old
+
+
+def test_plumbing_check_reports_every_rank():
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--plumbing-check"], env=_env(), capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    for r in (0, 1):  # per rank: its stages, and the first collective's completion
+        assert f"[bench rank {r}/2 dev cpu] stage first collective" in out.stderr
+        assert f"[bench rank {r}/2 dev cpu] first collective complete" in out.stderr
+
+
+def test_deadline_names_the_stuck_rank():
+    """A rank that never reaches the first collective: the waiting rank's deadline ends the job with a non-zero
+    status and names the stuck rank and its stage (distributed.Watchdog), within a few deadlines."""
+    import time
+    t0 = time.time()
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--plumbing-check"],
+                         env=_env(PG_BENCH_STALL_RANK="1", PG_BENCH_DEADLINE="8"), capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode != 0
+    assert "DEADLINE" in out.stderr, out.stderr[-3000:]
+    assert "stuck: rank 1 in 'stall (test hook)'" in out.stderr, out.stderr[-3000:]
+    assert time.time() - t0 < 120
