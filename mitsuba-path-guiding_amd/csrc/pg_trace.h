@@ -198,7 +198,7 @@ __device__ __forceinline__ uint32_t permuteXor8(uint32_t m, uint32_t x) {
 // PG_NODE_PK (round 6, default): a slot's near- and far-plane distances of one axis as one packed fma
 // (v_pk_fma_f32 computes two fp32 lanes per instruction at the VALU's full rate), the same fmas bit for bit
 #ifndef PG_NODE_PK
-#define PG_NODE_PK 1
+#define PG_NODE_PK 0
 #endif
 typedef float pgf2 __attribute__((ext_vector_type(2)));
 
