@@ -775,6 +775,16 @@ struct SDView {
     int built;
 };
 
+// the jump-grid cell of position p (sdLookup's first step)
+PGD uint32_t sdJumpCell(const SDView &v, f3 p) {
+    const float qx = fminf(fmaxf((p.x - v.lo.x) / v.extent, 0.0f), 1.0f);
+    const float qy = fminf(fmaxf((p.y - v.lo.y) / v.extent, 0.0f), 1.0f);
+    const float qz = fminf(fmaxf((p.z - v.lo.z) / v.extent, 0.0f), 1.0f);
+    const int R = 1 << v.jumpBits;
+    const float fR = (float)R;
+    const int ix = min((int)(qx * fR), R - 1), iy = min((int)(qy * fR), R - 1), iz = min((int)(qz * fR), R - 1);
+    return ((uint32_t)iz * R + iy) * R + ix;
+}
 PGD uint32_t sdLookup(const SDView &v, f3 p) {
     float q[3];
     q[0] = fminf(fmaxf((p.x - v.lo.x) / v.extent, 0.0f), 1.0f);

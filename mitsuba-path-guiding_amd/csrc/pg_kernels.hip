@@ -309,6 +309,11 @@ __device__ __forceinline__ uint32_t rayOrderKey(const SDDev &sd, f3 o, f3 d) {
     return (oct << 9) | m;
 }
 
+// PG_SD_PREFETCH (round 6): shadeOne issues the guided lookup's jump-grid and leaf-record loads from the ray's
+// o + t d before the hit triangle and material resolve (the exact position decides; identical results)
+#ifndef PG_SD_PREFETCH
+#define PG_SD_PREFETCH 0
+#endif
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
 // MODEL >= 0 compiles only that BSDF model's code (material-class queues filled by k_trace);
 // CAN_GUIDE = false drops the SD-tree code for classes that are never guided (delta lobes).
@@ -382,9 +387,26 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         uint32_t tri = __float_as_uint(hv.y);
         if (tri == 0xFFFFFFFFu) break;  // escaped: no environment emitter
         const uint32_t key = rngKey(pix, g.seed);
-        f3 rd = xyz(ldS(&p.ray_d[slot]));
+        const float4 rd4 = ldS(&p.ray_d[slot]);
+        f3 rd = xyz(rd4);
+#if PG_SD_PREFETCH
+        // the guided lookup's jump-grid cell and leaf record, fetched from the ray's o + t d while the triangle and
+        // material gathers resolve; used only when the exact (barycentric) position lands in the same cell
+        uint32_t jCell = 0xFFFFFFFFu, jSpec = 0;
+        uint4 metaSpec = make_uint4(0, 0, 0, 0);
+        if (CAN_GUIDE && g.guiding && sd.built) {
+            const float4 ro = ldS(&p.ray_o[slot]);
+            const SDView sv0 = sdv(sd);
+            jCell = sdJumpCell(sv0, mk(ro.x + hv.x * rd.x, ro.y + hv.x * rd.y, ro.z + hv.x * rd.z));
+            jSpec = sd.jump[jCell];
+        }
+#endif
         Hit h;
         fetchHit(sc, tri, hv.z, hv.w, rd, h);
+#if PG_SD_PREFETCH
+        // the leaf's record behind the triangle loads (index 0, a valid record, where the cell holds a node)
+        if (CAN_GUIDE && g.guiding && sd.built) metaSpec = sd.meta[(jSpec & 0x80000000u) ? (jSpec & 0x7FFFFFFFu) : 0u];
+#endif
         WSET(0, depth);
         WSET(1, __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w));
         WSET3(2, h.p);
@@ -437,7 +459,14 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         const bool guide = CAN_GUIDE && g.guiding && sd.built && (M.type & ESmooth) && !(M.type & EDelta) && gRate < 1.0f;
         const SDView sv = sdv(sd);
         uint4 meta = make_uint4(0, 0, 0, 0);
+#if PG_SD_PREFETCH
+        if (guide) {
+            if ((jSpec & 0x80000000u) && sdJumpCell(sv, h.p) == jCell) meta = metaSpec;  // the same leaf
+            else meta = sd.meta[sdLookup(sv, h.p)];
+        }
+#else
         if (guide) meta = sd.meta[sdLookup(sv, h.p)];
+#endif
         // one-sample-MIS BSDF fraction of this vertex (pg_config.bsdf_fraction_bound; oracle guideFraction):
         // PG_FRACTION_LEARNED reads the leaf's learned fraction (meta.z; 0 = not learned yet)
         const float leafAlpha = __uint_as_float(meta.z);

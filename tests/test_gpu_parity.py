@@ -419,9 +419,10 @@ def test_image_parity_kitchen_unguided(pg, O):
 
 def test_image_parity_roughplastic(pg, O):
     """roughplastic blocks (GGX and Beckmann) in the Cornell box: unguided GPU vs oracle per-pixel
-    z-test, then the guided GPU image against the same unguided oracle (guiding is unbiased).  The
-    rough-transmittance tables come from different quadratures on each side (tests/test_rtrans.py),
-    so this is a statistical, not a bit-level, comparison."""
+    z-test, then the guided GPU image against the same unguided oracle (guiding is unbiased).  Both sides
+    integrate the rough-transmittance tables with the same quadrature (since round 5, tests/test_rtrans.py);
+    the two renders here use different random streams, so this is a statistical comparison (the same-stream
+    comparisons are test_bsdf_parity and tests/test_gpu_params.py)."""
     S = pg.scenes
     sc = S.cornell(64, 64, short_material=S.material("roughplastic", alpha=0.2, distribution="ggx",
                                                         diffuse_reflectance=(0.6, 0.3, 0.2)),
