@@ -417,7 +417,8 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
             e["avg_launch_ms_rocprof"] = round(cal / 1e6, 4)
             e["frac_rocprof"] = round(v[1] / v[2] / (cal / 1e9) / 1e9 / HBM_PEAK_GBS, 5)
         out[k] = e
-    return {"bound": "hbm", **headline_frac(achieved, per_launch, ms / max(launches, 1), out[dom]),
+    return {"bound": "hbm", **headline_frac(achieved, per_launch, ms / max(launches, 1), out[dom],
+                                            profiled_workload(a, integ.dev.cfg.world_size)),
             "traffic": traffic, "traffic_source": source,
             "traffic_over_algorithmic": round(traffic / per_launch, 3) if traffic else None,
             "kernel": dom, "dominant_by": "algorithmic bytes per pass (time shares under kernels)",
@@ -432,18 +433,29 @@ def kernel_roofline(pg, scene, integ, local, a, spp=32):
             "kernels": out}
 
 
-def headline_frac(achieved_hip, per_launch, avg_ms_hip, dom):
+def profiled_workload(a, world):
+    """Whether this run's calibration launches are the ones tools/profile.sh profiled: the default bench
+    workload of its scene on one rank (a shard of N ranks, --quick or another size launches smaller passes)."""
+    dflt = (1024, 1024) if a.scene == "smoke" else (1280, 720)
+    return (world == 1 and a.scene in ("ajar_door", "smoke") and not a.quick and (a.width, a.height) == dflt
+            and a.spp == 1024 and a.train == 5)
+
+
+def headline_frac(achieved_hip, per_launch, avg_ms_hip, dom, profiled=True):
     """The roofline's headline figures.  `achieved` / `frac` / `avg_launch_ms` take the dominant kernel's
     average launch duration from the committed rocprofv3 kernel trace of the same calibration launches
     (profiles/pmc_*_latest.json "calibration_avg_ns"), so they reproduce from profiles/ alone; this run's
     HIP-event duration on the driver's box is reported beside them (`frac_hip_events`), with the ratio of
-    the two boxes' durations named when they differ by more than 2 %.  Without a committed summary the HIP
-    events are the headline."""
+    the two boxes' durations named when they differ by more than 2 %.  Without a committed summary, or when
+    this run's calibration is not the profiled workload (`profiled`: a rank of an N-GPU shard, --quick, another
+    size), the HIP events are the headline."""
     cal_ms = dom.get("avg_launch_ms_rocprof")
     hip = {"frac_hip_events": round(achieved_hip / HBM_PEAK_GBS, 5), "avg_launch_ms_hip_events": round(avg_ms_hip, 4)}
-    if not cal_ms:
+    if not cal_ms or not profiled:
+        why = "HIP events, this run" + ("" if not cal_ms else
+                                        " (the committed profile is of the one-rank default workload, not this one)")
         return {"achieved": round(achieved_hip, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved_hip / HBM_PEAK_GBS, 5), "frac_source": "HIP events, this run",
+                "frac": round(achieved_hip / HBM_PEAK_GBS, 5), "frac_source": why,
                 "avg_launch_ms": round(avg_ms_hip, 4), **hip}
     achieved = per_launch / (cal_ms / 1e3) / 1e9
     out = {"achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -540,7 +552,8 @@ def wavefront_roofline(pg, scene, integ, local, a, spp):
     dom = max(kernels, key=lambda k: kernels[k][1])
     ms, nbytes, launches, _ = kernels[dom]
     achieved = nbytes / (ms / 1e3) / 1e9 if ms > 0 else 0.0
-    return {"bound": "hbm", **headline_frac(achieved, nbytes / max(launches, 1), ms / max(launches, 1), out[dom]),
+    return {"bound": "hbm", **headline_frac(achieved, nbytes / max(launches, 1), ms / max(launches, 1), out[dom],
+                                            profiled_workload(a, integ.dev.cfg.world_size)),
             "kernel": dom,
             "traffic": out[dom].get("traffic_bytes_per_launch"), "traffic_source": source,
             "traffic_over_algorithmic": out[dom].get("traffic_over_algorithmic"),

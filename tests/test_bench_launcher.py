@@ -78,3 +78,17 @@ def test_deadline_names_the_stuck_rank():
     assert "DEADLINE" in out.stderr, out.stderr[-3000:]
     assert "stuck: rank 1 in 'stall (test hook)'" in out.stderr, out.stderr[-3000:]
     assert time.time() - t0 < 120
+
+
+def test_headline_frac_source():
+    """The line's headline fraction uses the committed rocprof duration only for the profiled workload."""
+    sys.path.insert(0, ROOT)
+    import bench
+    dom = {"avg_launch_ms_rocprof": 2.0}
+    r = bench.headline_frac(2000.0, 4e9, 1.9, dom, profiled=True)
+    assert r["avg_launch_ms"] == 2.0 and abs(r["achieved"] - 2000.0) < 1e-6 and r["frac"] == 0.25
+    assert r["frac_hip_events"] == 0.25 and "box_difference" in r  # 1.9 vs 2.0 ms: 5 %
+    r = bench.headline_frac(500.0, 1e8, 0.2, dom, profiled=False)
+    assert r["avg_launch_ms"] == 0.2 and r["frac"] == round(500.0 / bench.HBM_PEAK_GBS, 5)
+    assert "not this one" in r["frac_source"]
+    assert bench.headline_frac(500.0, 1e8, 0.2, {}, profiled=True)["frac_source"] == "HIP events, this run"
