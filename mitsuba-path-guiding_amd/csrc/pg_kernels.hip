@@ -328,6 +328,17 @@ __device__ __forceinline__ void stPinfoZW(uint4 *p, uint32_t z, uint32_t w) {
     reinterpret_cast<uint2 *>(p)[1] = make_uint2(z, w);
 }
 
+#if PG_TRAV_STATS
+extern "C" int pg_debug_trav_stats(unsigned long long *out, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(pgTravStats), 8 * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(pgTravStats), z, 8 * 8) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 // Debug build only (PG_WATCH=1, make watch -> build/libpgamd_watch.so; tools/diverge_c3.py): shadeOne
 // logs every vertex of one (pixel, sample) path, the same record the oracle's Li writes (oracle.cpp
 // g_vtxLog): depth, original triangle, p, T, alpha, guided, mode, woPdf, weight, wo, L, NEE

@@ -61,6 +61,16 @@ __device__ __forceinline__ void stS(float4 *p, float4 a) { *p = a; }
 __device__ __forceinline__ void stS(uint4 *p, uint4 a) { *p = a; }
 #endif
 
+// Traversal statistics (debug build PG_TRAV_STATS=1, make travstats; tools/r06_trav_stats.py): per walk kind
+// (0 closest, 1 any hit) the walks, node visits, triangle tests and executed node-test iterations of whole waves
+#ifndef PG_TRAV_STATS
+#define PG_TRAV_STATS 0
+#endif
+#if PG_TRAV_STATS
+__device__ unsigned long long pgTravStats[8];
+#define PG_TSTAT(i, v) atomicAdd(&pgTravStats[i], (unsigned long long)(v))
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // BVH traversal.  Replaces ShapeKDTree::rayIntersect / rayIntersectHavran (skdtree.cpp:112-142,
 // sahkdtree3.h:178-308) with the same contract: closest t in [tmin, tmax] (any hit for shadow
@@ -221,8 +231,14 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
     uint2 T = make_uint2(0u, 0u);
     int sp = 0;
     bool found = false;
+#if PG_TRAV_STATS
+    PG_TSTAT(4, 1);
+#endif
     for (;;) {
         if (G.y > 0x00FFFFFFu) {
+#if PG_TRAV_STATS
+            PG_TSTAT(5, 1);
+#endif
             const int bit = 31 - __clz(G.y);
             const uint32_t slot = (uint32_t)(bit - 24) ^ octinv;
             const uint32_t ni = G.x + __popc(G.y & 0xFFu & ((1u << slot) - 1u));
@@ -282,6 +298,9 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
         while (T.y != 0) {
             const uint32_t tr = T.x + (uint32_t)(__ffs(T.y) - 1);
             T.y &= T.y - 1u;
+#if PG_TRAV_STATS
+            PG_TSTAT(6, 1);
+#endif
             float tt, bu, bv;
             if (triHit(tris, tr, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tr, hitTri)) {
                 found = true;
@@ -397,9 +416,15 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
     int node = 0;
     int leaf = 0;
     bool found = false;
+#if PG_TRAV_STATS
+    uint32_t nVisit = 0, nTri = 0;
+#endif
     while (node != DONE) {
         const float tcull = tmax * 1.000001f + tslack;
         while (node >= 0 && node != DONE) {
+#if PG_TRAV_STATS
+            nVisit++;
+#endif
             const float4 *np = nodes + (size_t)PG_QNODE_F4 * node;
             float k[4];
             int r[4];
@@ -525,11 +550,19 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
             if (!__any(leaf >= 0)) break;
         }
         while (leaf < 0) {
+#if PG_TRAV_STATS
+            nTri += (~(uint32_t)leaf) & 15u;
+#endif
             if (leafTest<ANY>(tris, leaf, o, d, tmin, tmax, hitTri, hu, hv, found)) return true;
             leaf = node;
             if (node < 0) node = sp > 0 ? (int)stk.get(--sp) : DONE;
         }
     }
+#if PG_TRAV_STATS
+    PG_TSTAT(0, 1);
+    PG_TSTAT(1, nVisit);
+    PG_TSTAT(2, nTri);
+#endif
     return found;
 }
 
