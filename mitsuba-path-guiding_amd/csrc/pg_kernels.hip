@@ -204,6 +204,73 @@ __device__ __forceinline__ void traceRows(const GParams &g, const SceneDev &sc, 
     }
 }
 
+// traceRows with persistent lanes (PG_TRACE_PERSIST, A/B, off): each wave takes a contiguous segment of its
+// shard's queue and runs the closest-hit walk one while-while round at a time (pg_trace.h Walk4); once at least
+// PG_TRACE_REFILL of its 64 lanes have finished their rays, they take the segment's next rays together (a lane
+// refill costs the whole wave the ray loads and the walk setup, so refills are batched, as k_volpath's).  A
+// finished lane writes its hit record and joins the class append of that round.  Every ray's walk is traverse4's,
+// so hits, films and trees are the grid-stride kernel's bit for bit (tests/test_gpu_parity.py, _configs, _params:
+// 90/90 with it on).  Measured slower (profiles/r06_persist/): C3 521-523 against 637 Mpaths/s, k_rays 31.6 against
+// 22.6 ms and k_shade_all 26.7 against 22.2 ms per calibration pass.  With 8 waves per SIMD the idle lanes of one
+// wave's while-while rounds are already covered by the other waves' issue, so the refill rounds only add their
+// ballots and setup; and the class queues come out in completion order instead of queue order, which costs the
+// shading kernel its ray coherence (6 waves per SIMD: 559-561, k_rays 27.0 ms).
+#ifndef PG_TRACE_PERSIST
+#define PG_TRACE_PERSIST 0
+#endif
+#ifndef PG_TRACE_REFILL
+#define PG_TRACE_REFILL 24
+#endif
+template <bool ENV>
+__device__ __forceinline__ void traceRowsPersist(const GParams &g, const SceneDev &sc, const PathDev &p, const Queue &q,
+                                                 const ClassQueues &cqs, float4 *first, uint32_t bid, uint32_t nblk,
+                                                 const TStack &stk) {
+    const uint32_t s = bid & (PG_QSHARDS - 1);
+    const uint32_t n = q.counts[s];
+    const uint32_t *items = q.items + (size_t)s * q.stride;
+    constexpr uint32_t kWavesPerBlock = TRACE_BLOCK / 64;
+    const uint32_t waves = (nblk / PG_QSHARDS) * kWavesPerBlock;
+    const uint32_t wv = (bid / PG_QSHARDS) * kWavesPerBlock + threadIdx.x / 64;
+    const uint32_t per = (n + waves - 1) / waves;
+    uint32_t cur = min(n, wv * per);
+    const uint32_t end = min(n, cur + per);
+    const int lane = threadIdx.x & 63;
+    bool active = false;
+    uint32_t slot = 0;
+    Walk4 w;
+    for (;;) {
+        const unsigned long long act = __ballot(active);
+        const uint32_t idle = 64u - (uint32_t)__popcll(act);
+        if (cur < end && (idle >= PG_TRACE_REFILL || act == 0)) {  // batched refill of the idle lanes
+            const uint32_t rank = (uint32_t)__popcll(~act & ((1ull << lane) - 1ull));
+            if (!active && cur + rank < end) {
+                slot = items[cur + rank];
+                const float4 o = ldS(&p.ray_o[slot]), d = ldS(&p.ray_d[slot]);
+                walk4Start(w, xyz(o), xyz(d), o.w, d.w);
+                active = true;
+            }
+            cur += min(idle, end - cur);
+        }
+        if (__ballot(active) == 0) break;  // the segment is done (a refill above found no ray left)
+        bool fin = false;
+        if (active) fin = walk4Round(w, sc.nodes, sc.tris, stk);
+        int cls = -1;
+        if (fin) {
+            const bool h = w.hitTri != 0xFFFFFFFFu;
+            float4 hr = make_float4(h ? w.tmax : 0.0f, __uint_as_float(h ? w.hitTri : 0xFFFFFFFFu), w.hu, w.hv);
+            if (first) first[slot] = hr;
+            if (ENV && !h) {
+                const f3 e = envEscapeRadiance(g, sc, p, slot, w.d);
+                hr = make_float4(e.x, hr.y, e.y, e.z);
+            }
+            stS(&p.hit[slot], hr);
+            cls = h ? (int)sc.tclass[w.hitTri] : PG_NUM_CLASSES;
+            active = false;
+        }
+        classAppend(cls, slot, cqs, s);
+    }
+}
+
 template <bool ENV>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                        float4 *first) {
@@ -283,8 +350,11 @@ __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_
             for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_TOP_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
             __syncthreads();
         }
-        traceRows<ENV, PG_RAYS_LDS_TOP != 0, PG_CLOSEST_WIDE != 0>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks,
-                                             threadStack(stack, p.stack_ovf), top, ntop);
+        if (PG_TRACE_PERSIST && !PG_RAYS_LDS_TOP && !PG_CLOSEST_WIDE && PG_BVH4 && PG_QNODE_QUANT)
+            traceRowsPersist<ENV>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks, threadStack(stack, p.stack_ovf));
+        else
+            traceRows<ENV, PG_RAYS_LDS_TOP != 0, PG_CLOSEST_WIDE != 0>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks,
+                                                 threadStack(stack, p.stack_ovf), top, ntop);
     }
 #else
     if (blockIdx.x < shadow_blocks)

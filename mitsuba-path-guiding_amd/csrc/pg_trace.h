@@ -566,6 +566,106 @@ __device__ __forceinline__ bool traverse4(const float4 *__restrict__ nodes, cons
     return found;
 }
 
+// ---- the 4-wide closest-hit walk as a resumable state (PG_TRACE_PERSIST, pg_kernels.hip traceRowsPersist) ----
+// The same per-ray constants, node test, sorting network, postponed leaf, tie rule and culling distance as
+// traverse4's default configuration (PG_QNODE_QUANT, PG_NODE_NEARFAR), split so a lane can run one round of
+// the while-while loop at a time: between rounds, lanes whose ray finished take a new ray, so the wave's lanes
+// stay busy instead of waiting for the round's longest ray.  Each ray's own sequence of node visits and leaf
+// tests is traverse4's, so it returns the same hit.
+struct Walk4 {
+    f3 o, d, idir, aN, aF;
+    float tmin, tmax, tslack, hu, hv;
+    uint32_t hitTri;
+    int node, leaf, sp;
+    bool negx, negy, negz;
+};
+__device__ __forceinline__ void walk4Start(Walk4 &w, f3 o, f3 d, float tmin, float tmax) {
+    const SlabRay sr = slabRay(o, d);
+    w.o = o;
+    w.d = d;
+    w.idir = sr.idir;
+    w.tslack = sr.tslack;
+    w.negx = sr.idir.x < 0.0f;
+    w.negy = sr.idir.y < 0.0f;
+    w.negz = sr.idir.z < 0.0f;
+    w.aN = mk(w.negx ? sr.addHi.x : sr.addLo.x, w.negy ? sr.addHi.y : sr.addLo.y, w.negz ? sr.addHi.z : sr.addLo.z);
+    w.aF = mk(w.negx ? sr.addLo.x : sr.addHi.x, w.negy ? sr.addLo.y : sr.addHi.y, w.negz ? sr.addLo.z : sr.addHi.z);
+    w.tmin = tmin;
+    w.tmax = tmax;
+    w.hitTri = 0xFFFFFFFFu;
+    w.hu = w.hv = 0.0f;
+    w.node = 0;
+    w.leaf = 0;
+    w.sp = 0;
+}
+// one round of traverse4's outer loop (the inner node loop until every lane of the round holds a leaf, then
+// the postponed leaves); returns true when the walk is over (w.hitTri = ~0: no hit)
+__device__ __forceinline__ bool walk4Round(Walk4 &w, const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                           const TStack &stk) {
+    const int DONE = 0x7fffffff;
+    const float INF = __builtin_huge_valf();
+    bool found = false;
+    const float tcull = w.tmax * 1.000001f + w.tslack;
+    while (w.node >= 0 && w.node != DONE) {
+        const float4 *np = nodes + (size_t)PG_QNODE_F4 * w.node;
+        const float4 n0 = np[0], rf = np[1], q0 = np[2], q1 = np[3];
+        const f3 idir = w.idir;
+        const uint32_t e = __float_as_uint(n0.w);
+        const float sx = __uint_as_float((e & 0xFFu) << 23) * idir.x;
+        const float sy = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y;
+        const float sz = __uint_as_float(((e >> 16) & 0xFFu) << 23) * idir.z;
+        const float ax = 2.38418579e-7f * fabsf(n0.x * idir.x);
+        const float ay = 2.38418579e-7f * fabsf(n0.y * idir.y);
+        const float az = 2.38418579e-7f * fabsf(n0.z * idir.z);
+        const float bnx = fmaf(n0.x, idir.x, w.aN.x) - ax, bfx = fmaf(n0.x, idir.x, w.aF.x) + ax;
+        const float bny = fmaf(n0.y, idir.y, w.aN.y) - ay, bfy = fmaf(n0.y, idir.y, w.aF.y) + ay;
+        const float bnz = fmaf(n0.z, idir.z, w.aN.z) - az, bfz = fmaf(n0.z, idir.z, w.aF.z) + az;
+        const uint32_t wnx = __float_as_uint(w.negx ? q0.y : q0.x), wfx = __float_as_uint(w.negx ? q0.x : q0.y);
+        const uint32_t wny = __float_as_uint(w.negy ? q0.w : q0.z), wfy = __float_as_uint(w.negy ? q0.z : q0.w);
+        const uint32_t wnz = __float_as_uint(w.negz ? q1.y : q1.x), wfz = __float_as_uint(w.negz ? q1.x : q1.y);
+        float k[4];
+        int r[4];
+#define PG_QB(w_, i) ((float)(((w_) >> (8 * (i))) & 0xFFu))
+#define PG_W4_SLOT(i, c)                                                                              \
+    {                                                                                                 \
+        const float tnx = fmaf(PG_QB(wnx, i), sx, bnx), tfx = fmaf(PG_QB(wfx, i), sx, bfx);           \
+        const float tny = fmaf(PG_QB(wny, i), sy, bny), tfy = fmaf(PG_QB(wfy, i), sy, bfy);           \
+        const float tnz = fmaf(PG_QB(wnz, i), sz, bnz), tfz = fmaf(PG_QB(wfz, i), sz, bfz);           \
+        const float cmin = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, w.tmin));                                \
+        const float cmax = fminf(fminf(tfx, tfy), fminf(tfz, tcull));                                 \
+        r[i] = __float_as_int(rf.c);                                                                  \
+        k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
+    }
+        PG_W4_SLOT(0, x) PG_W4_SLOT(1, y) PG_W4_SLOT(2, z) PG_W4_SLOT(3, w)
+#undef PG_W4_SLOT
+#undef PG_QB
+        cxch(k[0], r[0], k[1], r[1]);
+        cxch(k[2], r[2], k[3], r[3]);
+        cxch(k[0], r[0], k[2], r[2]);
+        cxch(k[1], r[1], k[3], r[3]);
+        cxch(k[1], r[1], k[2], r[2]);
+        if (k[0] == INF) {
+            w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+        } else {
+            w.node = r[0];
+            if (k[3] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[3]);
+            if (k[2] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[2]);
+            if (k[1] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[1]);
+        }
+        if (w.node < 0 && w.leaf >= 0) {
+            w.leaf = w.node;
+            w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+        }
+        if (!__any(w.leaf >= 0)) break;
+    }
+    while (w.leaf < 0) {
+        leafTest<false>(tris, w.leaf, w.o, w.d, w.tmin, w.tmax, w.hitTri, w.hu, w.hv, found);
+        w.leaf = w.node;
+        if (w.node < 0) w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+    }
+    return w.node == DONE;
+}
+
 // While-while traversal with postponed leaves (Aila & Laine 2009): lanes keep descending inner
 // nodes until every lane of the wave holds a leaf, then all lanes test triangles together.  This
 // keeps the 64-wide wave in one code path most of the time (if-if traversal measured 23 % lane
