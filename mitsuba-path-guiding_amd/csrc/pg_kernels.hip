@@ -271,6 +271,59 @@ __device__ __forceinline__ void traceRowsPersist(const GParams &g, const SceneDe
     }
 }
 
+// traceRows with two rays per lane (PG_TRACE_PAIR, A/B): a block's grid-stride step takes 2 x TRACE_BLOCK rows
+// of its shard, lane t rows base + t and base + TRACE_BLOCK + t, and walks both at once (pg_trace.h walk4Pair),
+// so each lane has two rays' node fetches in flight; both class appends follow in row order.  The second
+// walk's stack is a second LDS column block and a second band of the overflow ring (kPairRing rows on).
+#ifndef PG_TRACE_PAIR
+#define PG_TRACE_PAIR 0
+#endif
+constexpr uint32_t kPairRing = PG_QSTACK_DEPTH - LDS_STACK;
+template <bool ENV>
+__device__ __forceinline__ void finishWalk(const GParams &g, const SceneDev &sc, const PathDev &p, const Walk4 &w,
+                                           uint32_t slot, float4 *first, int &cls) {
+    const bool h = w.hitTri != 0xFFFFFFFFu;
+    float4 hr = make_float4(h ? w.tmax : 0.0f, __uint_as_float(h ? w.hitTri : 0xFFFFFFFFu), w.hu, w.hv);
+    if (first) first[slot] = hr;
+    if (ENV && !h) {
+        const f3 e = envEscapeRadiance(g, sc, p, slot, w.d);
+        hr = make_float4(e.x, hr.y, e.y, e.z);
+    }
+    stS(&p.hit[slot], hr);
+    cls = h ? (int)sc.tclass[w.hitTri] : PG_NUM_CLASSES;
+}
+template <bool ENV>
+__device__ __forceinline__ void traceRowsPair(const GParams &g, const SceneDev &sc, const PathDev &p, const Queue &q,
+                                              const ClassQueues &cqs, float4 *first, uint32_t bid, uint32_t nblk,
+                                              const TStack &sa, const TStack &sb) {
+    const uint32_t s = bid & (PG_QSHARDS - 1);
+    const uint32_t n = q.counts[s];
+    const uint32_t *items = q.items + (size_t)s * q.stride;
+    for (uint32_t base = (bid / PG_QSHARDS) * 2 * TRACE_BLOCK; base < n; base += nblk / PG_QSHARDS * 2 * TRACE_BLOCK) {
+        const uint32_t ia = base + threadIdx.x, ib = ia + TRACE_BLOCK;
+        uint32_t slotA = 0, slotB = 0;
+        Walk4 a, b;
+        walk4Idle(a);
+        walk4Idle(b);
+        if (ia < n) {
+            slotA = items[ia];
+            const float4 o = ldS(&p.ray_o[slotA]), d = ldS(&p.ray_d[slotA]);
+            walk4Start(a, xyz(o), xyz(d), o.w, d.w);
+        }
+        if (ib < n) {
+            slotB = items[ib];
+            const float4 o = ldS(&p.ray_o[slotB]), d = ldS(&p.ray_d[slotB]);
+            walk4Start(b, xyz(o), xyz(d), o.w, d.w);
+        }
+        walk4Pair(a, b, sc.nodes, sc.tris, sa, sb);
+        int ca = -1, cb = -1;
+        if (ia < n) finishWalk<ENV>(g, sc, p, a, slotA, first, ca);
+        if (ib < n) finishWalk<ENV>(g, sc, p, b, slotB, first, cb);
+        classAppend(ca, slotA, cqs, s);
+        classAppend(cb, slotB, cqs, s);
+    }
+}
+
 template <bool ENV>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                        float4 *first) {
@@ -336,7 +389,8 @@ template <bool ENV>
 #endif
 __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_RAYS_WAVES))) void k_rays(GParams g, SceneDev sc, PathDev p, Queue q, ClassQueues cqs,
                                                       Queue shq, uint32_t shadow_blocks) {
-    __shared__ uint32_t stack[2 * WIDE_LDS_STACK * TRACE_BLOCK];  // >= LDS_STACK words per thread
+    // >= LDS_STACK words per thread (twice that for the paired walks)
+    __shared__ uint32_t stack[(PG_TRACE_PAIR ? 2 : 1) * 2 * WIDE_LDS_STACK * TRACE_BLOCK];
 #if PG_RAYS_TRACE_FIRST  // the costlier closest-hit blocks dispatched first (profiles/r03zg_rays_order_ab)
     const uint32_t trace_blocks = gridDim.x - shadow_blocks;
     if (blockIdx.x >= trace_blocks) {
@@ -350,11 +404,15 @@ __global__ __launch_bounds__(TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(PG_
             for (uint32_t k = threadIdx.x; k < (uint32_t)ntop * PG_TOP_NODE_F4; k += TRACE_BLOCK) top[k] = sc.nodes[k];
             __syncthreads();
         }
-        if (PG_TRACE_PERSIST && !PG_RAYS_LDS_TOP && !PG_CLOSEST_WIDE && PG_BVH4 && PG_QNODE_QUANT)
-            traceRowsPersist<ENV>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks, threadStack(stack, p.stack_ovf));
+        const TStack sa = threadStack(stack, p.stack_ovf);
+        if (PG_TRACE_PAIR && !PG_RAYS_LDS_TOP && !PG_CLOSEST_WIDE && PG_BVH4 && PG_QNODE_QUANT)
+            traceRowsPair<ENV>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks, sa,
+                               TStack{sa.lds + LDS_STACK * TRACE_BLOCK, sa.ovf + (size_t)kPairRing * sa.ostride, sa.ostride});
+        else if (PG_TRACE_PERSIST && !PG_RAYS_LDS_TOP && !PG_CLOSEST_WIDE && PG_BVH4 && PG_QNODE_QUANT)
+            traceRowsPersist<ENV>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks, sa);
         else
             traceRows<ENV, PG_RAYS_LDS_TOP != 0, PG_CLOSEST_WIDE != 0>(g, sc, p, q, cqs, nullptr, blockIdx.x, trace_blocks,
-                                                 threadStack(stack, p.stack_ovf), top, ntop);
+                                                 sa, top, ntop);
     }
 #else
     if (blockIdx.x < shadow_blocks)
@@ -1353,7 +1411,8 @@ static inline uint32_t blocks(uint64_t n, uint32_t b) { return (uint32_t)((n + b
 size_t pg_stack_overflow_words(uint64_t max_threads) {
     if (max_threads == 0) max_threads = (uint64_t)TRACE_MAX_BLOCKS * TRACE_BLOCK;
     const size_t words = std::max<size_t>(std::max(STACK_DEPTH, PG_BVH4 ? PG_QSTACK_DEPTH : 0) - LDS_STACK,
-                                          2 * (STACK_DEPTH - WIDE_LDS_STACK));
+                                          2 * (STACK_DEPTH - WIDE_LDS_STACK)) +
+                         (PG_TRACE_PAIR ? kPairRing : 0);  // the paired walks' second band
     return words * max_threads;
 }
 // threads k_trace_rays launches for n rays: its overflow stride is gridDim.x * TRACE_BLOCK
@@ -1431,7 +1490,8 @@ void pg_launch_rays(hipStream_t s, const GParams &g, const SceneDev &sc, const P
     ClassQueues cq;
     for (int c = 0; c <= PG_NUM_CLASSES; ++c) cq.q[c] = class_queues[c];
     const uint32_t sb = max_shadow_shard ? shardGrid(max_shadow_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS).x : 0;
-    const uint32_t tb = max_shard ? shardGrid(max_shard, TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS).x : 0;
+    const uint32_t tb =
+        max_shard ? shardGrid(max_shard, (PG_TRACE_PAIR ? 2 : 1) * TRACE_BLOCK, TRACE_MAX_BLOCKS / PG_QSHARDS).x : 0;
     if (sb + tb == 0) return;
     if (tb == 0) {  // no trace rows: k_rays needs at least one trace block per shard to stay sharded
         hipLaunchKernelGGL(k_shadow, dim3(sb), dim3(TRACE_BLOCK), 0, s, sc, p, shq);

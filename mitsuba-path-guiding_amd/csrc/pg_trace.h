@@ -122,11 +122,10 @@ struct WStack {
 #ifndef PG_TRI_PRELOAD
 #define PG_TRI_PRELOAD 0
 #endif
-__device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
-                                       float &tt, float &bu, float &bv) {
-#if PG_TRIACCEL
+// triHitRow0: the test with the record's first row already loaded (the paired walk issues both rays' rows first)
+__device__ __forceinline__ bool triHitRow0(const float4 r0, const float4 *__restrict__ tris, uint32_t tr, f3 o, f3 d,
+                                           float tmin, float tmax, float &tt, float &bu, float &bv) {
 #pragma clang fp contract(off)
-    const float4 r0 = tris[3 * tr + 0];
 #if PG_TRI_PRELOAD
     const float4 r1 = tris[3 * tr + 1];
     const float2 r2 = *reinterpret_cast<const float2 *>(tris + 3 * tr + 2);
@@ -152,6 +151,11 @@ __device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t
     bu = u;
     bv = v;
     return true;
+}
+__device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
+                                       float &tt, float &bu, float &bv) {
+#if PG_TRIACCEL
+    return triHitRow0(tris[3 * tr + 0], tris, tr, o, d, tmin, tmax, tt, bu, bv);
 #else
     const float4 w0 = tris[3 * tr + 0];
     float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
@@ -598,33 +602,36 @@ __device__ __forceinline__ void walk4Start(Walk4 &w, f3 o, f3 d, float tmin, flo
     w.leaf = 0;
     w.sp = 0;
 }
-// one round of traverse4's outer loop (the inner node loop until every lane of the round holds a leaf, then
-// the postponed leaves); returns true when the walk is over (w.hitTri = ~0: no hit)
-__device__ __forceinline__ bool walk4Round(Walk4 &w, const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
-                                           const TStack &stk) {
+// one node of the 4-wide BVH (quantised: origin + exponents, child refs, near/far byte planes)
+struct QNode4 {
+    float4 n0, rf, q0, q1;
+};
+__device__ __forceinline__ QNode4 walk4Fetch(const float4 *__restrict__ nodes, int node) {
+    const float4 *np = nodes + (size_t)PG_QNODE_F4 * node;
+    return QNode4{np[0], np[1], np[2], np[3]};
+}
+// one node visit of traverse4 on fetched node data: w.node becomes the nearest hit child (the others pushed
+// far to near) or the popped entry, and a leaf is parked in w.leaf when that slot is free
+__device__ __forceinline__ void walk4Visit(Walk4 &w, const QNode4 &nd, float tcull, const TStack &stk) {
     const int DONE = 0x7fffffff;
     const float INF = __builtin_huge_valf();
-    bool found = false;
-    const float tcull = w.tmax * 1.000001f + w.tslack;
-    while (w.node >= 0 && w.node != DONE) {
-        const float4 *np = nodes + (size_t)PG_QNODE_F4 * w.node;
-        const float4 n0 = np[0], rf = np[1], q0 = np[2], q1 = np[3];
-        const f3 idir = w.idir;
-        const uint32_t e = __float_as_uint(n0.w);
-        const float sx = __uint_as_float((e & 0xFFu) << 23) * idir.x;
-        const float sy = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y;
-        const float sz = __uint_as_float(((e >> 16) & 0xFFu) << 23) * idir.z;
-        const float ax = 2.38418579e-7f * fabsf(n0.x * idir.x);
-        const float ay = 2.38418579e-7f * fabsf(n0.y * idir.y);
-        const float az = 2.38418579e-7f * fabsf(n0.z * idir.z);
-        const float bnx = fmaf(n0.x, idir.x, w.aN.x) - ax, bfx = fmaf(n0.x, idir.x, w.aF.x) + ax;
-        const float bny = fmaf(n0.y, idir.y, w.aN.y) - ay, bfy = fmaf(n0.y, idir.y, w.aF.y) + ay;
-        const float bnz = fmaf(n0.z, idir.z, w.aN.z) - az, bfz = fmaf(n0.z, idir.z, w.aF.z) + az;
-        const uint32_t wnx = __float_as_uint(w.negx ? q0.y : q0.x), wfx = __float_as_uint(w.negx ? q0.x : q0.y);
-        const uint32_t wny = __float_as_uint(w.negy ? q0.w : q0.z), wfy = __float_as_uint(w.negy ? q0.z : q0.w);
-        const uint32_t wnz = __float_as_uint(w.negz ? q1.y : q1.x), wfz = __float_as_uint(w.negz ? q1.x : q1.y);
-        float k[4];
-        int r[4];
+    const float4 n0 = nd.n0, rf = nd.rf, q0 = nd.q0, q1 = nd.q1;
+    const f3 idir = w.idir;
+    const uint32_t e = __float_as_uint(n0.w);
+    const float sx = __uint_as_float((e & 0xFFu) << 23) * idir.x;
+    const float sy = __uint_as_float(((e >> 8) & 0xFFu) << 23) * idir.y;
+    const float sz = __uint_as_float(((e >> 16) & 0xFFu) << 23) * idir.z;
+    const float ax = 2.38418579e-7f * fabsf(n0.x * idir.x);
+    const float ay = 2.38418579e-7f * fabsf(n0.y * idir.y);
+    const float az = 2.38418579e-7f * fabsf(n0.z * idir.z);
+    const float bnx = fmaf(n0.x, idir.x, w.aN.x) - ax, bfx = fmaf(n0.x, idir.x, w.aF.x) + ax;
+    const float bny = fmaf(n0.y, idir.y, w.aN.y) - ay, bfy = fmaf(n0.y, idir.y, w.aF.y) + ay;
+    const float bnz = fmaf(n0.z, idir.z, w.aN.z) - az, bfz = fmaf(n0.z, idir.z, w.aF.z) + az;
+    const uint32_t wnx = __float_as_uint(w.negx ? q0.y : q0.x), wfx = __float_as_uint(w.negx ? q0.x : q0.y);
+    const uint32_t wny = __float_as_uint(w.negy ? q0.w : q0.z), wfy = __float_as_uint(w.negy ? q0.z : q0.w);
+    const uint32_t wnz = __float_as_uint(w.negz ? q1.y : q1.x), wfz = __float_as_uint(w.negz ? q1.x : q1.y);
+    float k[4];
+    int r[4];
 #define PG_QB(w_, i) ((float)(((w_) >> (8 * (i))) & 0xFFu))
 #define PG_W4_SLOT(i, c)                                                                              \
     {                                                                                                 \
@@ -636,34 +643,106 @@ __device__ __forceinline__ bool walk4Round(Walk4 &w, const float4 *__restrict__ 
         r[i] = __float_as_int(rf.c);                                                                  \
         k[i] = (cmin <= cmax * kBoxRel && r[i] != PG_QNODE_EMPTY) ? cmin : INF;                       \
     }
-        PG_W4_SLOT(0, x) PG_W4_SLOT(1, y) PG_W4_SLOT(2, z) PG_W4_SLOT(3, w)
+    PG_W4_SLOT(0, x) PG_W4_SLOT(1, y) PG_W4_SLOT(2, z) PG_W4_SLOT(3, w)
 #undef PG_W4_SLOT
 #undef PG_QB
-        cxch(k[0], r[0], k[1], r[1]);
-        cxch(k[2], r[2], k[3], r[3]);
-        cxch(k[0], r[0], k[2], r[2]);
-        cxch(k[1], r[1], k[3], r[3]);
-        cxch(k[1], r[1], k[2], r[2]);
-        if (k[0] == INF) {
-            w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
-        } else {
-            w.node = r[0];
-            if (k[3] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[3]);
-            if (k[2] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[2]);
-            if (k[1] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[1]);
-        }
-        if (w.node < 0 && w.leaf >= 0) {
-            w.leaf = w.node;
-            w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
-        }
+    cxch(k[0], r[0], k[1], r[1]);
+    cxch(k[2], r[2], k[3], r[3]);
+    cxch(k[0], r[0], k[2], r[2]);
+    cxch(k[1], r[1], k[3], r[3]);
+    cxch(k[1], r[1], k[2], r[2]);
+    if (k[0] == INF) {
+        w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+    } else {
+        w.node = r[0];
+        if (k[3] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[3]);
+        if (k[2] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[2]);
+        if (k[1] != INF && w.sp < PG_QSTACK_DEPTH) stk.put(w.sp++, (uint32_t)r[1]);
+    }
+    if (w.node < 0 && w.leaf >= 0) {
+        w.leaf = w.node;
+        w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+    }
+}
+// after a parked leaf's triangles: the next parked entry (traverse4's leaf loop step)
+__device__ __forceinline__ void walk4NextLeaf(Walk4 &w, const TStack &stk) {
+    const int DONE = 0x7fffffff;
+    w.leaf = w.node;
+    if (w.node < 0) w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+}
+// one round of traverse4's outer loop (the inner node loop until every lane of the round holds a leaf, then
+// the postponed leaves); returns true when the walk is over (w.hitTri = ~0: no hit)
+__device__ __forceinline__ bool walk4Round(Walk4 &w, const float4 *__restrict__ nodes, const float4 *__restrict__ tris,
+                                           const TStack &stk) {
+    const int DONE = 0x7fffffff;
+    bool found = false;
+    const float tcull = w.tmax * 1.000001f + w.tslack;
+    while (w.node >= 0 && w.node != DONE) {
+        walk4Visit(w, walk4Fetch(nodes, w.node), tcull, stk);
         if (!__any(w.leaf >= 0)) break;
     }
     while (w.leaf < 0) {
         leafTest<false>(tris, w.leaf, w.o, w.d, w.tmin, w.tmax, w.hitTri, w.hu, w.hv, found);
-        w.leaf = w.node;
-        if (w.node < 0) w.node = w.sp > 0 ? (int)stk.get(--w.sp) : DONE;
+        walk4NextLeaf(w, stk);
     }
     return w.node == DONE;
+}
+
+// ---- two closest-hit walks per lane, interleaved (PG_TRACE_PAIR, pg_kernels.hip traceRowsPair) ----
+// Each step issues both rays' node (or triangle) loads before either ray's test, so a lane keeps two
+// dependent chains' requests in flight.  Each walk is traverse4's while-while walk (the inner loop runs
+// while a descending ray of the wave has a free leaf slot; then every parked leaf is tested), so the hits
+// are traverse4's: the closest (t, original index) over the visited boxes, whatever the visit order.
+__device__ __forceinline__ void walk4Idle(Walk4 &w) {
+    w.node = 0x7fffffff;
+    w.leaf = 0;
+    w.sp = 0;
+    w.hitTri = 0xFFFFFFFFu;
+    w.tmax = 0.0f;
+    w.hu = w.hv = 0.0f;
+}
+// one triangle of a parked leaf, its first row already loaded (triHitRow0: triHit's test bit for bit)
+__device__ __forceinline__ void walk4Tri(Walk4 &w, const float4 *__restrict__ tris, uint32_t tr, float4 r0) {
+    float tt, bu, bv;
+    if (triHitRow0(r0, tris, tr, w.o, w.d, w.tmin, w.tmax, tt, bu, bv) && acceptHit(tris, tt, w.tmax, tr, w.hitTri)) {
+        w.tmax = tt;
+        w.hitTri = tr;
+        w.hu = bu;
+        w.hv = bv;
+    }
+}
+__device__ __forceinline__ void walk4Pair(Walk4 &a, Walk4 &b, const float4 *__restrict__ nodes,
+                                          const float4 *__restrict__ tris, const TStack &sa, const TStack &sb) {
+    const int DONE = 0x7fffffff;
+    while (a.node != DONE || b.node != DONE) {
+        const float ca = a.tmax * 1.000001f + a.tslack, cb = b.tmax * 1.000001f + b.tslack;
+        for (;;) {
+            const bool da = a.node >= 0 && a.node != DONE, db = b.node >= 0 && b.node != DONE;
+            if (!(da || db)) break;
+            QNode4 na, nb;
+            if (da) na = walk4Fetch(nodes, a.node);
+            if (db) nb = walk4Fetch(nodes, b.node);
+            if (da) walk4Visit(a, na, ca, sa);
+            if (db) walk4Visit(b, nb, cb, sb);
+            const bool free = (a.leaf >= 0 && a.node >= 0 && a.node != DONE) || (b.leaf >= 0 && b.node >= 0 && b.node != DONE);
+            if (!__any(free)) break;
+        }
+        for (;;) {
+            const bool la = a.leaf < 0, lb = b.leaf < 0;
+            if (!(la || lb)) break;
+            const uint32_t ra = la ? ~(uint32_t)a.leaf : 0u, rb = lb ? ~(uint32_t)b.leaf : 0u;
+            const uint32_t fa = ra >> 4, na = ra & 15u, fb = rb >> 4, nb = rb & 15u;
+            for (uint32_t k = 0; k < na || k < nb; ++k) {
+                float4 ta, tb;
+                if (k < na) ta = tris[3 * (fa + k)];
+                if (k < nb) tb = tris[3 * (fb + k)];
+                if (k < na) walk4Tri(a, tris, fa + k, ta);
+                if (k < nb) walk4Tri(b, tris, fb + k, tb);
+            }
+            if (la) walk4NextLeaf(a, sa);
+            if (lb) walk4NextLeaf(b, sb);
+        }
+    }
 }
 
 // While-while traversal with postponed leaves (Aila & Laine 2009): lanes keep descending inner
