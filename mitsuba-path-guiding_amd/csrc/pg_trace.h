@@ -325,11 +325,39 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
 
 // Postponed-leaf triangle tests shared by the binary and the 4-wide closest-hit walks: every
 // triangle of leaf ref `leaf` (< 0: ~leaf = first << 4 | count) against the ray.
+// PG_LEAF_PAIRS (A/B): the triangles are taken two at a time with both first rows loaded before either
+// test (the tests, and so the accepted hit, stay in triangle order)
+#ifndef PG_LEAF_PAIRS
+#define PG_LEAF_PAIRS 1
+#endif
 template <bool ANY>
 __device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int leaf, f3 o, f3 d, float tmin,
                                          float &tmax, uint32_t &hitTri, float &hu, float &hv, bool &found) {
     const uint32_t lr = ~(uint32_t)leaf;
     const uint32_t first = lr >> 4, cnt = lr & 15u;
+#if PG_LEAF_PAIRS && PG_TRIACCEL
+    for (uint32_t k = 0; k < cnt; k += 2) {
+        const uint32_t ta = first + k, tb = first + min(k + 1, cnt - 1);
+        const float4 ra = tris[3 * ta], rb = tris[3 * tb];
+        float tt, bu, bv;
+        if (triHitRow0(ra, tris, ta, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, ta, hitTri)) {
+            found = true;
+            if (ANY) return true;
+            tmax = tt;
+            hitTri = ta;
+            hu = bu;
+            hv = bv;
+        }
+        if (k + 1 < cnt && triHitRow0(rb, tris, tb, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tb, hitTri)) {
+            found = true;
+            if (ANY) return true;
+            tmax = tt;
+            hitTri = tb;
+            hu = bu;
+            hv = bv;
+        }
+    }
+#else
     for (uint32_t k = 0; k < cnt; ++k) {
         const uint32_t tr = first + k;
         float tt, bu, bv;
@@ -343,6 +371,7 @@ __device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int le
             hv = bv;
         }
     }
+#endif
     return false;
 }
 
