@@ -216,6 +216,17 @@ __device__ __forceinline__ uint32_t permuteXor8(uint32_t m, uint32_t x) {
 #endif
 typedef float pgf2 __attribute__((ext_vector_type(2)));
 
+// PG_LEAF_PAIRS (default): leaf triangles are taken two at a time with both first rows loaded before either
+// test (the tests, and so the accepted hit, stay in triangle order): closest hits k_rays 22.1 against 22.5 ms
+// per calibration pass, C3 634-635 against 625-626 Mpaths/s (profiles/r06_leafpairs/)
+#ifndef PG_LEAF_PAIRS
+#define PG_LEAF_PAIRS 1
+#endif
+// the same for the 8-wide walk's triangle groups (shadow rays): k_rays 21.75 against 22.21 ms, C3 653 against
+// 649 Mpaths/s (profiles/r06_wideleafpairs/)
+#ifndef PG_WIDE_LEAF_PAIRS
+#define PG_WIDE_LEAF_PAIRS 1
+#endif
 // Traversal of the 8-wide BVH (after Ylitie, Karras & Laine 2017): the current node group
 // G = (child_base, hit bits 24..31 in octant order | imask bits 0..7) and triangle group
 // T = (tri_base, hit bits 0..23); one node is opened per step, its remaining siblings stay on the
@@ -299,6 +310,33 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
             G = make_uint2(__float_as_uint(n1.x), nodeHits | imask);
             T = make_uint2(__float_as_uint(n1.y), triHits);
         }
+#if PG_WIDE_LEAF_PAIRS && PG_TRIACCEL && !PG_TRAV_STATS
+        while (T.y != 0) {  // two triangles per step, both first rows loaded up front
+            const uint32_t ta = T.x + (uint32_t)(__ffs(T.y) - 1);
+            T.y &= T.y - 1u;
+            const bool two = T.y != 0;
+            const uint32_t tb = two ? T.x + (uint32_t)(__ffs(T.y) - 1) : ta;
+            if (two) T.y &= T.y - 1u;
+            const float4 ra = tris[3 * ta], rb = tris[3 * tb];
+            float tt, bu, bv;
+            if (triHitRow0(ra, tris, ta, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, ta, hitTri)) {
+                found = true;
+                if (ANY) return true;
+                tmax = tt;
+                hitTri = ta;
+                hu = bu;
+                hv = bv;
+            }
+            if (two && triHitRow0(rb, tris, tb, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tb, hitTri)) {
+                found = true;
+                if (ANY) return true;
+                tmax = tt;
+                hitTri = tb;
+                hu = bu;
+                hv = bv;
+            }
+        }
+#else
         while (T.y != 0) {
             const uint32_t tr = T.x + (uint32_t)(__ffs(T.y) - 1);
             T.y &= T.y - 1u;
@@ -315,6 +353,7 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
                 hv = bv;
             }
         }
+#endif
         if (G.y <= 0x00FFFFFFu) {
             if (sp == 0) break;
             G = stk.get(--sp);
@@ -325,11 +364,6 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
 
 // Postponed-leaf triangle tests shared by the binary and the 4-wide closest-hit walks: every
 // triangle of leaf ref `leaf` (< 0: ~leaf = first << 4 | count) against the ray.
-// PG_LEAF_PAIRS (A/B): the triangles are taken two at a time with both first rows loaded before either
-// test (the tests, and so the accepted hit, stay in triangle order)
-#ifndef PG_LEAF_PAIRS
-#define PG_LEAF_PAIRS 1
-#endif
 template <bool ANY>
 __device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int leaf, f3 o, f3 d, float tmin,
                                          float &tmax, uint32_t &hitTri, float &hu, float &hv, bool &found) {
