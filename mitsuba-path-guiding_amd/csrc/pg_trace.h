@@ -218,7 +218,8 @@ typedef float pgf2 __attribute__((ext_vector_type(2)));
 
 // PG_LEAF_PAIRS (default): leaf triangles are taken two at a time with both first rows loaded before either
 // test (the tests, and so the accepted hit, stay in triangle order): closest hits k_rays 22.1 against 22.5 ms
-// per calibration pass, C3 634-635 against 625-626 Mpaths/s (profiles/r06_leafpairs/)
+// per calibration pass, C3 634-635 against 625-626 Mpaths/s (profiles/r06_leafpairs/).  PG_LEAF_PAIRS=3 / 4 take
+// three / four per step: k_rays 22.13 / 22.42 against 22.02 ms (profiles/r06_leafgroup/)
 #ifndef PG_LEAF_PAIRS
 #define PG_LEAF_PAIRS 1
 #endif
@@ -370,25 +371,23 @@ __device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int le
     const uint32_t lr = ~(uint32_t)leaf;
     const uint32_t first = lr >> 4, cnt = lr & 15u;
 #if PG_LEAF_PAIRS && PG_TRIACCEL
-    for (uint32_t k = 0; k < cnt; k += 2) {
-        const uint32_t ta = first + k, tb = first + min(k + 1, cnt - 1);
-        const float4 ra = tris[3 * ta], rb = tris[3 * tb];
-        float tt, bu, bv;
-        if (triHitRow0(ra, tris, ta, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, ta, hitTri)) {
-            found = true;
-            if (ANY) return true;
-            tmax = tt;
-            hitTri = ta;
-            hu = bu;
-            hv = bv;
-        }
-        if (k + 1 < cnt && triHitRow0(rb, tris, tb, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tb, hitTri)) {
-            found = true;
-            if (ANY) return true;
-            tmax = tt;
-            hitTri = tb;
-            hu = bu;
-            hv = bv;
+    constexpr uint32_t G = PG_LEAF_PAIRS > 1 ? PG_LEAF_PAIRS : 2;  // triangles per step
+    for (uint32_t k = 0; k < cnt; k += G) {
+        float4 r[G];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) r[j] = tris[3 * (first + min(k + j, cnt - 1))];
+#pragma unroll
+        for (uint32_t j = 0; j < G; ++j) {
+            const uint32_t tr = first + k + j;
+            float tt, bu, bv;
+            if (k + j < cnt && triHitRow0(r[j], tris, tr, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, tr, hitTri)) {
+                found = true;
+                if (ANY) return true;
+                tmax = tt;
+                hitTri = tr;
+                hu = bu;
+                hv = bv;
+            }
         }
     }
 #else
