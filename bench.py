@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-quality", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="path chunks in flight (pg_config.path_lanes, 0 = 3)")
-    ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = auto: 2^26 for C3's final render on one GPU, else 2^25)")
+    ap.add_argument("--paths-in-flight", type=int, default=0, help="paths per chunk (0 = auto: C3's final render on one GPU in 12 chunks, else 2^25)")
     ap.add_argument("--exchange", default=None, choices=["allreduce", "allgather", "capi", "capi-allgather"],
                     help="postprogression exchange (N > 1): the library's own RCCL communicator (pg_comm_*, the C++ "
                          "adapter's path): all-reduce of the tree statistics ('capi', default with RCCL) or all-gather "
@@ -222,7 +222,7 @@ def main():
                     if capi_comm else D.make_exchange(on_dev, mode=a.exchange))
     else:
         exchange = None
-    # one progression for the final render (the device chunks it into 2^26-path chunks on one GPU, 3 in flight)
+    # one progression for the final render (the device cuts it into 12 chunks on one GPU, 3 in flight)
     Tracer = GuidedVolumetricPathTracer if vol else GuidedPathTracer
     if a.props is None:
         a.props = "{}" if vol else json.dumps(BENCH_GUIDING)

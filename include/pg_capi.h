@@ -195,8 +195,9 @@ typedef struct pg_config {
     int32_t rank;                 /* image-tile shard of this context */
     int32_t world_size;
     uint32_t tile_size;           /* 32 (Scene::setBlockSize default) */
-    uint32_t max_paths_in_flight; /* paths per chunk; 0 = auto: 2^25, or 2^26 for a path-integrator pass of at
-                                     least 3 x lanes x 2^26 paths (both capped to 70 % of free device memory) */
+    uint32_t max_paths_in_flight; /* paths per chunk; 0 = auto: 2^25, or four rounds of lanes (<= 2^27 paths a
+                                     chunk) for a path-integrator pass of at least 3 x lanes x 2^26 paths; both
+                                     capped to 70 % of the free device memory */
     int32_t gpu_depth_cap;        /* hard bounce cap on the device when max_depth < 0 (1024; the path integrator
                                      clamps it to 1098, and pg_create rejects a path-integrator max_depth above
                                      1097 with PG_ERR_INVALID; the volpath integrator honours both exactly) */

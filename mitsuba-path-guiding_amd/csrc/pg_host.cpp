@@ -1702,14 +1702,17 @@ static pg_status renderPass(Ctx *c, uint32_t spp, uint32_t sample_offset, int32_
     // 2^25 paths per chunk by default: bigger chunks mean fewer sparse tail bounces (each costs a
     // class-count readback) per path.  C3 with 3 lanes: 2^22 491, 2^23 552, 2^24 569, 2^25 587
     // Mpaths/s (DESIGN.md "Lanes"; round 2: 2^26 / 2^27 within noise, profiles/r02zq_chunk_ab).  Round 6, with
-    // the faster kernels: 2^26 650.2-650.5 against 633-644 (2^25) and 637-648 (2^27) (profiles/r06_chunk/), so a
-    // pass that holds at least three rounds of lanes of 2^26-path chunks (C3's final render on one GPU) takes
-    // 2^26; smaller passes (training, an N-GPU shard) keep 2^25 so every lane still gets several chunks.
+    // the faster kernels, C3's final render (943.7 M paths, 3 lanes) by chunk count: 30 (2^25) 633-644, 15
+    // (2^26) 646-650, 12 655-660, 9 (2^27) 637-648 Mpaths/s (profiles/r06_chunk/, r06_chunk2/).  So a pass of at
+    // least 3 x lanes x 2^26 paths is cut into four rounds of lanes (whole sample layers, at most 2^27 paths a
+    // chunk); smaller passes (training, an N-GPU shard) keep 2^25 so every lane still gets several chunks.
     // A non-recording lane holds ~6.6 GB per 2^25 paths; recording lanes add 32 training vertices per path.
     const uint64_t total = (uint64_t)npix * spp;
-    uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight
-                   : total >= 3ull * (uint64_t)c->nlanes * (1ull << 26) ? (1u << 26)
-                                                                        : (1u << 25);
+    uint32_t cap = c->cfg.max_paths_in_flight ? c->cfg.max_paths_in_flight : (1u << 25);
+    if (!c->cfg.max_paths_in_flight && total >= 3ull * (uint64_t)c->nlanes * (1ull << 26)) {
+        const uint32_t rounds = 4u * (uint32_t)c->nlanes;
+        cap = (uint32_t)std::min<uint64_t>((uint64_t)((spp + rounds - 1) / rounds) * npix, 1ull << 27);
+    }
     if (!c->cfg.max_paths_in_flight) {
         // ... but at most 70 % of the device memory this context can use for path state (free memory
         // plus what its lanes already hold), e.g. when several contexts or ranks share one GPU
