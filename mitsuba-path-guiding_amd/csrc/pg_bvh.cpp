@@ -477,9 +477,12 @@ static bool buildWide(const float *P, const uint32_t *I, uint32_t nt, uint32_t s
     out.wide_depth = wideDepth;
     if (wideDepth + 1 > stack_limit || order.size() != nt) return false;
     out.order.swap(order);
-    out.tris.assign(12 * (size_t)nt, 0.0f);
-    for (uint32_t k = 0; k < nt; ++k)
-        (PG_TRIACCEL ? triAccelRecord : woopRecord)(P, I, out.order[k], &out.tris[12 * (size_t)k]);
+    out.tris.assign(4 * (size_t)PG_TRI_F4(nt), 0.0f);
+    for (uint32_t k = 0; k < nt; ++k) {
+        float rec[12];
+        (PG_TRIACCEL ? triAccelRecord : woopRecord)(P, I, out.order[k], rec);
+        for (uint32_t r = 0; r < 3; ++r) std::memcpy(&out.tris[4 * (size_t)PG_TRI_ROW(k, r)], rec + 4 * r, 16);
+    }
     return true;
 }
 

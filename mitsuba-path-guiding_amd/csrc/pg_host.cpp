@@ -890,14 +890,14 @@ pg_status pg_upload_scene(void *ctx, const pg_scene_desc *d) {
     pgh::BvhOut bvh;
     if (!pgh::buildBvh(d->positions, d->indices, nt, kStackDepth, bvh))
         return fail(c, PG_ERR_INVALID, "pg_upload_scene: BVH deeper than the traversal stack");
-    std::vector<float> shade((size_t)20 * nt);
+    std::vector<float> shade((size_t)4 * PG_TRI_SHADE_STRIDE * nt, 0.0f);
     std::vector<uint8_t> tclass(nt), tcheap(nt);
     c->diffuse_null = true;
     for (uint32_t i = 0; i < d->num_materials; ++i)
         if (d->materials[i].type != PG_BSDF_DIFFUSE && d->materials[i].type != PG_BSDF_NULL) c->diffuse_null = false;
     for (uint32_t k = 0; k < nt; ++k) {
         uint32_t t = bvh.order[k];
-        packShade(&shade[20 * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
+        packShade(&shade[4 * PG_TRI_SHADE_STRIDE * (size_t)k], d->positions, d->normals, d->indices, t, triBits[t], t);
         tclass[k] = (uint8_t)materialClass(d->materials[triBits[t] & 0xFFFFu].type);
         // volumetric wavefront: surfaces whose interaction skips the shadow walk through media (delta
         // BSDFs) or ends the path at once (emitters: black in the scenes here) -- VolDev::tcheap

@@ -547,7 +547,7 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         if (CAN_GUIDE && g.guiding && sd.built) metaSpec = sd.meta[(jSpec & 0x80000000u) ? (jSpec & 0x7FFFFFFFu) : 0u];
 #endif
         WSET(0, depth);
-        WSET(1, __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w));
+        WSET(1, __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_STRIDE * tri + 2].w));
         WSET3(2, h.p);
         f3 Le = mk1(0.f);
         if (h.emitter >= 0 && dot(h.shN, -rd) > 0) {  // AreaLight::eval (area.cpp)
@@ -1007,7 +1007,7 @@ __global__ __launch_bounds__(256) void k_film(GParams g, SceneDev sc, PathDev p,
             const uint32_t tri = __float_as_uint(hv.y);
             f3 a = mk1(0.f), n = mk(0.f, 0.f, -1.f);  // Denoiser::Sample defaults (denoiser.h:12-16): escaped ray
             if (tri != 0xFFFFFFFFu) {
-                const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
+                const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_STRIDE * tri;
                 const float4 s1 = r[1], s3 = r[3], s4 = r[4];
                 const float b0 = 1 - hv.z - hv.w;
                 n = normalize(xyz(s3) * b0 + mk(s3.w, s4.x, s4.y) * hv.z + mk(s4.z, s4.w, s1.w) * hv.w);  // fetchHit's shN
@@ -1345,7 +1345,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace_rays(SceneDev sc, const f
         for (int k = 0; k < 16; ++k) q[k] = rec[k];
         return;
     }
-    uint32_t orig = hit ? __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri + 2].w) : 0xFFFFFFFFu;
+    uint32_t orig = hit ? __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_STRIDE * tri + 2].w) : 0xFFFFFFFFu;
     h[0] = hit ? tmax : 0.0f;
     h[1] = __uint_as_float(orig);
     h[2] = u;

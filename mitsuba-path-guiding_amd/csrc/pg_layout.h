@@ -113,6 +113,20 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 #ifndef PG_TRIACCEL
 #define PG_TRIACCEL 1
 #endif
+// PG_TRI_BLOCKED: the records in blocks of 8 BVH-order triangles (384 B, three 128-B lines): the 8 first rows,
+// then the 8 (row 1, row 2) pairs.  A leaf's first-row loads share one line, and rows 1-2, loaded only for
+// triangles whose plane distance passes, never straddle a line.  0: three consecutive rows per triangle.
+#ifndef PG_TRI_BLOCKED
+#define PG_TRI_BLOCKED 0
+#endif
+// float4 index of row r (0-2) of BVH-order triangle tr; PG_TRI_F4(nt) float4 for nt triangles
+#if PG_TRI_BLOCKED
+#define PG_TRI_ROW(tr, r) (24u * ((uint32_t)(tr) >> 3) + ((r) == 0 ? ((uint32_t)(tr) & 7u) : 7u + 2u * ((uint32_t)(tr) & 7u) + (r)))
+#define PG_TRI_F4(nt) (24u * (((uint32_t)(nt) + 7u) >> 3))
+#else
+#define PG_TRI_ROW(tr, r) (3u * (uint32_t)(tr) + (r))
+#define PG_TRI_F4(nt) (3u * (uint32_t)(nt))
+#endif
 
 // Volumetric flight order key (pg_volpath.hip flightKey): 0 = 16^3 cells (4096 sort bins), 1 = direction
 // octant + 8^3 cells (4096), 2 = 8^3 cells (512 bins: an eighth of the counting sort's per-tile atomics)
@@ -129,6 +143,11 @@ static_assert(sizeof(GMedium) == 128, "GMedium layout");
 //   [4] n1.y, n1.z, n2.x, n2.y
 // The same layout is used for the compact emitter-triangle array.
 #define PG_TRI_SHADE_F4 5
+// float4 per triangle in the BVH-order array (tshade); 8 pads a record to one 128-B line (A/B: half of the
+// 80-B records straddle two).  The emitter-triangle array keeps PG_TRI_SHADE_F4.
+#ifndef PG_TRI_SHADE_STRIDE
+#define PG_TRI_SHADE_STRIDE PG_TRI_SHADE_F4
+#endif
 
 // Binary BVH node for closest-hit rays (PG_BVH4 = 0 builds; 4 x float4 = 64 B):
 //   [0] c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y   [1] c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y
@@ -211,7 +230,10 @@ inline void pg_qnode_box(const float *node, int s, float lo[3], float hi[3]) {
 //   [2] qlo.x[8] qlo.y[8]   [3] qlo.z[8] qhi.x[8]   [4] qhi.y[8] qhi.z[8]   (uint8, slot order)
 // Slot s holds the child that rays of direction octant s (bit a = negative along axis a) should
 // visit first, so traversal orders hits by slot ^ (7 - octant) without sorting.
+// PG_WIDE_NODE_F4: float4 per node; 8 pads a node to one 128-B line (A/B: half of the 80-B nodes straddle two)
+#ifndef PG_WIDE_NODE_F4
 #define PG_WIDE_NODE_F4 5
+#endif
 #define PG_WIDE_LEAF_MAX 3
 
 // Material classes of the per-bounce shading queues (k_classify -> k_shade<MODEL>)

@@ -127,8 +127,8 @@ __device__ __forceinline__ bool triHitRow0(const float4 r0, const float4 *__rest
                                            float tmin, float tmax, float &tt, float &bu, float &bv) {
 #pragma clang fp contract(off)
 #if PG_TRI_PRELOAD
-    const float4 r1 = tris[3 * tr + 1];
-    const float2 r2 = *reinterpret_cast<const float2 *>(tris + 3 * tr + 2);
+    const float4 r1 = tris[PG_TRI_ROW(tr, 1)];
+    const float2 r2 = *reinterpret_cast<const float2 *>(tris + PG_TRI_ROW(tr, 2));
 #endif
     const uint32_t k = __float_as_uint(r0.w);  // projection axis; (u, v) = the next two axes cyclically
     const float ou = k == 0 ? o.y : (k == 1 ? o.z : o.x), ov = k == 0 ? o.z : (k == 1 ? o.x : o.y);
@@ -138,13 +138,13 @@ __device__ __forceinline__ bool triHitRow0(const float4 r0, const float4 *__rest
     tt = (r0.z - ou * r0.x - ov * r0.y - ok) / (du * r0.x + dv * r0.y + dk);
     if (!(tt >= tmin && tt <= tmax)) return false;
 #if !PG_TRI_PRELOAD
-    const float4 r1 = tris[3 * tr + 1];
+    const float4 r1 = tris[PG_TRI_ROW(tr, 1)];
 #endif
     const float hu = ou + tt * du - r1.x, hv = ov + tt * dv - r1.y;
     const float u = hv * r1.z + hu * r1.w;
     if (!(u >= 0.0f)) return false;
 #if !PG_TRI_PRELOAD
-    const float2 r2 = *reinterpret_cast<const float2 *>(tris + 3 * tr + 2);
+    const float2 r2 = *reinterpret_cast<const float2 *>(tris + PG_TRI_ROW(tr, 2));
 #endif
     const float v = hu * r2.x + hv * r2.y;
     if (!(v >= 0.0f && u + v <= 1.0f)) return false;
@@ -155,17 +155,17 @@ __device__ __forceinline__ bool triHitRow0(const float4 r0, const float4 *__rest
 __device__ __forceinline__ bool triHit(const float4 *__restrict__ tris, uint32_t tr, f3 o, f3 d, float tmin, float tmax,
                                        float &tt, float &bu, float &bv) {
 #if PG_TRIACCEL
-    return triHitRow0(tris[3 * tr + 0], tris, tr, o, d, tmin, tmax, tt, bu, bv);
+    return triHitRow0(tris[PG_TRI_ROW(tr, 0)], tris, tr, o, d, tmin, tmax, tt, bu, bv);
 #else
-    const float4 w0 = tris[3 * tr + 0];
+    const float4 w0 = tris[PG_TRI_ROW(tr, 0)];
     float dz = d.x * w0.x + d.y * w0.y + d.z * w0.z;
     float oz = w0.w - (o.x * w0.x + o.y * w0.y + o.z * w0.z);
     tt = oz / dz;
     if (!(tt >= tmin && tt <= tmax)) return false;
-    const float4 w1 = tris[3 * tr + 1];
+    const float4 w1 = tris[PG_TRI_ROW(tr, 1)];
     float a = (w1.w + o.x * w1.x + o.y * w1.y + o.z * w1.z) + tt * (d.x * w1.x + d.y * w1.y + d.z * w1.z);
     if (!(a >= 0.0f && a <= 1.0f)) return false;
-    const float4 w2 = tris[3 * tr + 2];
+    const float4 w2 = tris[PG_TRI_ROW(tr, 2)];
     float b = (w2.w + o.x * w2.x + o.y * w2.y + o.z * w2.z) + tt * (d.x * w2.x + d.y * w2.y + d.z * w2.z);
     if (!(b >= 0.0f && a + b <= 1.0f)) return false;
     bu = b;             // weight of p1
@@ -182,7 +182,7 @@ __device__ __forceinline__ bool acceptHit(const float4 *__restrict__ tris, float
                                           uint32_t hitTri) {
     if (tt < tmax || hitTri == 0xFFFFFFFFu) return true;
 #if PG_TRIACCEL
-    return __float_as_uint(tris[3 * tr + 2].z) < __float_as_uint(tris[3 * hitTri + 2].z);
+    return __float_as_uint(tris[PG_TRI_ROW(tr, 2)].z) < __float_as_uint(tris[PG_TRI_ROW(hitTri, 2)].z);
 #else
     return tr < hitTri;  // Woop rows carry no original id: BVH order (A/B builds only)
 #endif
@@ -318,7 +318,7 @@ __device__ __forceinline__ bool traverseWide(const float4 *__restrict__ nodes, c
             const bool two = T.y != 0;
             const uint32_t tb = two ? T.x + (uint32_t)(__ffs(T.y) - 1) : ta;
             if (two) T.y &= T.y - 1u;
-            const float4 ra = tris[3 * ta], rb = tris[3 * tb];
+            const float4 ra = tris[PG_TRI_ROW(ta, 0)], rb = tris[PG_TRI_ROW(tb, 0)];
             float tt, bu, bv;
             if (triHitRow0(ra, tris, ta, o, d, tmin, tmax, tt, bu, bv) && acceptHit(tris, tt, tmax, ta, hitTri)) {
                 found = true;
@@ -375,7 +375,7 @@ __device__ __forceinline__ bool leafTest(const float4 *__restrict__ tris, int le
     for (uint32_t k = 0; k < cnt; k += G) {
         float4 r[G];
 #pragma unroll
-        for (uint32_t j = 0; j < G; ++j) r[j] = tris[3 * (first + min(k + j, cnt - 1))];
+        for (uint32_t j = 0; j < G; ++j) r[j] = tris[PG_TRI_ROW(first + min(k + j, cnt - 1), 0)];
 #pragma unroll
         for (uint32_t j = 0; j < G; ++j) {
             const uint32_t tr = first + k + j;
@@ -796,8 +796,8 @@ __device__ __forceinline__ void walk4Pair(Walk4 &a, Walk4 &b, const float4 *__re
             const uint32_t fa = ra >> 4, na = ra & 15u, fb = rb >> 4, nb = rb & 15u;
             for (uint32_t k = 0; k < na || k < nb; ++k) {
                 float4 ta, tb;
-                if (k < na) ta = tris[3 * (fa + k)];
-                if (k < nb) tb = tris[3 * (fb + k)];
+                if (k < na) ta = tris[PG_TRI_ROW(fa + k, 0)];
+                if (k < nb) tb = tris[PG_TRI_ROW(fb + k, 0)];
                 if (k < na) walk4Tri(a, tris, fa + k, ta);
                 if (k < nb) walk4Tri(b, tris, fb + k, tb);
             }
@@ -990,7 +990,7 @@ struct Hit {
 };
 
 __device__ __forceinline__ void fetchHit(const SceneDev &sc, uint32_t tri, float u, float v, f3 rd, Hit &h) {
-    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
+    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_STRIDE * tri;
     float4 s0 = r[0], s1 = r[1], s2 = r[2], s3 = r[3], s4 = r[4];
     uint32_t bits = __float_as_uint(s0.w);
     h.mat = bits & 0xFFFFu;

@@ -428,7 +428,7 @@ __device__ __forceinline__ bool closestHit(const SceneDev &sc, f3 o, f3 d, float
     return traverse<false>(sc.nodes, sc.tris, o, d, tmin, t, tri, u, v, stk);
 }
 __device__ __forceinline__ uint32_t triBits(const SceneDev &sc, uint32_t tri) {
-    return __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_F4 * tri].w);
+    return __float_as_uint(sc.tshade[(size_t)PG_TRI_SHADE_STRIDE * tri].w);
 }
 __device__ __forceinline__ bool isNullMat(const SceneDev &sc, uint32_t bits) {
     return (sc.mats[bits & 0xFFFFu].type & ENull) != 0;
@@ -438,7 +438,7 @@ __device__ __forceinline__ int targetMedium(uint32_t tm, f3 d, f3 n) {
     return dot(d, n) > 0 ? (int)(tm >> 16) - 1 : (int)(tm & 0xFFFFu) - 1;
 }
 __device__ __forceinline__ f3 rawFaceNormal(const SceneDev &sc, uint32_t tri) {
-    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_F4 * tri;
+    const float4 *r = sc.tshade + (size_t)PG_TRI_SHADE_STRIDE * tri;
     const f3 p0 = xyz(r[0]), p1 = xyz(r[1]), p2 = xyz(r[2]);
     return normalize(cross(p1 - p0, p2 - p0));
 }

@@ -17,7 +17,9 @@ std::vector<float> g_P;
 std::vector<uint32_t> g_I;
 
 bool triHit(uint32_t tr, const float *o, const float *d, float tmin, float tmax, float &tt) {
-    const float *w = &g_bvh.tris[12 * (size_t)tr];
+    // the record's three rows, wherever PG_TRI_ROW puts them
+    float w[12];
+    for (uint32_t r = 0; r < 3; ++r) std::memcpy(&w[4 * r], &g_bvh.tris[4 * (size_t)PG_TRI_ROW(tr, r)], 16);
 #if PG_TRIACCEL
     // TriAccel::rayIntersect (triaccel.h:96-157), the device triHit's arithmetic (no contraction)
     uint32_t k;
@@ -47,8 +49,8 @@ bool accept(float tt, float tmax, uint32_t tr, uint32_t best) {
     if (tt < tmax || best == 0xFFFFFFFFu) return true;
 #if PG_TRIACCEL
     uint32_t a, b;
-    std::memcpy(&a, &g_bvh.tris[12 * (size_t)tr + 10], 4);
-    std::memcpy(&b, &g_bvh.tris[12 * (size_t)best + 10], 4);
+    std::memcpy(&a, &g_bvh.tris[4 * (size_t)PG_TRI_ROW(tr, 2) + 2], 4);
+    std::memcpy(&b, &g_bvh.tris[4 * (size_t)PG_TRI_ROW(best, 2) + 2], 4);
     return a < b;
 #else
     return tr < best;
