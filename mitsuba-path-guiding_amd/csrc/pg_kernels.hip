@@ -442,6 +442,11 @@ __device__ __forceinline__ uint32_t rayOrderKey(const SDDev &sd, f3 o, f3 d) {
 #ifndef PG_SD_PREFETCH
 #define PG_SD_PREFETCH 0
 #endif
+// PG_MAT_UNIFORM (round 6, A/B): shadeOne loads its material record once per distinct material of the wave, at a
+// wave-uniform address (readfirstlane waterfall), instead of as a per-lane gather
+#ifndef PG_MAT_UNIFORM
+#define PG_MAT_UNIFORM 0
+#endif
 // one bounce of Li for every queued path (progressive_path.cpp:149-306 + guiding)
 // MODEL >= 0 compiles only that BSDF model's code (material-class queues filled by k_trace);
 // CAN_GUIDE = false drops the SD-tree code for classes that are never guided (delta lobes).
@@ -583,7 +588,19 @@ __device__ __forceinline__ void shadeOne(const GParams &g, const SceneDev &sc, c
         }
         WSET3(5, T);
         if (depth > g.depth_cap) break;
+#if PG_MAT_UNIFORM
+        // one uniform (scalar-cache) load per distinct material of the wave instead of eight 16-B gathers per lane
+        GMat M;
+        for (;;) {
+            const uint32_t u = __builtin_amdgcn_readfirstlane(h.mat);
+            if (h.mat == u) {
+                M = mats[u];
+                break;
+            }
+        }
+#else
         const GMat M = mats[h.mat];
+#endif
         if ((flags & PF_EMITTED_QUERY) && h.emitter >= 0 && (!g.hide_emitters || (flags & PF_SCATTERED))) {
             L = L + T * Le;
             dirtyL = true;
